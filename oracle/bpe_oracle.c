@@ -1,0 +1,249 @@
+/*
+ * bpe_oracle.c — CPU restatement of the reference's BPE merge-training hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP engine in
+ * bpe-tokenizer_amd/csrc.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load liboracle.so; the product path (libbpe.so, the N-API addon, core.js) never does.
+ *
+ * Reference: beenotung/bpe-tokenizer v2.2.0, /root/reference/core.ts.
+ * Pinned against the reference's own outputs: tests/golden/small_cases.json and
+ * tests/golden/config2.json were produced by running core.ts itself (oracle/gen_golden.py), and
+ * tests/test_oracle_golden.py checks this file against every one of them.
+ *
+ * Corpus layout used here (and by the tests): flat int32 token ids (token.index, i.e. code point
+ * minus one — core.ts:149,189,316,485) plus int64 sample offsets: sample s is ids[off[s], off[s+1]).
+ * One sample == one element of BPETokenizer.corpus_in_code (core.ts:106,206).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------------------------------------
+ * Pair-count table: dense V*V uint32 when small, open-addressing hash otherwise.  Zero means
+ * "absent", exactly like `b_c_weights.get(b)` returning undefined (core.ts:280-284).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    int dense;
+    int64_t V;
+    uint32_t *cnt;      /* dense: V*V */
+    uint64_t *keys;     /* hash: key+1 (0 = empty) */
+    uint32_t *vals;
+    uint64_t cap;
+} pair_table;
+
+static int pt_init(pair_table *t, int64_t V, int64_t n_tokens) {
+    memset(t, 0, sizeof *t);
+    t->V = V;
+    if (V <= 8192) {
+        t->dense = 1;
+        t->cnt = (uint32_t *)calloc((size_t)(V * V > 0 ? V * V : 1), sizeof(uint32_t));
+        return t->cnt ? 0 : -1;
+    }
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)n_tokens * 2 + 16) cap <<= 1;
+    t->cap = cap;
+    t->keys = (uint64_t *)calloc(cap, sizeof(uint64_t));
+    t->vals = (uint32_t *)calloc(cap, sizeof(uint32_t));
+    return (t->keys && t->vals) ? 0 : -1;
+}
+
+static void pt_free(pair_table *t) {
+    free(t->cnt);
+    free(t->keys);
+    free(t->vals);
+}
+
+static inline uint32_t *pt_slot(pair_table *t, int32_t a, int32_t b) {
+    if (t->dense) return &t->cnt[(int64_t)a * t->V + b];
+    uint64_t key = ((uint64_t)(uint32_t)a << 32 | (uint32_t)b) + 1;
+    uint64_t h = key * 0x9E3779B97F4A7C15ull;
+    uint64_t i = (h >> 17) & (t->cap - 1);
+    for (;;) {
+        if (t->keys[i] == key) return &t->vals[i];
+        if (t->keys[i] == 0) {
+            t->keys[i] = key;
+            return &t->vals[i];
+        }
+        i = (i + 1) & (t->cap - 1);
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * findNextMerge — core.ts:247-326, restated literally (scan order, running argmax).
+ *   max_length: 0 == falsy == unlimited (core.ts:255,272); any other value filters
+ *               len16[a] + len16[b] <= max_length (core.ts:270-273).
+ *   min_weight: 0 == falsy -> 2 (`options?.min_weight || 2`, core.ts:256).
+ * Returns 0 and (a, b, W) when a merge exists, 1 when the reference returns null
+ * (core.ts:312-313), <0 on allocation failure.
+ * ------------------------------------------------------------------------------------------- */
+int oracle_find_next_merge(const int32_t *ids, const int64_t *off, int64_t n_samples,
+                           const int32_t *len16, int32_t n_tokens, int64_t max_length,
+                           int64_t min_weight, int32_t *out_a, int32_t *out_b, int64_t *out_w) {
+    if (min_weight == 0) min_weight = 2;                               /* core.ts:256 */
+    pair_table t;
+    if (pt_init(&t, n_tokens, off[n_samples])) return -1;
+    int32_t max_a = -1, max_b = -1;
+    int64_t max_c_index = -1, max_c_weight = 0;                        /* core.ts:260-263 */
+    for (int64_t s = 0; s < n_samples; s++) {                          /* core.ts:265 */
+        int32_t last_a = -1, a = -1;                                   /* core.ts:266-267 */
+        for (int64_t i = off[s]; i < off[s + 1]; i++) {                /* core.ts:268 */
+            int32_t b = ids[i];                                        /* core.ts:269 */
+            if (a >= 0 && (!max_length || (int64_t)len16[a] + len16[b] <= max_length)) {
+                uint32_t *slot = pt_slot(&t, a, b);                    /* core.ts:274-280 */
+                int64_t c_weight = *slot;
+                if (!c_weight) {                                       /* core.ts:281-283 */
+                    *slot = 1;
+                    c_weight = 1;
+                } else {
+                    if (a == b && last_a == a) {                       /* core.ts:285-290 */
+                        last_a = -1;
+                        a = b;
+                        continue;
+                    }
+                    c_weight++;                                        /* core.ts:291-292 */
+                    *slot = (uint32_t)c_weight;
+                }
+                int64_t c_index = (int64_t)a + b;                      /* core.ts:294 */
+                if (!max_c_weight || c_weight > max_c_weight ||        /* core.ts:296-305 */
+                    (c_weight == max_c_weight && c_index < max_c_index)) {
+                    max_a = a;
+                    max_b = b;
+                    max_c_weight = c_weight;
+                    max_c_index = c_index;
+                }
+            }
+            last_a = a;                                                /* core.ts:307-308 */
+            a = b;
+        }
+    }
+    pt_free(&t);
+    if (!max_c_weight) return 1;                                       /* core.ts:312 */
+    if (max_c_weight < min_weight) return 1;                           /* core.ts:313 */
+    *out_a = max_a;
+    *out_b = max_b;
+    *out_w = max_c_weight;
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * applyMerge corpus rewrite — core.ts:356-359: `sample.replaceAll(a.code + b.code, c.code)`,
+ * i.e. leftmost non-overlapping replacement of the token bigram (a, b) by c in every sample.
+ * Rewrites in place, updates off[], returns the number of replacements.
+ * ------------------------------------------------------------------------------------------- */
+int64_t oracle_apply_merge(int32_t *ids, int64_t *off, int64_t n_samples, int32_t a, int32_t b,
+                           int32_t c) {
+    int64_t w = 0, o = 0;
+    for (int64_t s = 0; s < n_samples; s++) {
+        int64_t beg = off[s], end = off[s + 1];
+        off[s] = o;
+        int64_t i = beg;
+        while (i < end) {
+            if (i + 1 < end && ids[i] == a && ids[i + 1] == b) {
+                ids[o++] = c;
+                i += 2;
+                w++;
+            } else {
+                ids[o++] = ids[i++];
+            }
+        }
+    }
+    off[n_samples] = o;
+    return w;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * mergeUntil — core.ts:365-383.  max_iterations 0 == falsy == unlimited (core.ts:376).
+ * New token index = current token-table length (core.ts:315), UTF-16 length of its chars =
+ * len16[a] + len16[b] (core.ts:318).  len16 must have room for n_tokens + merges entries.
+ * Writes (a, b, W) triples to out_abw (capacity `cap` triples); returns the merge count.
+ * ------------------------------------------------------------------------------------------- */
+int64_t oracle_merge_until(int32_t *ids, int64_t *off, int64_t n_samples, int32_t *len16,
+                           int32_t n_tokens, int64_t max_length, int64_t min_weight,
+                           int64_t max_iterations, int64_t *out_abw, int64_t cap) {
+    int64_t n = 0;
+    for (int64_t it = 1; !max_iterations || it <= max_iterations; it++) {
+        int32_t a, b;
+        int64_t w;
+        int rc = oracle_find_next_merge(ids, off, n_samples, len16, n_tokens, max_length,
+                                        min_weight, &a, &b, &w);
+        if (rc != 0) break;
+        int32_t c = n_tokens++;
+        len16[c] = len16[a] + len16[b];
+        oracle_apply_merge(ids, off, n_samples, a, b, c);
+        if (n < cap) {
+            out_abw[3 * n] = a;
+            out_abw[3 * n + 1] = b;
+            out_abw[3 * n + 2] = w;
+        }
+        n++;
+    }
+    return n;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Per-shard pair-count export (for the multi-rank exchange tests): counts every counted pair of
+ * the shard exactly as findNextMerge does (core.ts:265-293, including the run-skip rule and the
+ * max_length filter), and reports, per pair, the count and the position (index into ids) of its
+ * last counted occurrence.  Output arrays have capacity `cap` entries; returns the number of
+ * distinct pairs (or -1 if cap is too small).
+ * ------------------------------------------------------------------------------------------- */
+int64_t oracle_count_pairs(const int32_t *ids, const int64_t *off, int64_t n_samples,
+                           const int32_t *len16, int32_t n_tokens, int64_t max_length,
+                           int32_t *pa, int32_t *pb, int64_t *pcount, int64_t *plast, int64_t cap) {
+    int64_t V = n_tokens;
+    int64_t *cnt = (int64_t *)calloc((size_t)(V * V > 0 ? V * V : 1), sizeof(int64_t));
+    int64_t *last = (int64_t *)malloc((size_t)(V * V > 0 ? V * V : 1) * sizeof(int64_t));
+    if (!cnt || !last) {
+        free(cnt);
+        free(last);
+        return -2;
+    }
+    for (int64_t s = 0; s < n_samples; s++) {
+        int32_t last_a = -1, a = -1;
+        for (int64_t i = off[s]; i < off[s + 1]; i++) {
+            int32_t b = ids[i];
+            if (a >= 0 && (!max_length || (int64_t)len16[a] + len16[b] <= max_length)) {
+                int64_t k = (int64_t)a * V + b;
+                if (cnt[k] && a == b && last_a == a) {
+                    last_a = -1;
+                    a = b;
+                    continue;
+                }
+                cnt[k]++;
+                last[k] = i - 1;
+            }
+            last_a = a;
+            a = b;
+        }
+    }
+    int64_t n = 0;
+    for (int64_t k = 0; k < V * V; k++) {
+        if (!cnt[k]) continue;
+        if (n >= cap) {
+            n = -1;
+            break;
+        }
+        pa[n] = (int32_t)(k / V);
+        pb[n] = (int32_t)(k % V);
+        pcount[n] = cnt[k];
+        plast[n] = last[k];
+        n++;
+    }
+    free(cnt);
+    free(last);
+    return n;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Synthetic corpus generator shared with the bench: xorshift32
+ * (x ^= x<<13; x ^= x>>17; x ^= x<<5), char = base + floor(x * A / 2^32).
+ * ------------------------------------------------------------------------------------------- */
+void oracle_xorshift_corpus(uint32_t seed, uint32_t A, uint32_t base, uint8_t *out, int64_t n) {
+    uint32_t x = seed;
+    for (int64_t i = 0; i < n; i++) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        out[i] = (uint8_t)(base + (uint32_t)(((uint64_t)x * A) >> 32));
+    }
+}

@@ -1,0 +1,172 @@
+"""ctypes wrapper over liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.  The
+product path (libbpe.so + bpe-tokenizer_amd host code) never does.
+
+`Corpus` mirrors the host-side bookkeeping of the reference's `addToCorpus` (core.ts:182-207):
+code point -> token index in first-appearance order across calls, UTF-16 length per token
+(`chars.length`, used by the max_length filter core.ts:270-273).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liboracle.so')
+_lib = None
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.oracle_find_next_merge.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int32,
+                                             ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p]
+        L.oracle_find_next_merge.restype = ctypes.c_int
+        L.oracle_apply_merge.argtypes = [i32p, i64p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32]
+        L.oracle_apply_merge.restype = ctypes.c_int64
+        L.oracle_merge_until.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int32,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, i64p,
+                                         ctypes.c_int64]
+        L.oracle_merge_until.restype = ctypes.c_int64
+        L.oracle_count_pairs.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int32,
+                                         ctypes.c_int64, i32p, i32p, i64p, i64p, ctypes.c_int64]
+        L.oracle_count_pairs.restype = ctypes.c_int64
+        L.oracle_xorshift_corpus.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_xorshift_corpus.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(arr, ct):
+    return arr.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def js_truthy_int(v):
+    """JS `x || 0` for the numeric options the tests use (None/0 -> 0)."""
+    return 0 if v is None else int(v)
+
+
+class Corpus:
+    """Token ids + sample offsets, with the reference's char->index bookkeeping."""
+
+    def __init__(self):
+        self.char_to_index = {}
+        self.chars = []          # token.chars per index (chars only for base tokens)
+        self.len16 = []
+        self.samples = []        # list of int32 arrays
+
+    def add(self, content):
+        ids = []
+        for ch in content:                                   # core.ts:185 (code points)
+            idx = self.char_to_index.get(ch)
+            if idx is None:
+                idx = len(self.chars)
+                self.char_to_index[ch] = idx
+                self.chars.append(ch)
+                self.len16.append(2 if ord(ch) > 0xFFFF else 1)
+            ids.append(idx)
+        self.samples.append(np.asarray(ids, dtype=np.int32))
+
+    def add_ids(self, ids):
+        self.samples.append(np.asarray(ids, dtype=np.int32))
+
+    def flat(self):
+        off = np.zeros(len(self.samples) + 1, dtype=np.int64)
+        for i, s in enumerate(self.samples):
+            off[i + 1] = off[i] + len(s)
+        ids = np.concatenate(self.samples) if self.samples else np.zeros(0, np.int32)
+        return np.ascontiguousarray(ids, dtype=np.int32), off
+
+
+class OracleState:
+    """Flat corpus state driven through the C restatement."""
+
+    def __init__(self, ids, off, len16, n_tokens, extra=1 << 16):
+        self.ids = np.array(ids, dtype=np.int32, copy=True)
+        if self.ids.size == 0:
+            self.ids = np.zeros(1, np.int32)[:0].copy()
+        self.off = np.array(off, dtype=np.int64, copy=True)
+        self.len16 = np.zeros(n_tokens + extra, dtype=np.int32)
+        self.len16[:len(len16)] = len16
+        self.n_tokens = n_tokens
+
+    @classmethod
+    def from_corpus(cls, c, extra=1 << 16):
+        ids, off = c.flat()
+        return cls(ids, off, c.len16, len(c.chars), extra)
+
+    def find_next_merge(self, max_length=None, min_weight=None):
+        a = ctypes.c_int32()
+        b = ctypes.c_int32()
+        w = ctypes.c_int64()
+        buf = self.ids if self.ids.size else np.zeros(1, np.int32)
+        rc = lib().oracle_find_next_merge(_p(buf, ctypes.c_int32), _p(self.off, ctypes.c_int64),
+                                          len(self.off) - 1, _p(self.len16, ctypes.c_int32),
+                                          self.n_tokens, js_truthy_int(max_length),
+                                          js_truthy_int(min_weight), ctypes.byref(a),
+                                          ctypes.byref(b), ctypes.byref(w))
+        if rc < 0:
+            raise MemoryError('oracle allocation failed')
+        return None if rc == 1 else (a.value, b.value, w.value)
+
+    def apply_merge(self, a, b, c=None):
+        if c is None:
+            c = self.n_tokens
+        if c >= self.n_tokens:
+            self.len16[c] = self.len16[a] + self.len16[b]
+            self.n_tokens = c + 1
+        buf = self.ids if self.ids.size else np.zeros(1, np.int32)
+        w = lib().oracle_apply_merge(_p(buf, ctypes.c_int32), _p(self.off, ctypes.c_int64),
+                                     len(self.off) - 1, a, b, c)
+        self.ids = self.ids[:self.off[-1]]
+        return w
+
+    def merge_until(self, max_length=None, min_weight=None, max_iterations=None):
+        merges = []
+        it = 1
+        while not max_iterations or it <= max_iterations:
+            m = self.find_next_merge(max_length, min_weight)
+            if m is None:
+                break
+            self.apply_merge(m[0], m[1])
+            merges.append(m)
+            it += 1
+        return merges
+
+    def samples(self):
+        return [self.ids[self.off[i]:self.off[i + 1]].tolist() for i in range(len(self.off) - 1)]
+
+    def count_pairs(self, max_length=None):
+        cap = max(16, self.n_tokens * self.n_tokens)
+        pa = np.zeros(cap, np.int32)
+        pb = np.zeros(cap, np.int32)
+        pc = np.zeros(cap, np.int64)
+        pl = np.zeros(cap, np.int64)
+        buf = self.ids if self.ids.size else np.zeros(1, np.int32)
+        n = lib().oracle_count_pairs(_p(buf, ctypes.c_int32), _p(self.off, ctypes.c_int64),
+                                     len(self.off) - 1, _p(self.len16, ctypes.c_int32),
+                                     self.n_tokens, js_truthy_int(max_length),
+                                     _p(pa, ctypes.c_int32), _p(pb, ctypes.c_int32),
+                                     _p(pc, ctypes.c_int64), _p(pl, ctypes.c_int64), cap)
+        if n < 0:
+            raise RuntimeError('oracle_count_pairs failed %d' % n)
+        return pa[:n], pb[:n], pc[:n], pl[:n]
+
+
+def xorshift_corpus(seed, A, base, n):
+    out = np.empty(n, dtype=np.uint8)
+    lib().oracle_xorshift_corpus(seed, A, base, out.ctypes.data, n)
+    return out
