@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Benchmark of the BPE merge-training hot path (findNextMerge + applyMerge, core.ts:247-360) on
+MI355X.  One step = one merge iteration: a full pair-count pass over the corpus resident in HBM,
+the argmax with the reference's tie-break, and the in-place rewrite.
+
+Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted on): a 1 GiB
+synthetic latin1 corpus (xorshift32 seed 12345, 256-char alphabet, 1 MiB samples; SURVEY.md
+§8(d)) per GPU, mergeUntil({min_weight: 2}).  Steps W+1..W+K of the merge sequence are timed.
+With N > 1 GPUs each rank holds its own contiguous 1 GiB shard of one corpus stream (weak
+scaling); the per-iteration pair-count exchange is an RCCL all-reduce (bpe-tokenizer_amd/sharded.py).
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, 'BASELINE.json')))['metric']
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ALG_BYTES_PER_PAIR_SCAN = 4    # K1 reads each int32 token once
+
+
+def cpu_baseline(sample_mib, budget_s):
+    """The C restatement (oracle/, single thread) on a bounded sample of the same workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    from oracle import OracleState
+    pkg = importlib.import_module('bpe-tokenizer_amd')
+    n = sample_mib << 20
+    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    lut = np.full(256, -1, np.int32)
+    uniq, idx = np.unique(data, return_index=True)
+    for k, u in enumerate(uniq[np.argsort(idx)]):
+        lut[u] = k
+    nt = int((lut >= 0).sum())
+    st = OracleState(lut[data], np.arange(0, n + 1, 1 << 20, dtype=np.int64), [1] * nt, nt,
+                     extra=4096)
+    del data
+    scans = 0
+    iters = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or iters < 2:
+        live = int(st.off[-1])
+        m = st.find_next_merge(None, 2)
+        if m is None:
+            break
+        st.apply_merge(m[0], m[1])
+        scans += live
+        iters += 1
+    dt = time.perf_counter() - t0
+    return {'value': scans / dt, 'unit': 'pair-scans/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d MiB of the same corpus stream (1 MiB samples), first %d merge '
+                      'iterations, oracle/bpe_oracle.c single-threaded, %.1f s' % (sample_mib, iters, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--corpus-mib', type=int, default=1024, help='corpus MiB per GPU')
+    ap.add_argument('--alphabet', type=int, default=256)
+    ap.add_argument('--cpu-sample-mib', type=int, default=64)
+    ap.add_argument('--cpu-budget-s', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get('RANK', '0'))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+
+    pkg = importlib.import_module('bpe-tokenizer_amd')
+    from importlib import import_module
+    sharded = import_module('bpe-tokenizer_amd.sharded')
+
+    n = args.corpus_mib << 20
+    base = 0 if args.alphabet == 256 else 0x20
+    trainer = sharded.ShardedTrainer.synthetic(device=local_rank, rank=rank, world=world,
+                                               bytes_per_rank=n, sample_bytes=1 << 20,
+                                               seed=12345, alphabet=args.alphabet, base=base,
+                                               dist=dist)
+
+    def step():
+        m = trainer.step(max_length=0, min_weight=2)
+        if m is None:
+            raise SystemExit('corpus exhausted before the timed steps finished')
+        return m
+
+    for _ in range(args.warmup):
+        step()
+    trainer.engine.reset_stats()
+    trainer.engine.stats_enable(True)
+    live0 = trainer.live_tokens_global()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scans = 0
+    for _ in range(args.steps):
+        scans += trainer.live_tokens_global()
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = trainer.engine.stats()
+
+    if rank == 0:
+        k1_ms = st['count_ms'] / max(1, st['count_launches'])
+        live_per_launch = st['live_tokens'] / max(1, st['iterations'])
+        achieved = ALG_BYTES_PER_PAIR_SCAN * live_per_launch / (k1_ms * 1e-3) / 1e9
+        out = {
+            'metric': METRIC,
+            'value': scans / dt,
+            'unit': 'pair-scans/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': dt * 1e3 / args.steps,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'int32',
+            'data': 'synthetic',
+            'config': {
+                'workload': 'C3: %d MiB/GPU latin1 corpus, xorshift32 seed 12345, %d-char alphabet, '
+                            '1 MiB samples; merges %d..%d of mergeUntil({min_weight:2})'
+                            % (args.corpus_mib, args.alphabet, args.warmup + 1,
+                               args.warmup + args.steps),
+                'corpus_tokens': live0,
+                'parallelism': 'corpus-sharded x%d' % world,
+            },
+            'roofline': {
+                'bound': 'hbm',
+                'kernel': 'k_count (K1 pair count)',
+                'achieved': achieved,
+                'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS,
+                'traffic': None,
+                'k1_avg_ms': k1_ms,
+                'alg_bytes_per_launch': ALG_BYTES_PER_PAIR_SCAN * live_per_launch,
+            },
+            'breakdown_ms_per_step': {
+                'count': st['count_ms'] / max(1, args.steps),
+                'select': st['select_ms'] / max(1, args.steps),
+                'apply': st['apply_ms'] / max(1, args.steps),
+                'tie_passes': st['tie_passes'],
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,238 @@
+"""bpe-tokenizer_amd — MI355X-native engine for the BPE merge-training hot path of
+beenotung/bpe-tokenizer (reference: core.ts findNextMerge/applyMerge/mergeUntil).
+
+This module is the Python (ctypes) binding of libbpe.so (C ABI: include/bpe.h).  The drop-in
+replacement of the reference's `BPETokenizer` class lives in js/core.js (Node N-API addon over the
+same C ABI); this binding serves the bench, the tests and multi-process (one rank per GPU) runs.
+
+There is no CPU fallback: importing works anywhere (so the C ABI can be inspected), but creating
+an `Engine` requires libbpe.so and a HIP device and raises otherwise.
+
+Import with ``importlib.import_module('bpe-tokenizer_amd')`` (the directory name has a hyphen).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libbpe.so')
+
+BPE_OK = 0
+BPE_NO_MERGE = 1
+MAX_VOCAB = 55296
+
+# Every symbol include/bpe.h and include/bpe_tools.h declare (checked by tests/test_capi.py).
+C_API = [
+    'bpe_version', 'bpe_last_error', 'bpe_device_count', 'bpe_create', 'bpe_destroy',
+    'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
+    'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
+    'bpe_apply_merge', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
+    'bpe_get_stream', 'bpe_synth_latin1',
+]
+
+
+class BpeError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ('count_ms', ctypes.c_double), ('count_launches', ctypes.c_int64),
+        ('count_slots', ctypes.c_int64), ('select_ms', ctypes.c_double),
+        ('apply_ms', ctypes.c_double), ('apply_launches', ctypes.c_int64),
+        ('apply_slots', ctypes.c_int64), ('tie_passes', ctypes.c_int64),
+        ('iterations', ctypes.c_int64), ('live_tokens', ctypes.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def build(force=False):
+    """Compiles libbpe.so for gfx950 (hipcc cross-compiles; no GPU needed)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(['make', '-s', '-C', HERE] + (['-B'] if force else []))
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Loads libbpe.so (raises if it was not built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BpeError('libbpe.so is missing: run make -C bpe-tokenizer_amd (HIP engine required)')
+    L = ctypes.CDLL(LIB_PATH)
+    i32p, i64p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)
+    vp = ctypes.c_void_p
+    sig = {
+        'bpe_version': ([], ctypes.c_int),
+        'bpe_last_error': ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        'bpe_device_count': ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        'bpe_create': ([ctypes.POINTER(vp), ctypes.c_int], ctypes.c_int),
+        'bpe_destroy': ([vp], ctypes.c_int),
+        'bpe_set_token_len16': ([vp, ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+        'bpe_num_tokens': ([vp, i32p], ctypes.c_int),
+        'bpe_add_sample': ([vp, i32p, ctypes.c_int64], ctypes.c_int),
+        'bpe_add_latin1': ([vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p],
+                           ctypes.c_int),
+        'bpe_clear_corpus': ([vp], ctypes.c_int),
+        'bpe_corpus_size': ([vp, i64p, i64p], ctypes.c_int),
+        'bpe_read_corpus': ([vp, i32p, ctypes.c_int64, i64p, ctypes.c_int64], ctypes.c_int),
+        'bpe_find_next_merge': ([vp, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p],
+                                ctypes.c_int),
+        'bpe_apply_merge': ([vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i64p],
+                            ctypes.c_int),
+        'bpe_merge_until': ([vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, i64p,
+                             ctypes.c_int64, i64p], ctypes.c_int),
+        'bpe_stats_enable': ([vp, ctypes.c_int], ctypes.c_int),
+        'bpe_get_stats': ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
+        'bpe_reset_stats': ([vp], ctypes.c_int),
+        'bpe_get_stream': ([vp, ctypes.POINTER(vp)], ctypes.c_int),
+        'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                              ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    lib().bpe_last_error(buf, 1024)
+    return buf.value.decode(errors='replace')
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise BpeError('%s failed (%d): %s' % (what, rc, last_error()))
+    return rc
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(lib().bpe_device_count(ctypes.byref(n)), 'bpe_device_count')
+    return n.value
+
+
+def synth_latin1(n, seed=12345, A=256, base=0, skip=0):
+    """SURVEY.md §8(d) synthetic corpus: xorshift32 bytes (jump-ahead `skip` outputs)."""
+    out = np.empty(n, dtype=np.uint8)
+    _check(lib().bpe_synth_latin1(seed, A, base, skip, out.ctypes.data, n), 'bpe_synth_latin1')
+    return out
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class Engine:
+    """One corpus shard on one HIP device (a `bpe_ctx`)."""
+
+    def __init__(self, device=0):
+        self._ctx = ctypes.c_void_p()
+        _check(lib().bpe_create(ctypes.byref(self._ctx), device), 'bpe_create')
+
+    def close(self):
+        if self._ctx:
+            lib().bpe_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # vocabulary -------------------------------------------------------------------------------
+    def set_token_len16(self, token_id, len16):
+        _check(lib().bpe_set_token_len16(self._ctx, token_id, len16), 'bpe_set_token_len16')
+
+    def num_tokens(self):
+        n = ctypes.c_int32()
+        _check(lib().bpe_num_tokens(self._ctx, ctypes.byref(n)), 'bpe_num_tokens')
+        return n.value
+
+    # corpus ------------------------------------------------------------------------------------
+    def add_sample(self, ids):
+        a = _i32(ids)
+        p = a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) if a.size else None
+        _check(lib().bpe_add_sample(self._ctx, p, a.size), 'bpe_add_sample')
+
+    def add_latin1(self, data, sample_bytes=0, char_to_id=None, n_tokens=None):
+        """Bulk ingest; returns (char_to_id[256], n_tokens, char_hist[256])."""
+        data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        cmap = np.full(256, -1, np.int32) if char_to_id is None else _i32(char_to_id).copy()
+        nt = ctypes.c_int32(self.num_tokens() if n_tokens is None else n_tokens)
+        hist = np.zeros(256, np.int64)
+        _check(lib().bpe_add_latin1(self._ctx, data.ctypes.data, data.size, sample_bytes,
+                                    cmap.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                    ctypes.byref(nt),
+                                    hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               'bpe_add_latin1')
+        return cmap, nt.value, hist
+
+    def clear_corpus(self):
+        _check(lib().bpe_clear_corpus(self._ctx), 'bpe_clear_corpus')
+
+    def corpus_size(self):
+        s, t = ctypes.c_int64(), ctypes.c_int64()
+        _check(lib().bpe_corpus_size(self._ctx, ctypes.byref(s), ctypes.byref(t)), 'bpe_corpus_size')
+        return s.value, t.value
+
+    def read_corpus(self):
+        """Returns (flat ids int32, sample offsets int64)."""
+        ns, nt = self.corpus_size()
+        ids = np.zeros(max(nt, 1), np.int32)
+        off = np.zeros(ns + 1, np.int64)
+        _check(lib().bpe_read_corpus(self._ctx, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                     ids.size, off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                     off.size), 'bpe_read_corpus')
+        return ids[:nt], off
+
+    def samples(self):
+        ids, off = self.read_corpus()
+        return [ids[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+
+    # hot path ----------------------------------------------------------------------------------
+    def find_next_merge(self, max_length=0, min_weight=0):
+        a, b, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        rc = _check(lib().bpe_find_next_merge(self._ctx, int(max_length or 0), int(min_weight or 0),
+                                              ctypes.byref(a), ctypes.byref(b), ctypes.byref(w)),
+                    'bpe_find_next_merge')
+        return None if rc == BPE_NO_MERGE else (a.value, b.value, w.value)
+
+    def apply_merge(self, a, b, c):
+        r = ctypes.c_int64()
+        _check(lib().bpe_apply_merge(self._ctx, a, b, c, ctypes.byref(r)), 'bpe_apply_merge')
+        return r.value
+
+    def merge_until(self, max_length=0, min_weight=0, max_iterations=0, cap=1 << 16):
+        out = np.zeros(3 * cap, np.int64)
+        n = ctypes.c_int64()
+        _check(lib().bpe_merge_until(self._ctx, int(max_length or 0), int(min_weight or 0),
+                                     int(max_iterations or 0),
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap,
+                                     ctypes.byref(n)), 'bpe_merge_until')
+        k = min(n.value, cap)
+        return [tuple(int(v) for v in out[3 * i:3 * i + 3]) for i in range(k)]
+
+    # measurement -------------------------------------------------------------------------------
+    def stats_enable(self, on=True):
+        _check(lib().bpe_stats_enable(self._ctx, 1 if on else 0), 'bpe_stats_enable')
+
+    def stats(self):
+        s = Stats()
+        _check(lib().bpe_get_stats(self._ctx, ctypes.byref(s)), 'bpe_get_stats')
+        return s.as_dict()
+
+    def reset_stats(self):
+        _check(lib().bpe_reset_stats(self._ctx), 'bpe_reset_stats')

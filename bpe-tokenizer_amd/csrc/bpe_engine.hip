@@ -1,0 +1,707 @@
+// bpe_engine.hip — libbpe: host side of the MI355X BPE merge-training engine + the C ABI of
+// include/bpe.h.  One context = one HIP device + one stream + one corpus shard in HBM.
+//
+// Per findNextMerge (core.ts:247-326):
+//   k_cold_clear -> k_count (K1) -> k_runs -> k_reduce_hot -> k_argmax_hot/cold (K2)
+//   -> k_collect -> [k_exact<TIE> when several pairs share (W, a+b)  (K3, rule R3)]
+// Per applyMerge (core.ts:332-360):
+//   k_exact<APPLY_COUNT> -> k_scan_regions -> k_exact<APPLY_SCATTER> (K4) into the ping-pong
+//   buffer, then swap.
+#include "bpe_kernels.hip.h"
+#include "bpe.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace bpe;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(e_ == hipErrorOutOfMemory ? BPE_ERR_OOM : BPE_ERR_HIP,             \
+                        std::string("bpe native: ") + #expr + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline void dfree(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+template <typename T>
+int dev_alloc(T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? BPE_ERR_OOM : BPE_ERR_HIP,
+                    std::string("bpe native: hipMalloc: ") + hipGetErrorString(e));
+    return BPE_OK;
+}
+
+}  // namespace
+
+struct bpe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // corpus (slots: ids + SEP after every sample, padded with SEP)
+    int32_t *d_ids = nullptr, *d_tmp = nullptr;
+    int64_t cap_slots = 0;
+    int64_t n_slots = 0;
+    int64_t n_samples = 0;
+    int64_t n_live = 0;
+    // vocabulary
+    std::vector<int32_t> h_len16;
+    std::vector<int64_t> h_count;      // occurrences per token in the corpus (exact)
+    int32_t *d_len16 = nullptr;
+    int64_t cap_vocab = 0;
+    bool len16_dirty = true;
+    // count state
+    uint32_t *d_partials = nullptr;
+    unsigned long long *d_spill = nullptr, *d_hot = nullptr;
+    RegionRun *d_runs = nullptr;
+    int64_t *d_carry = nullptr, *d_kept = nullptr, *d_outoff = nullptr;
+    Result *d_res = nullptr, *h_res = nullptr;
+    int2 *d_cand = nullptr;
+    ColdTable cold{};
+    uint32_t *d_cold_nused = nullptr;
+    uint64_t cold_cap = 0;
+    bool runs_valid = false;   // d_runs/d_carry describe the current corpus
+    // geometry of the last pass
+    int64_t n_chunks = 0, cpr = 0;
+    int R = 0, G = 0;
+    // stats
+    bool stats_on = false;
+    bpe_stats stats{};
+    hipEvent_t ev[6] = {};
+};
+
+namespace {
+
+int set_device(bpe_ctx *c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return BPE_OK;
+}
+
+// Ensures slot capacity for `need` slots plus one spare chunk of SEP padding (both buffers).
+int ensure_slots(bpe_ctx *c, int64_t need) {
+    const int64_t want = ((need + CHUNK - 1) / CHUNK + 2) * CHUNK;
+    if (want <= c->cap_slots) return BPE_OK;
+    int64_t cap = std::max<int64_t>(want, c->cap_slots * 3 / 2);
+    cap = (cap + CHUNK - 1) / CHUNK * CHUNK;
+    int32_t *ids, *tmp;
+    int rc;
+    if ((rc = dev_alloc(&ids, cap))) return rc;
+    if ((rc = dev_alloc(&tmp, cap))) {
+        dfree(ids);
+        return rc;
+    }
+    HIP_TRY(hipMemsetAsync(ids, 0xFF, cap * sizeof(int32_t), c->stream));
+    if (c->d_ids && c->n_slots)
+        HIP_TRY(hipMemcpyAsync(ids, c->d_ids, c->n_slots * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                               c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dfree(c->d_ids);
+    dfree(c->d_tmp);
+    c->d_ids = ids;
+    c->d_tmp = tmp;
+    c->cap_slots = cap;
+    return BPE_OK;
+}
+
+int ensure_vocab(bpe_ctx *c, int64_t n) {
+    if ((int64_t)c->h_len16.size() < n) {
+        c->h_len16.resize(n, 1);
+        c->h_count.resize(n, 0);
+        c->len16_dirty = true;
+    }
+    if (n > c->cap_vocab) {
+        int64_t cap = std::max<int64_t>(n, std::max<int64_t>(1024, c->cap_vocab * 2));
+        dfree(c->d_len16);
+        int rc = dev_alloc(&c->d_len16, cap);
+        if (rc) return rc;
+        c->cap_vocab = cap;
+        c->len16_dirty = true;
+    }
+    return BPE_OK;
+}
+
+int sync_len16(bpe_ctx *c) {
+    if (!c->len16_dirty || c->h_len16.empty()) return BPE_OK;
+    HIP_TRY(hipMemcpyAsync(c->d_len16, c->h_len16.data(), c->h_len16.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, c->stream));
+    c->len16_dirty = false;
+    return BPE_OK;
+}
+
+// Upper bound on distinct cold pairs: every counted occurrence with an id >= HOT involves at
+// least one cold-token occurrence, and every token occurrence is in at most two pairs.
+uint64_t cold_bound(const bpe_ctx *c) {
+    uint64_t s = 0;
+    for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
+    uint64_t b = 2 * s + 16;
+    const uint64_t V = c->h_len16.size();
+    if (V > HOT) b = std::min<uint64_t>(b, V * V);
+    return std::min<uint64_t>(b, (uint64_t)c->n_live + 16);
+}
+
+int ensure_cold(bpe_ctx *c) {
+    uint64_t need = cold_bound(c);
+    uint64_t cap = 1024;
+    while (cap < 2 * need) cap <<= 1;
+    if (cap <= c->cold_cap) return BPE_OK;
+    if (cap > (1ull << 31)) return fail(BPE_ERR_OOM, "bpe native: cold pair table too large");
+    dfree(c->cold.keys);
+    dfree(c->cold.counts);
+    dfree(c->cold.used);
+    int rc;
+    if ((rc = dev_alloc(&c->cold.keys, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.counts, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.used, cap))) return rc;
+    HIP_TRY(hipMemsetAsync(c->cold.keys, 0xFF, cap * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->cold.counts, 0, cap * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_cold_nused, 0, sizeof(uint32_t), c->stream));
+    c->cold_cap = cap;
+    c->cold.mask = (uint32_t)(cap - 1);
+    int lg = 0;
+    while ((1ull << lg) < cap) ++lg;
+    c->cold.shift = 32 - lg;
+    c->cold.n_used = c->d_cold_nused;
+    c->cold.overflow = c->d_cold_nused + 1;
+    return BPE_OK;
+}
+
+void geometry(bpe_ctx *c) {
+    c->n_chunks = std::max<int64_t>(1, (c->n_slots + CHUNK - 1) / CHUNK);
+    c->cpr = (c->n_chunks + MAX_REGIONS - 1) / MAX_REGIONS;
+    c->R = (int)((c->n_chunks + c->cpr - 1) / c->cpr);
+    c->G = (c->R + WAVES_PER_WG - 1) / WAVES_PER_WG;
+}
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+// One full count pass: K1 + run resolution + reduction; leaves d_hot and the cold table filled.
+int count_pass(bpe_ctx *c, int64_t max_length) {
+    int rc;
+    if ((rc = ensure_cold(c))) return rc;
+    if ((rc = sync_len16(c))) return rc;
+    geometry(c);
+    hipStream_t s = c->stream;
+    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
+    HIP_TRY(hipMemsetAsync(c->d_cold_nused, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->d_spill, 0, HOT_BINS * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
+    const size_t lds = HIST_WORDS * sizeof(uint32_t);
+    if (max_length)
+        k_count<true><<<c->G, WG, lds, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_len16,
+                                            max_length, c->d_partials, c->d_spill, c->cold,
+                                            c->d_runs);
+    else
+        k_count<false><<<c->G, WG, lds, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_len16, 0,
+                                             c->d_partials, c->d_spill, c->cold, c->d_runs);
+    HIP_TRY(hipGetLastError());
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
+    k_runs<<<(c->R + 255) / 256, 256, 0, s>>>(c->d_runs, c->R, c->d_carry, c->d_len16, max_length,
+                                              max_length ? 1 : 0, c->d_spill, c->cold, 1);
+    k_reduce_hot<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
+    HIP_TRY(hipGetLastError());
+    c->runs_valid = true;
+    return BPE_OK;
+}
+
+// Run info only (for an apply without a preceding find on the same corpus, e.g. restoreMerge).
+int runs_pass(bpe_ctx *c) {
+    return count_pass(c, 0);
+}
+
+int exact_args(bpe_ctx *c, ExactArgs &A) {
+    memset(&A, 0, sizeof A);
+    A.ids = c->d_ids;
+    A.n_chunks = c->n_chunks;
+    A.cpr = c->cpr;
+    A.n_slots = c->n_slots;
+    A.R = c->R;
+    A.carry_off = c->d_carry;
+    A.res = c->d_res;
+    return BPE_OK;
+}
+
+int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int32_t *b,
+            int64_t *w) {
+    if (min_weight == 0) min_weight = 2;                              // core.ts:256
+    if (c->n_live < 2) return BPE_NO_MERGE;
+    int rc;
+    if ((rc = count_pass(c, max_length))) return rc;
+    hipStream_t s = c->stream;
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_res);
+    k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_res);
+    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->cold, c->d_res, c->d_cand);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    uint32_t ovf = 0;
+    HIP_TRY(hipMemcpyAsync(&ovf, c->cold.overflow, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[2], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ovf) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    if (c->stats_on) {
+        c->stats.count_ms += ev_ms(c->ev[0], c->ev[1]);
+        c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
+        c->stats.count_launches += 1;
+        c->stats.count_slots += c->n_chunks * CHUNK;
+        c->stats.iterations += 1;
+        c->stats.live_tokens += c->n_live;
+    }
+    const Result &R = *c->h_res;
+    if (R.best == 0) return BPE_NO_MERGE;                             // core.ts:312
+    const int64_t W = (int64_t)(R.best >> 17);
+    if (W < min_weight) return BPE_NO_MERGE;                          // core.ts:313
+    const unsigned n_cand = R.n_cand;
+    if (n_cand == 0 || n_cand > (unsigned)CAND_CAP)
+        return fail(BPE_ERR_STATE, "bpe native: bad candidate count");
+    std::vector<int2> cand(n_cand);
+    HIP_TRY(hipMemcpyAsync(cand.data(), c->d_cand, n_cand * sizeof(int2), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int32_t ba = cand[0].x, bb = cand[0].y;
+    if (n_cand > 1) {
+        // R3: several pairs share W and a+b -> the one whose last counted occurrence is earliest
+        // (the pair that reached W first in the reference's scan, core.ts:296-305)
+        unsigned long long best_pos = ~0ull;
+        for (unsigned j0 = 0; j0 < n_cand; j0 += MAX_CAND) {
+            const unsigned nb = std::min<unsigned>(MAX_CAND, n_cand - j0);
+            ExactArgs A;
+            exact_args(c, A);
+            A.n_cand = (int)nb;
+            for (unsigned j = 0; j < nb; ++j) {
+                A.ca[j] = cand[j0 + j].x;
+                A.cb[j] = cand[j0 + j].y;
+            }
+            HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+            if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
+            k_exact<TIE><<<(c->R + 3) / 4, 256, 0, s>>>(A);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+            if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (c->stats_on) {
+                c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
+                c->stats.tie_passes += 1;
+            }
+            for (unsigned j = 0; j < nb; ++j) {
+                const unsigned long long p = c->h_res->last[j];
+                if (p && p < best_pos) {
+                    best_pos = p;
+                    ba = cand[j0 + j].x;
+                    bb = cand[j0 + j].y;
+                }
+            }
+        }
+        if (best_pos == ~0ull) return fail(BPE_ERR_STATE, "bpe native: tie pass found no occurrence");
+    }
+    *a = ba;
+    *b = bb;
+    *w = W;
+    return BPE_OK;
+}
+
+int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
+    if (a < 0 || b < 0 || cc < 0 || cc >= BPE_MAX_VOCAB)
+        return fail(cc >= BPE_MAX_VOCAB ? BPE_ERR_VOCAB : BPE_ERR_ARG,
+                    "bpe native: token id out of range (vocab is limited to 55295 tokens)");
+    if (a >= (int64_t)c->h_len16.size() || b >= (int64_t)c->h_len16.size())
+        return fail(BPE_ERR_ARG, "bpe native: apply_merge with an unregistered token");
+    int rc;
+    if ((rc = ensure_vocab(c, (int64_t)cc + 1))) return rc;
+    c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                   // core.ts:318
+    c->len16_dirty = true;
+    if (c->n_live < 2) {
+        if (replaced) *replaced = 0;
+        return BPE_OK;
+    }
+    if (!c->runs_valid)
+        if ((rc = runs_pass(c))) return rc;
+    geometry(c);
+    hipStream_t s = c->stream;
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    ExactArgs A;
+    exact_args(c, A);
+    A.a = a;
+    A.b = b;
+    A.c = cc;
+    A.kept = c->d_kept;
+    A.out_off = c->d_outoff;
+    A.out = c->d_tmp;
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
+    k_exact<APPLY_COUNT><<<(c->R + 3) / 4, 256, 0, s>>>(A);
+    k_scan_regions<<<1, 1024, 0, s>>>(c->d_kept, c->R, c->d_outoff, c->d_res);
+    k_exact<APPLY_SCATTER><<<(c->R + 3) / 4, 256, 0, s>>>(A);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t kept = (int64_t)c->h_res->kept_total;
+    const int64_t R = (int64_t)c->h_res->replaced;
+    // SEP padding after the compacted corpus (at least one spare chunk)
+    const int64_t pad_end = ((kept + CHUNK - 1) / CHUNK + 1) * CHUNK;
+    HIP_TRY(hipMemsetAsync(c->d_tmp + kept, 0xFF, (pad_end - kept) * sizeof(int32_t), s));
+    std::swap(c->d_ids, c->d_tmp);
+    c->n_slots = kept;
+    c->n_live -= R;
+    c->h_count[a] -= R;
+    c->h_count[b] -= R;
+    c->h_count[cc] += R;
+    c->runs_valid = false;
+    if (c->stats_on) {
+        c->stats.apply_ms += ev_ms(c->ev[0], c->ev[1]);
+        c->stats.apply_launches += 1;
+        c->stats.apply_slots += c->n_chunks * CHUNK;
+    }
+    if (replaced) *replaced = R;
+    return BPE_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int bpe_version(void) { return 100; }
+
+int bpe_last_error(char *buf, size_t cap) {
+    if (!buf || !cap) return BPE_ERR_ARG;
+    snprintf(buf, cap, "%s", g_err.c_str());
+    return BPE_OK;
+}
+
+int bpe_device_count(int *n) {
+    if (!n) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int k = 0;
+    if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+    *n = k;
+    return BPE_OK;
+}
+
+int bpe_create(bpe_ctx **out, int device) {
+    if (!out) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(BPE_ERR_HIP, "bpe native: no HIP device available (MI355X required)");
+    if (device < 0 || device >= n) return fail(BPE_ERR_ARG, "bpe native: bad device index");
+    bpe_ctx *c = new bpe_ctx();
+    c->device = device;
+    int rc;
+    auto bail = [&](int code) {
+        bpe_destroy(c);
+        return code;
+    };
+    if ((rc = set_device(c))) return bail(rc);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipStreamCreate failed"));
+    for (auto &e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(fail(BPE_ERR_HIP, "bpe native: event"));
+    if ((rc = dev_alloc(&c->d_partials, (size_t)MAX_WG * HIST_WORDS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_spill, HOT_BINS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_hot, HOT_BINS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_runs, MAX_REGIONS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_carry, MAX_REGIONS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_kept, MAX_REGIONS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_outoff, MAX_REGIONS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_res, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_cand, CAND_CAP))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_cold_nused, 4))) return bail(rc);
+    if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
+    if (hipMemset(c->d_cold_nused, 0, 16) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
+    if ((rc = ensure_slots(c, 0))) return bail(rc);
+    if ((rc = ensure_vocab(c, 0))) return bail(rc);
+    if ((rc = ensure_cold(c))) return bail(rc);
+    if (hipFuncSetAttribute((const void *)k_count<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HIST_WORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_count<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HIST_WORDS * sizeof(uint32_t)) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: cannot reserve 128 KiB of LDS"));
+    *out = c;
+    return BPE_OK;
+}
+
+int bpe_destroy(bpe_ctx *c) {
+    if (!c) return BPE_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
+                    c->d_runs, c->d_carry, c->d_kept, c->d_outoff, c->d_res, c->d_cand, c->d_cold_nused,
+                    c->cold.keys, c->cold.counts, c->cold.used};
+    for (void *p : ptrs)
+        dfree(p);
+    if (c->h_res) (void)hipHostFree(c->h_res);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return BPE_OK;
+}
+
+int bpe_set_token_len16(bpe_ctx *c, int32_t id, int32_t len16) {
+    if (!c || id < 0 || len16 < 0) return fail(BPE_ERR_ARG, "bpe native: bad token registration");
+    if (id >= BPE_MAX_VOCAB)
+        return fail(BPE_ERR_VOCAB, "bpe native: vocab is limited to 55295 tokens (UTF-16 surrogates)");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if ((rc = ensure_vocab(c, (int64_t)id + 1))) return rc;
+    if (c->h_len16[id] != len16) {
+        c->h_len16[id] = len16;
+        c->len16_dirty = true;
+    }
+    return BPE_OK;
+}
+
+int bpe_num_tokens(bpe_ctx *c, int32_t *n) {
+    if (!c || !n) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    *n = (int32_t)c->h_len16.size();
+    return BPE_OK;
+}
+
+int bpe_add_sample(bpe_ctx *c, const int32_t *ids, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !ids)) return fail(BPE_ERR_ARG, "bpe native: bad sample");
+    int rc = set_device(c);
+    if (rc) return rc;
+    int32_t mx = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= BPE_MAX_VOCAB)
+            return fail(BPE_ERR_ARG, "bpe native: token id out of range in sample");
+        mx = std::max(mx, ids[i]);
+    }
+    if ((rc = ensure_vocab(c, (int64_t)mx + 1))) return rc;
+    if ((rc = ensure_slots(c, c->n_slots + n + 1))) return rc;
+    if (n) HIP_TRY(hipMemcpy(c->d_ids + c->n_slots, ids, n * sizeof(int32_t), hipMemcpyHostToDevice));
+    const int32_t sep = SEP;
+    HIP_TRY(hipMemcpy(c->d_ids + c->n_slots + n, &sep, sizeof(int32_t), hipMemcpyHostToDevice));
+    for (int64_t i = 0; i < n; ++i) c->h_count[ids[i]] += 1;
+    c->n_slots += n + 1;
+    c->n_samples += 1;
+    c->n_live += n;
+    c->runs_valid = false;
+    return BPE_OK;
+}
+
+int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_bytes,
+                   int32_t char_to_id[256], int32_t *n_tokens_io, int64_t char_hist[256]) {
+    if (!c || n < 0 || (n > 0 && !bytes) || !char_to_id || !n_tokens_io || sample_bytes < 0)
+        return fail(BPE_ERR_ARG, "bpe native: bad latin1 ingest arguments");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (n == 0) {
+        if (char_hist) memset(char_hist, 0, 256 * sizeof(int64_t));
+        return bpe_add_sample(c, nullptr, 0);
+    }
+    if (sample_bytes == 0 || sample_bytes > n) sample_bytes = n;
+    const int64_t n_smp = (n + sample_bytes - 1) / sample_bytes;
+    hipStream_t s = c->stream;
+    uint8_t *d_bytes = nullptr;
+    unsigned long long *d_stats = nullptr;   // first[256] + hist[256]
+    int32_t *d_map = nullptr;
+    if ((rc = dev_alloc(&d_bytes, n))) return rc;
+    if ((rc = dev_alloc(&d_stats, 512)) || (rc = dev_alloc(&d_map, 256))) {
+        dfree(d_bytes);
+        dfree(d_stats);
+        return rc;
+    }
+    auto cleanup = [&]() {
+        dfree(d_bytes);
+        dfree(d_stats);
+        dfree(d_map);
+    };
+    std::vector<unsigned long long> st(512);
+    if (hipMemcpyAsync(d_bytes, bytes, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d_stats, 0xFF, 256 * sizeof(unsigned long long), s) != hipSuccess ||
+        hipMemsetAsync(d_stats + 256, 0, 256 * sizeof(unsigned long long), s) != hipSuccess) {
+        cleanup();
+        return fail(BPE_ERR_HIP, "bpe native: latin1 upload failed");
+    }
+    const int blocks = (int)std::min<int64_t>(2048, (n + 65535) / 65536);
+    k_byte_stats<<<blocks, 256, 0, s>>>(d_bytes, n, d_stats, d_stats + 256);
+    if (hipMemcpyAsync(st.data(), d_stats, 512 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                       s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        cleanup();
+        return fail(BPE_ERR_HIP, "bpe native: latin1 stats failed");
+    }
+    // first-appearance order for unseen chars (core.ts:186-199)
+    std::vector<std::pair<unsigned long long, int>> fresh;
+    for (int ch = 0; ch < 256; ++ch)
+        if (st[256 + ch] && char_to_id[ch] < 0) fresh.push_back({st[ch], ch});
+    std::sort(fresh.begin(), fresh.end());
+    int32_t next = *n_tokens_io;
+    for (auto &p : fresh) {
+        if (next >= BPE_MAX_VOCAB) {
+            cleanup();
+            return fail(BPE_ERR_VOCAB, "bpe native: vocab limit");
+        }
+        char_to_id[p.second] = next++;
+    }
+    if ((rc = ensure_vocab(c, next))) {
+        cleanup();
+        return rc;
+    }
+    for (int ch = 0; ch < 256; ++ch) {
+        if (st[256 + ch] == 0) continue;
+        const int32_t id = char_to_id[ch];
+        c->h_count[id] += (int64_t)st[256 + ch];
+        if (id >= *n_tokens_io) {
+            c->h_len16[id] = 1;
+            c->len16_dirty = true;
+        }
+    }
+    *n_tokens_io = next;
+    if (char_hist)
+        for (int ch = 0; ch < 256; ++ch) char_hist[ch] = (int64_t)st[256 + ch];
+    if ((rc = ensure_slots(c, c->n_slots + n + n_smp))) {
+        cleanup();
+        return rc;
+    }
+    if (hipMemcpyAsync(d_map, char_to_id, 256 * sizeof(int32_t), hipMemcpyHostToDevice, s) !=
+        hipSuccess) {
+        cleanup();
+        return fail(BPE_ERR_HIP, "bpe native: map upload failed");
+    }
+    k_expand_latin1<<<4096, 256, 0, s>>>(d_bytes, n, sample_bytes, d_map, c->d_ids + c->n_slots);
+    hipError_t e = hipStreamSynchronize(s);
+    cleanup();
+    if (e != hipSuccess) return fail(BPE_ERR_HIP, "bpe native: latin1 expand failed");
+    c->n_slots += n + n_smp;
+    c->n_samples += n_smp;
+    c->n_live += n;
+    c->runs_valid = false;
+    return BPE_OK;
+}
+
+int bpe_clear_corpus(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_ids, 0xFF, c->cap_slots * sizeof(int32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_tmp, 0xFF, c->cap_slots * sizeof(int32_t), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->n_slots = c->n_samples = c->n_live = 0;
+    std::fill(c->h_count.begin(), c->h_count.end(), 0);
+    c->runs_valid = false;
+    return BPE_OK;
+}
+
+int bpe_corpus_size(bpe_ctx *c, int64_t *n_samples, int64_t *n_tokens) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    if (n_samples) *n_samples = c->n_samples;
+    if (n_tokens) *n_tokens = c->n_live;
+    return BPE_OK;
+}
+
+int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
+                    int64_t off_cap) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    if (ids_cap < c->n_live || off_cap < c->n_samples + 1 || (c->n_live && !ids_out) || !sample_off)
+        return fail(BPE_ERR_ARG, "bpe native: read_corpus buffers too small");
+    int rc = set_device(c);
+    if (rc) return rc;
+    std::vector<int32_t> slots(c->n_slots);
+    if (c->n_slots)
+        HIP_TRY(hipMemcpy(slots.data(), c->d_ids, c->n_slots * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int64_t o = 0, sidx = 0;
+    sample_off[0] = 0;
+    for (int64_t i = 0; i < c->n_slots; ++i) {
+        if (slots[i] == SEP) sample_off[++sidx] = o;
+        else ids_out[o++] = slots[i];
+    }
+    if (sidx != c->n_samples || o != c->n_live)
+        return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
+    return BPE_OK;
+}
+
+int bpe_find_next_merge(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a,
+                        int32_t *b, int64_t *w) {
+    if (!c || !a || !b || !w) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return do_find(c, max_length, min_weight, a, b, w);
+}
+
+int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return do_apply(c, a, b, cc, replaced);
+}
+
+int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
+                    int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    if (!c || !n_merges || (cap > 0 && !out_abw))
+        return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    int64_t n = 0;
+    for (int64_t it = 1; !max_iterations || it <= max_iterations; ++it) {   // core.ts:374-378
+        int32_t a, b;
+        int64_t w;
+        rc = do_find(c, max_length, min_weight, &a, &b, &w);
+        if (rc == BPE_NO_MERGE) break;
+        if (rc) return rc;
+        const int32_t cc = (int32_t)c->h_len16.size();
+        int64_t rep = 0;
+        if ((rc = do_apply(c, a, b, cc, &rep))) return rc;
+        if (rep != w) return fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+        if (n < cap) {
+            out_abw[3 * n] = a;
+            out_abw[3 * n + 1] = b;
+            out_abw[3 * n + 2] = w;
+        }
+        ++n;
+    }
+    *n_merges = n;
+    return BPE_OK;
+}
+
+int bpe_stats_enable(bpe_ctx *c, int on) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    c->stats_on = on != 0;
+    return BPE_OK;
+}
+
+int bpe_get_stats(bpe_ctx *c, bpe_stats *out) {
+    if (!c || !out) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    *out = c->stats;
+    return BPE_OK;
+}
+
+int bpe_reset_stats(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    memset(&c->stats, 0, sizeof c->stats);
+    return BPE_OK;
+}
+
+int bpe_get_stream(bpe_ctx *c, void **stream) {
+    if (!c || !stream) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    *stream = (void *)c->stream;
+    return BPE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+/*
+ * bpe.h — C ABI of libbpe: the MI355X (gfx950) engine for the BPE merge-training hot path of
+ * beenotung/bpe-tokenizer (reference: /root/reference/core.ts, v2.2.0).
+ *
+ * The reference has no FFI layer: its drop-in boundary is the public `BPETokenizer` class
+ * (core.ts:77).  These entry points are exactly what that class's corpus-touching methods need;
+ * the host side (bpe-tokenizer_amd/js/core.js over the N-API addon, or any ctypes/cgo binding —
+ * see INTEGRATION.md) keeps the token table, codes, JSON and encode/decode bookkeeping and calls
+ * down here for every pass over the corpus.
+ *
+ * Conventions
+ *   - Every function returns an int status: BPE_OK (0), BPE_NO_MERGE (1, "findNextMerge returned
+ *     null"), or a negative error code; bpe_last_error() returns the message of the last error
+ *     raised on the calling thread.
+ *   - Token ids are the reference's `token.index` (code point of `token.code` minus one,
+ *     core.ts:149,189,316,485).  Ids must stay below BPE_MAX_VOCAB (55 296): above it the
+ *     reference's codes become lone UTF-16 surrogates (hard part 8).
+ *   - Caller-owned host buffers are copied in/out; the library never retains host pointers.
+ *   - A context owns one HIP device, one stream and all device memory of one corpus shard.
+ *   - There is no CPU fallback: without a usable HIP device bpe_create() fails with BPE_ERR_HIP.
+ */
+#ifndef BPE_H
+#define BPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BPE_OK 0
+#define BPE_NO_MERGE 1
+#define BPE_ERR_ARG (-1)
+#define BPE_ERR_HIP (-2)
+#define BPE_ERR_OOM (-3)
+#define BPE_ERR_STATE (-4)
+#define BPE_ERR_VOCAB (-5)
+
+#define BPE_MAX_VOCAB 55296
+
+typedef struct bpe_ctx bpe_ctx;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int bpe_version(void);
+
+/* Copies the last error message of this thread (NUL-terminated, truncated to cap). */
+int bpe_last_error(char *buf, size_t cap);
+
+/* Number of visible HIP devices (0 when none). */
+int bpe_device_count(int *n);
+
+/* `new BPETokenizer()` (core.ts:77-106): an empty corpus shard on HIP device `device`. */
+int bpe_create(bpe_ctx **out, int device);
+int bpe_destroy(bpe_ctx *ctx);
+
+/* ---- vocabulary ------------------------------------------------------------------------------
+ * Registers token `id` with the UTF-16 length of its chars (`token.chars.length`, used by the
+ * max_length filter, core.ts:270-273).  Grows the table when id >= current size.  Called by the
+ * host for every new char token (core.ts:186-199) and on fromJSON (core.ts:147-162); merged tokens
+ * are registered by bpe_apply_merge itself (len16[c] = len16[a] + len16[b], core.ts:318). */
+int bpe_set_token_len16(bpe_ctx *ctx, int32_t id, int32_t len16);
+int bpe_num_tokens(bpe_ctx *ctx, int32_t *n_tokens);
+
+/* ---- corpus ----------------------------------------------------------------------------------
+ * addToCorpus (core.ts:182-207) / restoreToCorpus (core.ts:213-216): appends ONE sample whose
+ * chars the host has already mapped to token ids.  n may be 0 (an empty sample). */
+int bpe_add_sample(bpe_ctx *ctx, const int32_t *ids, int64_t n);
+
+/* Bulk native ingest for corpora JS strings cannot hold: `n` latin1 bytes
+ * (byte b == code point b), split into samples of `sample_bytes` (last one shorter; 0 = one
+ * sample).  char_to_id[256] is in/out: -1 marks an unseen char; unseen chars get ids
+ * *n_tokens_io, *n_tokens_io+1, ... in first-appearance order (core.ts:186-199).  char_hist[256]
+ * receives the per-char occurrence counts of this call (the weight/original_weight increments of
+ * core.ts:192-202).  Each new char is registered with len16 = 1. */
+int bpe_add_latin1(bpe_ctx *ctx, const uint8_t *bytes, int64_t n, int64_t sample_bytes,
+                   int32_t char_to_id[256], int32_t *n_tokens_io, int64_t char_hist[256]);
+
+/* `corpus_in_code = []` (example/import-merge-log-to-ram.ts:21-22): drops every sample. */
+int bpe_clear_corpus(bpe_ctx *ctx);
+
+/* Sample count and live token count (excluding sample separators). */
+int bpe_corpus_size(bpe_ctx *ctx, int64_t *n_samples, int64_t *n_tokens);
+
+/* Materialises `corpus_in_code` (core.ts:106): all samples' ids back to back into ids_out
+ * (capacity ids_cap) and n_samples+1 offsets into sample_off (capacity off_cap). */
+int bpe_read_corpus(bpe_ctx *ctx, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
+                    int64_t off_cap);
+
+/* ---- hot path ----------------------------------------------------------------------------------
+ * findNextMerge (core.ts:247-326).  max_length: 0 = falsy = unlimited (core.ts:255,272);
+ * min_weight: 0 = falsy = 2 (core.ts:256).  On BPE_OK writes the chosen pair (a, b) and its count
+ * W (== c.weight == c.original_weight, core.ts:317-323); BPE_NO_MERGE when the reference returns
+ * null (core.ts:312-313).  The selection is bit-identical to the reference's running argmax
+ * (max W, then min a+b, then earliest W-th counted occurrence — SURVEY.md Appendix A). */
+int bpe_find_next_merge(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int32_t *a,
+                        int32_t *b, int64_t *w);
+
+/* applyMerge corpus rewrite (core.ts:356-359, `replaceAll(a.code+b.code, c.code)`): every
+ * leftmost non-overlapping occurrence of (a, b) becomes c.  Also registers c (len16 sum).
+ * `replaced` (may be NULL) receives the replacement count (== W for a merge from findNextMerge). */
+int bpe_apply_merge(bpe_ctx *ctx, int32_t a, int32_t b, int32_t c, int64_t *replaced);
+
+/* mergeUntil (core.ts:365-383).  max_iterations 0 = unlimited.  New tokens get ids
+ * bpe_num_tokens(), bpe_num_tokens()+1, ...  (core.ts:315).  Writes (a, b, W) int64 triples into
+ * out_abw (capacity `cap` triples) and the number of merges into *n_merges. */
+int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_t max_iterations,
+                    int64_t *out_abw, int64_t cap, int64_t *n_merges);
+
+/* ---- measurement -------------------------------------------------------------------------------
+ * HIP-event timings of the kernels, recorded on the context's own stream. */
+typedef struct {
+    double count_ms;          /* pair-count kernel (K1), summed over launches */
+    int64_t count_launches;
+    int64_t count_slots;      /* int32 slots streamed by K1, summed over launches */
+    double select_ms;         /* run resolution + reduce + argmax + tie kernels */
+    double apply_ms;          /* apply kernels (match/count + scan + scatter) */
+    int64_t apply_launches;
+    int64_t apply_slots;      /* int32 slots read by the apply scatter, summed */
+    int64_t tie_passes;       /* iterations that needed the R3 tie-break pass */
+    int64_t iterations;       /* findNextMerge calls that scanned the corpus */
+    int64_t live_tokens;      /* sum over those calls of live corpus tokens (pair-scans) */
+} bpe_stats;
+
+int bpe_stats_enable(bpe_ctx *ctx, int on);
+int bpe_get_stats(bpe_ctx *ctx, bpe_stats *out);
+int bpe_reset_stats(bpe_ctx *ctx);
+
+/* Raw device pointer of the context's HIP stream (hipStream_t), for callers that order their own
+ * work (collectives, events) against the engine. */
+int bpe_get_stream(bpe_ctx *ctx, void **stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPE_H */

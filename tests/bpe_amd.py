@@ -1,0 +1,32 @@
+"""Test-side access to the product package (the hyphenated directory bpe-tokenizer_amd)."""
+import importlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+pkg = importlib.import_module('bpe-tokenizer_amd')
+
+
+def run_engine(samples_ids, len16, opts, device=0):
+    """Drives the HIP engine exactly like the reference's merge loop (core.ts:374-381)."""
+    e = pkg.Engine(device)
+    for i, l in enumerate(len16):
+        e.set_token_len16(i, l)
+    for s in samples_ids:
+        e.add_sample(s)
+    merges = []
+    it = 1
+    max_it = opts.get('max_iterations')
+    n_tokens = len(len16)
+    while not max_it or it <= max_it:
+        m = e.find_next_merge(opts.get('max_length') or 0, opts.get('min_weight') or 0)
+        if m is None:
+            break
+        rep = e.apply_merge(m[0], m[1], n_tokens)
+        assert rep == m[2], 'replaced %d != W %d' % (rep, m[2])
+        n_tokens += 1
+        merges.append(m)
+        it += 1
+    return e, merges

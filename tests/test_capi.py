@@ -1,0 +1,54 @@
+"""CPU-side checks of the C ABI: the library builds, loads and exports every declared symbol."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from bpe_amd import ROOT, pkg
+
+
+def declared_symbols():
+    names = []
+    for h in ('bpe.h', 'bpe_tools.h'):
+        src = open(os.path.join(ROOT, 'include', h)).read()
+        names += re.findall(r'^int (bpe_\w+)\(', src, re.M)
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    pkg.build()
+    out = subprocess.check_output(['nm', '-D', '--defined-only', pkg.LIB_PATH]).decode()
+    exported = set(re.findall(r' T (bpe_\w+)', out))
+    decl = declared_symbols()
+    assert decl, 'no declarations parsed'
+    missing = [d for d in decl if d not in exported]
+    assert not missing, missing
+    assert sorted(decl) == sorted(pkg.C_API)
+
+
+def test_library_loads_and_reports_no_device_without_gpu():
+    L = pkg.lib()
+    assert L.bpe_version() >= 100
+    n = pkg.device_count()
+    if n == 0:
+        with pytest.raises(pkg.BpeError, match='no HIP device'):
+            pkg.Engine(0)
+
+
+def test_code_object_is_gfx950():
+    data = open(pkg.LIB_PATH, 'rb').read()
+    assert b'hipv4-amdgcn-amd-amdhsa--gfx950' in data
+    assert b'gfx942' not in data and b'gfx90a' not in data
+
+
+def test_synthetic_generator_matches_oracle_and_jumps():
+    import numpy as np
+    from oracle import xorshift_corpus
+    a = pkg.synth_latin1(1 << 16, seed=12345, A=95, base=0x20)
+    assert a.tolist() == xorshift_corpus(12345, 95, 0x20, 1 << 16).tolist()
+    b = pkg.synth_latin1(1000, seed=12345, A=256, base=0, skip=5000)
+    full = pkg.synth_latin1(6000, seed=12345, A=256, base=0)
+    assert np.array_equal(b, full[5000:])
+    big = pkg.synth_latin1(1 << 23, seed=7, A=256)           # multithreaded path
+    assert np.array_equal(big[-100:], pkg.synth_latin1(100, seed=7, A=256, skip=(1 << 23) - 100))

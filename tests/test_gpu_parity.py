@@ -1,0 +1,178 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden vectors and the
+oracle.  Bit-exact merge sequences and corpora are required everywhere."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from bpe_amd import pkg, run_engine
+from golden_util import load_config2, load_small
+from oracle import Corpus, OracleState
+
+pytestmark = pytest.mark.gpu
+
+
+def engine_case(case):
+    c = Corpus()
+    for s in case['samples']:
+        c.add(s)
+    e, merges = run_engine(c.samples, c.len16, case['opts'])
+    return c, e, merges
+
+
+def test_small_golden_cases():
+    """All reference-generated small cases (spec inputs + 1500 seeded random corpora)."""
+    bad = []
+    for case in load_small():
+        c, e, merges = engine_case(case)
+        got = [list(m) for m in merges]
+        if got != case['merges'] or e.samples() != case['final_ids']:
+            bad.append((case['name'], got[:5], case['merges'][:5]))
+        e.close()
+        if len(bad) > 5:
+            break
+    assert not bad, bad
+
+
+def test_config1_drop_in_numbers():
+    """BASELINE config 1: 'aaabdaaabac', mergeUntil({min_weight:2})."""
+    c = Corpus()
+    c.add('aaabdaaabac')
+    e, merges = run_engine(c.samples, c.len16, {'min_weight': 2})
+    assert merges == [(0, 0, 2), (0, 1, 2), (4, 5, 2)]
+    assert e.samples() == [[6, 2, 6, 0, 3]]
+
+
+def random_corpus(rng, n_tokens, alphabet, run_bias, n_samples):
+    """Seeded corpus with controllable run structure (runs exercise the X X skip rule)."""
+    out = []
+    per = max(1, n_tokens // n_samples)
+    for _ in range(n_samples):
+        L = rng.randint(0, 2 * per)
+        toks = np.empty(L, np.int32)
+        i = 0
+        while i < L:
+            t = rng.randrange(alphabet)
+            k = 1 if rng.random() > run_bias else rng.randint(2, 12 if rng.random() < 0.9 else 900)
+            toks[i:i + k] = t
+            i += k
+        out.append(toks[:L])
+    return out
+
+
+@pytest.mark.parametrize('seed', range(12))
+def test_random_vs_oracle(seed):
+    rng = random.Random(seed)
+    n_tokens = rng.choice([3000, 40000, 300000, 1500000])
+    alphabet = rng.choice([2, 3, 5, 20, 95, 256, 300])
+    samples = random_corpus(rng, n_tokens, alphabet, rng.choice([0.0, 0.05, 0.3, 0.7]),
+                            rng.choice([1, 3, 17, 200]))
+    len16 = [rng.choice([1, 1, 1, 2]) for _ in range(alphabet)]
+    opts = {'max_iterations': rng.choice([20, 60]),
+            'max_length': rng.choice([0, 0, 3, 4, 6]),
+            'min_weight': rng.choice([0, 2, 3])}
+    st = OracleState(np.concatenate(samples) if samples else np.zeros(0, np.int32),
+                     np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64),
+                     len16, alphabet)
+    want = st.merge_until(opts['max_length'], opts['min_weight'], opts['max_iterations'])
+    e, got = run_engine(samples, len16, opts)
+    assert got == want
+    assert e.samples() == st.samples()
+
+
+@pytest.mark.parametrize('n', [9, 10, 1023, 1024, 65536 * 3 + 7, 3_000_001])
+def test_long_runs_cross_chunks_and_regions(n):
+    """'x' * n (+ a breaker) — runs far longer than a chunk and than a region."""
+    samples = [np.zeros(n, np.int32), np.array([0, 0, 1, 0, 0, 0], np.int32),
+               np.concatenate([np.zeros(n // 3, np.int32), [1], np.zeros(n // 2, np.int32)]).astype(np.int32)]
+    st = OracleState(np.concatenate(samples), np.array([0, n, n + 6, n + 6 + len(samples[2])],
+                                                       np.int64), [1, 1], 2)
+    want = st.merge_until(0, 0, 0)
+    e, got = run_engine(samples, [1, 1], {})
+    assert got == want
+    assert e.samples() == st.samples()
+
+
+def test_ties_need_r3():
+    """Many pairs with equal W and equal a+b: the earliest W-th occurrence must win (R3)."""
+    rng = random.Random(5)
+    for trial in range(20):
+        V = rng.choice([12, 40, 300])
+        B = V - 1                              # breaker token, keeps pairs apart
+        s = rng.randint(V // 3, V - 2)         # common a+b
+        pairs = [(i, s - i) for i in range(0, s + 1) if s - i < B and i < B]
+        rng.shuffle(pairs)
+        pairs = pairs[:rng.randint(2, len(pairs))]
+        r = rng.randint(1, 5)
+        seq = []
+        events = [p for p in pairs for _ in range(r)]
+        rng.shuffle(events)
+        for a, b in events:
+            seq += [a, b, B]
+        samples = [np.array(seq, np.int32)]
+        len16 = [1] * V
+        st = OracleState(samples[0], np.array([0, len(seq)], np.int64), len16, V)
+        want = st.merge_until(0, -1, 30)
+        e, got = run_engine(samples, len16, {'min_weight': -1, 'max_iterations': 30})
+        assert got == want, trial
+        assert e.samples() == st.samples()
+
+
+def test_latin1_ingest_matches_host_mapping():
+    data = pkg.synth_latin1(3 << 20, seed=99, A=200, base=40)
+    e = pkg.Engine(0)
+    cmap, nt, hist = e.add_latin1(data, sample_bytes=1 << 20)
+    first = {}
+    for b in data.tolist():
+        if b not in first:
+            first[b] = len(first)
+    assert nt == len(first)
+    for b, i in first.items():
+        assert cmap[b] == i
+    assert hist.sum() == data.size
+    ids, off = e.read_corpus()
+    assert off.tolist() == [0, 1 << 20, 2 << 20, 3 << 20]
+    assert np.array_equal(ids, cmap[data])
+
+
+def test_config2_golden():
+    """BASELINE config 2: 10 MiB ASCII, 1000 merges — merge list and final-corpus SHA-256 equal
+    the reference's own run (tests/golden/config2.json)."""
+    g = load_config2()
+    if g is None:
+        pytest.skip('config2 fixture not generated')
+    data = pkg.synth_latin1(g['total'], seed=g['seed'], A=g['A'], base=g['base'])
+    e = pkg.Engine(0)
+    cmap, nt, hist = e.add_latin1(data, sample_bytes=g['sample'])
+    assert nt == g['char_count']
+    merges = e.merge_until(0, g['min_weight'], g['max_iterations'])
+    assert [list(m) for m in merges] == g['merges']
+    ids, off = e.read_corpus()
+    h = hashlib.sha256()
+    for i in range(len(off) - 1):
+        h.update(np.append(ids[off[i]:off[i + 1]], -1).astype('<i4').tobytes())
+    assert h.hexdigest() == g['final_ids_sha256']
+
+
+@pytest.mark.slow
+def test_config3_prefix_vs_oracle():
+    """1 GiB, 256-char corpus (BASELINE config 3): first merges equal the C restatement; apply
+    removes exactly W tokens each time."""
+    n = 1 << 30
+    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    e = pkg.Engine(0)
+    cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    ids = cmap[data]
+    del data
+    off = np.arange(0, n + 1, 1 << 20, dtype=np.int64)
+    st = OracleState(ids, off, [1] * nt, nt, extra=64)
+    del ids
+    for _ in range(3):
+        want = st.find_next_merge(0, 2)
+        got = e.find_next_merge(0, 2)
+        assert got == want
+        c = st.n_tokens
+        st.apply_merge(want[0], want[1])
+        assert e.apply_merge(got[0], got[1], c) == got[2]
+    assert e.corpus_size()[1] == st.off[-1]
