@@ -124,8 +124,9 @@ def main():
     st = trainer.engine.stats()
 
     if rank == 0:
-        k1_ms = st['count_ms'] / max(1, st['count_launches'])
-        live_per_launch = st['live_tokens'] / max(1, st['iterations'])
+        k1_ms = st['step_ms'] / max(1, st['step_launches'])
+        live_per_launch = st['step_live'] / max(1, st['step_launches'])
+        slots_per_launch = st['step_slots'] / max(1, st['step_launches'])
         achieved = ALG_BYTES_PER_PAIR_SCAN * live_per_launch / (k1_ms * 1e-3) / 1e9
         out = {
             'metric': METRIC,
@@ -150,20 +151,21 @@ def main():
             },
             'roofline': {
                 'bound': 'hbm',
-                'kernel': 'k_count (K1 pair count)',
+                'kernel': 'k_step (fused K4 apply + K1 pair count, one pass per merge)',
                 'achieved': achieved,
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': None,
-                'k1_avg_ms': k1_ms,
+                'kernel_avg_ms': k1_ms,
                 'alg_bytes_per_launch': ALG_BYTES_PER_PAIR_SCAN * live_per_launch,
+                'slots_streamed_per_launch': slots_per_launch,
             },
             'breakdown_ms_per_step': {
-                'count': st['count_ms'] / max(1, args.steps),
+                'stream_pass': st['step_ms'] / max(1, args.steps),
                 'select': st['select_ms'] / max(1, args.steps),
-                'apply': st['apply_ms'] / max(1, args.steps),
                 'tie_passes': st['tie_passes'],
+                'compactions': st['compactions'],
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -29,7 +29,7 @@ C_API = [
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
-    'bpe_get_stream', 'bpe_synth_latin1',
+    'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount',
 ]
 
 
@@ -39,11 +39,11 @@ class BpeError(RuntimeError):
 
 class Stats(ctypes.Structure):
     _fields_ = [
-        ('count_ms', ctypes.c_double), ('count_launches', ctypes.c_int64),
-        ('count_slots', ctypes.c_int64), ('select_ms', ctypes.c_double),
-        ('apply_ms', ctypes.c_double), ('apply_launches', ctypes.c_int64),
-        ('apply_slots', ctypes.c_int64), ('tie_passes', ctypes.c_int64),
+        ('step_ms', ctypes.c_double), ('step_launches', ctypes.c_int64),
+        ('step_slots', ctypes.c_int64), ('step_live', ctypes.c_int64),
+        ('select_ms', ctypes.c_double), ('tie_passes', ctypes.c_int64),
         ('iterations', ctypes.c_int64), ('live_tokens', ctypes.c_int64),
+        ('compactions', ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -94,6 +94,7 @@ def lib():
         'bpe_get_stats': ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         'bpe_reset_stats': ([vp], ctypes.c_int),
         'bpe_get_stream': ([vp, ctypes.POINTER(vp)], ctypes.c_int),
+        'bpe_recount': ([vp], ctypes.c_int),
         'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                               ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     }
@@ -233,6 +234,10 @@ class Engine:
         s = Stats()
         _check(lib().bpe_get_stats(self._ctx, ctypes.byref(s)), 'bpe_get_stats')
         return s.as_dict()
+
+    def recount(self):
+        """One plain streaming count pass (K1 alone; measurement helper)."""
+        _check(lib().bpe_recount(self._ctx), 'bpe_recount')
 
     def reset_stats(self):
         _check(lib().bpe_reset_stats(self._ctx), 'bpe_reset_stats')

@@ -1,14 +1,16 @@
 // bpe_engine.hip — libbpe: host side of the MI355X BPE merge-training engine + the C ABI of
 // include/bpe.h.  One context = one HIP device + one stream + one corpus shard in HBM.
 //
-// Per findNextMerge (core.ts:247-326):
-//   k_cold_clear -> k_count (K1) -> k_runs -> k_reduce_hot -> k_argmax_hot/cold (K2)
-//   -> k_collect -> [k_exact<TIE> when several pairs share (W, a+b)  (K3, rule R3)]
-// Per applyMerge (core.ts:332-360):
-//   k_exact<APPLY_COUNT> -> k_scan_regions -> k_exact<APPLY_SCATTER> (K4) into the ping-pong
-//   buffer, then swap.
+// The corpus is never compacted per merge: chunks stay left-packed and a merge rewrites only the
+// chunks it touches.  One streaming kernel (k_step) does both halves of an iteration:
+//   applyMerge(a, b, c)   (core.ts:332-360)  -> k_step<MERGE>: apply to every chunk, then count the
+//                                               post-merge pairs, k_runs, k_reduce_hot
+//   findNextMerge(opts)   (core.ts:247-326)  -> (k_step<plain> only if no counts are cached)
+//                                               k_argmax_hot/cold, k_collect, [k_tie (rule R3)]
+// so a mergeUntil iteration streams the corpus exactly once.
 #include "bpe_kernels.hip.h"
 #include "bpe.h"
+#include "bpe_tools.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -55,31 +57,34 @@ int dev_alloc(T **p, size_t n) {
 struct bpe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // corpus (slots: ids + SEP after every sample, padded with SEP)
+    // corpus: n_chunks left-packed chunks + one all-SEP spare chunk
     int32_t *d_ids = nullptr, *d_tmp = nullptr;
     int64_t cap_slots = 0;
-    int64_t n_slots = 0;
+    int64_t n_chunks = 0;
+    int64_t live_slots = 0;    // live slots (tokens + SEPs)
     int64_t n_samples = 0;
-    int64_t n_live = 0;
+    int64_t n_live = 0;        // live tokens
+    bool packed = true;        // live slots are a dense prefix (only the last chunk has a tail)
     // vocabulary
     std::vector<int32_t> h_len16;
     std::vector<int64_t> h_count;      // occurrences per token in the corpus (exact)
     int32_t *d_len16 = nullptr;
     int64_t cap_vocab = 0;
     bool len16_dirty = true;
-    // count state
+    // pass state
     uint32_t *d_partials = nullptr;
-    unsigned long long *d_spill = nullptr, *d_hot = nullptr;
-    RegionRun *d_runs = nullptr;
-    int64_t *d_carry = nullptr, *d_kept = nullptr, *d_outoff = nullptr;
+    unsigned long long *d_spill = nullptr, *d_hot = nullptr, *d_total = nullptr;
+    RegionSum *d_sums = nullptr;
+    RegionCarry *d_carry = nullptr;
+    int64_t *d_outoff = nullptr;
     Result *d_res = nullptr, *h_res = nullptr;
     int2 *d_cand = nullptr;
     ColdTable cold{};
-    uint32_t *d_cold_nused = nullptr;
+    uint32_t *d_cold_flags = nullptr;   // [0] n_used, [1] overflow
     uint64_t cold_cap = 0;
-    bool runs_valid = false;   // d_runs/d_carry describe the current corpus
-    // geometry of the last pass
-    int64_t n_chunks = 0, cpr = 0;
+    bool counts_valid = false;   // d_hot + cold table describe the current corpus
+    bool carry_valid = false;    // d_sums / d_carry describe the current corpus and geometry
+    int64_t cpr = 0;
     int R = 0, G = 0;
     // stats
     bool stats_on = false;
@@ -94,9 +99,16 @@ int set_device(bpe_ctx *c) {
     return BPE_OK;
 }
 
-// Ensures slot capacity for `need` slots plus one spare chunk of SEP padding (both buffers).
-int ensure_slots(bpe_ctx *c, int64_t need) {
-    const int64_t want = ((need + CHUNK - 1) / CHUNK + 2) * CHUNK;
+void geometry(bpe_ctx *c) {
+    const int64_t nc = std::max<int64_t>(1, c->n_chunks);
+    c->cpr = (nc + MAX_REGIONS - 1) / MAX_REGIONS;
+    c->R = (int)((nc + c->cpr - 1) / c->cpr);
+    c->G = (c->R + WAVES_PER_WG - 1) / WAVES_PER_WG;
+}
+
+// Capacity for `chunks` data chunks + the spare chunk, in both buffers.  Preserves the data.
+int ensure_chunks(bpe_ctx *c, int64_t chunks) {
+    const int64_t want = (chunks + 1) * CHUNK;
     if (want <= c->cap_slots) return BPE_OK;
     int64_t cap = std::max<int64_t>(want, c->cap_slots * 3 / 2);
     cap = (cap + CHUNK - 1) / CHUNK * CHUNK;
@@ -107,16 +119,30 @@ int ensure_slots(bpe_ctx *c, int64_t need) {
         dfree(ids);
         return rc;
     }
-    HIP_TRY(hipMemsetAsync(ids, 0xFF, cap * sizeof(int32_t), c->stream));
-    if (c->d_ids && c->n_slots)
-        HIP_TRY(hipMemcpyAsync(ids, c->d_ids, c->n_slots * sizeof(int32_t), hipMemcpyDeviceToDevice,
-                               c->stream));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ids, SEP, cap, c->stream));
+    if (c->d_ids && c->n_chunks)
+        HIP_TRY(hipMemcpyAsync(ids, c->d_ids, c->n_chunks * CHUNK * sizeof(int32_t),
+                               hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     dfree(c->d_ids);
     dfree(c->d_tmp);
     c->d_ids = ids;
     c->d_tmp = tmp;
     c->cap_slots = cap;
+    return BPE_OK;
+}
+
+// After writing live slots [0, live_slots) densely: TOMB to the end of the last chunk, SEP spare.
+int seal_packed(bpe_ctx *c) {
+    c->n_chunks = (c->live_slots + CHUNK - 1) / CHUNK;
+    const int64_t end = c->n_chunks * CHUNK;
+    if (end > c->live_slots)
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + c->live_slots), TOMB,
+                                  end - c->live_slots, c->stream));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + end), SEP, CHUNK, c->stream));
+    c->packed = true;
+    c->counts_valid = c->carry_valid = false;
+    geometry(c);
     return BPE_OK;
 }
 
@@ -145,23 +171,21 @@ int sync_len16(bpe_ctx *c) {
     return BPE_OK;
 }
 
-// Upper bound on distinct cold pairs: every counted occurrence with an id >= HOT involves at
-// least one cold-token occurrence, and every token occurrence is in at most two pairs.
-uint64_t cold_bound(const bpe_ctx *c) {
-    uint64_t s = 0;
+// Upper bound on distinct cold pairs in the next pass: every counted pair with an id >= HOT
+// involves a cold-token occurrence, and each occurrence sits in at most two pairs.  `extra` bounds
+// the occurrences of a token created by the pass itself.
+int ensure_cold(bpe_ctx *c, uint64_t extra) {
+    uint64_t s = extra;
     for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
-    uint64_t b = 2 * s + 16;
-    const uint64_t V = c->h_len16.size();
-    if (V > HOT) b = std::min<uint64_t>(b, V * V);
-    return std::min<uint64_t>(b, (uint64_t)c->n_live + 16);
-}
-
-int ensure_cold(bpe_ctx *c) {
-    uint64_t need = cold_bound(c);
+    uint64_t need = 2 * s + 16;
+    const uint64_t V = c->h_len16.size() + 1;
+    need = std::min<uint64_t>(need, V * V);
+    need = std::min<uint64_t>(need, (uint64_t)c->n_live + 16);
     uint64_t cap = 1024;
     while (cap < 2 * need) cap <<= 1;
     if (cap <= c->cold_cap) return BPE_OK;
     if (cap > (1ull << 31)) return fail(BPE_ERR_OOM, "bpe native: cold pair table too large");
+    HIP_TRY(hipStreamSynchronize(c->stream));
     dfree(c->cold.keys);
     dfree(c->cold.counts);
     dfree(c->cold.used);
@@ -171,22 +195,16 @@ int ensure_cold(bpe_ctx *c) {
     if ((rc = dev_alloc(&c->cold.used, cap))) return rc;
     HIP_TRY(hipMemsetAsync(c->cold.keys, 0xFF, cap * sizeof(uint32_t), c->stream));
     HIP_TRY(hipMemsetAsync(c->cold.counts, 0, cap * sizeof(uint32_t), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_cold_nused, 0, sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), c->stream));
     c->cold_cap = cap;
     c->cold.mask = (uint32_t)(cap - 1);
     int lg = 0;
     while ((1ull << lg) < cap) ++lg;
     c->cold.shift = 32 - lg;
-    c->cold.n_used = c->d_cold_nused;
-    c->cold.overflow = c->d_cold_nused + 1;
+    c->cold.n_used = c->d_cold_flags;
+    c->cold.overflow = c->d_cold_flags + 1;
+    c->counts_valid = false;
     return BPE_OK;
-}
-
-void geometry(bpe_ctx *c) {
-    c->n_chunks = std::max<int64_t>(1, (c->n_slots + CHUNK - 1) / CHUNK);
-    c->cpr = (c->n_chunks + MAX_REGIONS - 1) / MAX_REGIONS;
-    c->R = (int)((c->n_chunks + c->cpr - 1) / c->cpr);
-    c->G = (c->R + WAVES_PER_WG - 1) / WAVES_PER_WG;
 }
 
 float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -195,51 +213,96 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
-// One full count pass: K1 + run resolution + reduction; leaves d_hot and the cold table filled.
-int count_pass(bpe_ctx *c, int64_t max_length) {
+// One streaming pass: (optionally apply the merge a,b -> cc, then) count every pair, stitch the
+// region boundaries and reduce the hot table.  Leaves counts + carries valid for the new corpus.
+// With a merge, *replaced receives the number of replacements.
+int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
-    if ((rc = ensure_cold(c))) return rc;
-    if ((rc = sync_len16(c))) return rc;
+    uint64_t extra = 0;
+    if (merge) extra = (uint64_t)std::max<int64_t>(0, std::min(c->h_count[a], c->h_count[b]));
+    if ((rc = ensure_cold(c, extra))) return rc;
     geometry(c);
     hipStream_t s = c->stream;
     k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
-    HIP_TRY(hipMemsetAsync(c->d_cold_nused, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->d_spill, 0, HOT_BINS * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
-    const size_t lds = HIST_WORDS * sizeof(uint32_t);
-    if (max_length)
-        k_count<true><<<c->G, WG, lds, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_len16,
-                                            max_length, c->d_partials, c->d_spill, c->cold,
-                                            c->d_runs);
+    if (merge)
+        k_step<true><<<c->G, WG, STEP_LDS, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a,
+                                                b, cc, c->d_partials, c->d_spill, c->cold,
+                                                c->d_sums, &c->d_res->replaced);
     else
-        k_count<false><<<c->G, WG, lds, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_len16, 0,
-                                             c->d_partials, c->d_spill, c->cold, c->d_runs);
+        k_step<false><<<c->G, WG, STEP_LDS, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
+                                                 -1, -1, -1, c->d_partials, c->d_spill, c->cold,
+                                                 c->d_sums, &c->d_res->replaced);
     HIP_TRY(hipGetLastError());
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
-    k_runs<<<(c->R + 255) / 256, 256, 0, s>>>(c->d_runs, c->R, c->d_carry, c->d_len16, max_length,
-                                              max_length ? 1 : 0, c->d_spill, c->cold, 1);
+    k_runs<<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill, c->cold);
     k_reduce_hot<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
     HIP_TRY(hipGetLastError());
-    c->runs_valid = true;
+    uint32_t flags[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[2], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    if (c->stats_on) {
+        c->stats.step_ms += ev_ms(c->ev[0], c->ev[1]);
+        c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
+        c->stats.step_launches += 1;
+        c->stats.step_slots += c->n_chunks * CHUNK;
+        c->stats.step_live += c->n_live;
+    }
+    if (merge) {
+        const int64_t R = (int64_t)c->h_res->replaced;
+        c->n_live -= R;
+        c->live_slots -= R;
+        c->h_count[a] -= R;
+        c->h_count[b] -= R;
+        c->h_count[cc] += R;
+        if (R) c->packed = false;
+        if (replaced) *replaced = R;
+    }
+    c->counts_valid = true;
+    c->carry_valid = true;
     return BPE_OK;
 }
 
-// Run info only (for an apply without a preceding find on the same corpus, e.g. restoreMerge).
-int runs_pass(bpe_ctx *c) {
-    return count_pass(c, 0);
+// Moves the live slots to a dense prefix (when dead slots waste too much of the stream, and
+// before appending to a merged corpus).  Needs valid region sums; leaves counts valid (they do
+// not depend on the layout) but invalidates the carries (the geometry changes).
+int compact(bpe_ctx *c) {
+    int rc;
+    if (c->packed) return BPE_OK;
+    if (!c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    hipStream_t s = c->stream;
+    k_scan_live<<<1, 1024, 0, s>>>(c->d_sums, c->R, c->d_outoff, c->d_total);
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
+    k_compact<<<(c->R + 3) / 4, 256, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_outoff,
+                                             c->d_tmp);
+    HIP_TRY(hipGetLastError());
+    unsigned long long total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if ((int64_t)total != c->live_slots)
+        return fail(BPE_ERR_STATE, "bpe native: compaction lost slots");
+    std::swap(c->d_ids, c->d_tmp);
+    const bool counts = c->counts_valid;
+    if ((rc = seal_packed(c))) return rc;
+    c->counts_valid = counts;
+    if (c->stats_on) c->stats.compactions += 1;
+    return BPE_OK;
 }
 
-int exact_args(bpe_ctx *c, ExactArgs &A) {
-    memset(&A, 0, sizeof A);
-    A.ids = c->d_ids;
-    A.n_chunks = c->n_chunks;
-    A.cpr = c->cpr;
-    A.n_slots = c->n_slots;
-    A.R = c->R;
-    A.carry_off = c->d_carry;
-    A.res = c->d_res;
-    return BPE_OK;
+int maybe_compact(bpe_ctx *c) {
+    const int64_t slots = c->n_chunks * CHUNK;
+    if (c->packed || slots < (1 << 20)) return BPE_OK;
+    if (c->live_slots * 4 >= slots * 3) return BPE_OK;   // keep while >= 75% of slots are live
+    int rc = compact(c);
+    if (rc) return rc;
+    return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout
 }
 
 int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int32_t *b,
@@ -247,31 +310,30 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
     if (c->n_live < 2) return BPE_NO_MERGE;
     int rc;
-    if ((rc = count_pass(c, max_length))) return rc;
+    if (!c->counts_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    if ((rc = sync_len16(c))) return rc;
     hipStream_t s = c->stream;
-    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_res);
-    k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_res);
-    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->cold, c->d_res, c->d_cand);
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res);
+    k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
+    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length, c->d_res,
+                                             c->d_cand);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    uint32_t ovf = 0;
-    HIP_TRY(hipMemcpyAsync(&ovf, c->cold.overflow, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[2], s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (ovf) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
     if (c->stats_on) {
-        c->stats.count_ms += ev_ms(c->ev[0], c->ev[1]);
-        c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
-        c->stats.count_launches += 1;
-        c->stats.count_slots += c->n_chunks * CHUNK;
+        c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
         c->stats.iterations += 1;
         c->stats.live_tokens += c->n_live;
     }
-    const Result &R = *c->h_res;
-    if (R.best == 0) return BPE_NO_MERGE;                             // core.ts:312
-    const int64_t W = (int64_t)(R.best >> 17);
-    if (W < min_weight) return BPE_NO_MERGE;                          // core.ts:313
-    const unsigned n_cand = R.n_cand;
+    const Result res = *c->h_res;
+    if (res.best == 0) return BPE_NO_MERGE;                            // core.ts:312
+    const int64_t W = (int64_t)(res.best >> 17);
+    if (W < min_weight) return BPE_NO_MERGE;                           // core.ts:313
+    const unsigned n_cand = res.n_cand;
     if (n_cand == 0 || n_cand > (unsigned)CAND_CAP)
         return fail(BPE_ERR_STATE, "bpe native: bad candidate count");
     std::vector<int2> cand(n_cand);
@@ -284,16 +346,22 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
         unsigned long long best_pos = ~0ull;
         for (unsigned j0 = 0; j0 < n_cand; j0 += MAX_CAND) {
             const unsigned nb = std::min<unsigned>(MAX_CAND, n_cand - j0);
-            ExactArgs A;
-            exact_args(c, A);
+            TieArgs A;
+            memset(&A, 0, sizeof A);
+            A.ids = c->d_ids;
+            A.n_chunks = c->n_chunks;
+            A.cpr = c->cpr;
+            A.R = c->R;
             A.n_cand = (int)nb;
+            A.carry = c->d_carry;
+            A.res = c->d_res;
             for (unsigned j = 0; j < nb; ++j) {
                 A.ca[j] = cand[j0 + j].x;
                 A.cb[j] = cand[j0 + j].y;
             }
             HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
             if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
-            k_exact<TIE><<<(c->R + 3) / 4, 256, 0, s>>>(A);
+            k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
             if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
@@ -329,50 +397,19 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     if ((rc = ensure_vocab(c, (int64_t)cc + 1))) return rc;
     c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                   // core.ts:318
     c->len16_dirty = true;
-    if (c->n_live < 2) {
-        if (replaced) *replaced = 0;
-        return BPE_OK;
-    }
-    if (!c->runs_valid)
-        if ((rc = runs_pass(c))) return rc;
-    geometry(c);
-    hipStream_t s = c->stream;
-    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-    ExactArgs A;
-    exact_args(c, A);
-    A.a = a;
-    A.b = b;
-    A.c = cc;
-    A.kept = c->d_kept;
-    A.out_off = c->d_outoff;
-    A.out = c->d_tmp;
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
-    k_exact<APPLY_COUNT><<<(c->R + 3) / 4, 256, 0, s>>>(A);
-    k_scan_regions<<<1, 1024, 0, s>>>(c->d_kept, c->R, c->d_outoff, c->d_res);
-    k_exact<APPLY_SCATTER><<<(c->R + 3) / 4, 256, 0, s>>>(A);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const int64_t kept = (int64_t)c->h_res->kept_total;
-    const int64_t R = (int64_t)c->h_res->replaced;
-    // SEP padding after the compacted corpus (at least one spare chunk)
-    const int64_t pad_end = ((kept + CHUNK - 1) / CHUNK + 1) * CHUNK;
-    HIP_TRY(hipMemsetAsync(c->d_tmp + kept, 0xFF, (pad_end - kept) * sizeof(int32_t), s));
-    std::swap(c->d_ids, c->d_tmp);
-    c->n_slots = kept;
-    c->n_live -= R;
-    c->h_count[a] -= R;
-    c->h_count[b] -= R;
-    c->h_count[cc] += R;
-    c->runs_valid = false;
-    if (c->stats_on) {
-        c->stats.apply_ms += ev_ms(c->ev[0], c->ev[1]);
-        c->stats.apply_launches += 1;
-        c->stats.apply_slots += c->n_chunks * CHUNK;
-    }
-    if (replaced) *replaced = R;
-    return BPE_OK;
+    if (replaced) *replaced = 0;
+    if (c->n_live < 2) return BPE_OK;
+    if (!c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    if ((rc = run_pass(c, true, a, b, cc, replaced))) return rc;
+    return maybe_compact(c);
+}
+
+int append_begin(bpe_ctx *c, int64_t extra_slots) {
+    int rc;
+    if (!c->packed)
+        if ((rc = compact(c))) return rc;
+    return ensure_chunks(c, (c->live_slots + extra_slots + CHUNK - 1) / CHUNK);
 }
 
 }  // namespace
@@ -382,7 +419,7 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
 // ================================================================================================
 extern "C" {
 
-int bpe_version(void) { return 100; }
+int bpe_version(void) { return 200; }
 
 int bpe_last_error(char *buf, size_t cap) {
     if (!buf || !cap) return BPE_ERR_ARG;
@@ -420,27 +457,26 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = dev_alloc(&c->d_partials, (size_t)MAX_WG * HIST_WORDS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_spill, HOT_BINS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_hot, HOT_BINS))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_runs, MAX_REGIONS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_total, 2))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_sums, MAX_REGIONS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_carry, MAX_REGIONS))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_kept, MAX_REGIONS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_outoff, MAX_REGIONS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_res, 1))) return bail(rc);
     if ((rc = dev_alloc(&c->d_cand, CAND_CAP))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_cold_nused, 4))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_cold_flags, 4))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
-    if (hipMemset(c->d_cold_nused, 0, 16) != hipSuccess)
+    if (hipMemset(c->d_cold_flags, 0, 16) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
-    if ((rc = ensure_slots(c, 0))) return bail(rc);
+    if ((rc = ensure_chunks(c, 1))) return bail(rc);
     if ((rc = ensure_vocab(c, 0))) return bail(rc);
-    if ((rc = ensure_cold(c))) return bail(rc);
-    if (hipFuncSetAttribute((const void *)k_count<true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            HIST_WORDS * sizeof(uint32_t)) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_count<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            HIST_WORDS * sizeof(uint32_t)) != hipSuccess)
-        return bail(fail(BPE_ERR_HIP, "bpe native: cannot reserve 128 KiB of LDS"));
+    if ((rc = ensure_cold(c, 0))) return bail(rc);
+    if (hipFuncSetAttribute((const void *)k_step<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)STEP_LDS) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_step<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)STEP_LDS) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: cannot reserve 144 KiB of LDS"));
+    if ((rc = seal_packed(c))) return bail(rc);
     *out = c;
     return BPE_OK;
 }
@@ -450,10 +486,9 @@ int bpe_destroy(bpe_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
-                    c->d_runs, c->d_carry, c->d_kept, c->d_outoff, c->d_res, c->d_cand, c->d_cold_nused,
-                    c->cold.keys, c->cold.counts, c->cold.used};
-    for (void *p : ptrs)
-        dfree(p);
+                    c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
+                    c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used};
+    for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -493,15 +528,17 @@ int bpe_add_sample(bpe_ctx *c, const int32_t *ids, int64_t n) {
         mx = std::max(mx, ids[i]);
     }
     if ((rc = ensure_vocab(c, (int64_t)mx + 1))) return rc;
-    if ((rc = ensure_slots(c, c->n_slots + n + 1))) return rc;
-    if (n) HIP_TRY(hipMemcpy(c->d_ids + c->n_slots, ids, n * sizeof(int32_t), hipMemcpyHostToDevice));
-    const int32_t sep = SEP;
-    HIP_TRY(hipMemcpy(c->d_ids + c->n_slots + n, &sep, sizeof(int32_t), hipMemcpyHostToDevice));
+    if ((rc = append_begin(c, n + 1))) return rc;
+    std::vector<int32_t> buf(ids, ids + n);
+    buf.push_back(SEP);
+    HIP_TRY(hipMemcpyAsync(c->d_ids + c->live_slots, buf.data(), buf.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, c->stream));
     for (int64_t i = 0; i < n; ++i) c->h_count[ids[i]] += 1;
-    c->n_slots += n + 1;
+    c->live_slots += n + 1;
     c->n_samples += 1;
     c->n_live += n;
-    c->runs_valid = false;
+    if ((rc = seal_packed(c))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return BPE_OK;
 }
 
@@ -517,6 +554,7 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
     }
     if (sample_bytes == 0 || sample_bytes > n) sample_bytes = n;
     const int64_t n_smp = (n + sample_bytes - 1) / sample_bytes;
+    if ((rc = append_begin(c, n + n_smp))) return rc;
     hipStream_t s = c->stream;
     uint8_t *d_bytes = nullptr;
     unsigned long long *d_stats = nullptr;   // first[256] + hist[256]
@@ -528,6 +566,7 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
         return rc;
     }
     auto cleanup = [&]() {
+        (void)hipStreamSynchronize(s);
         dfree(d_bytes);
         dfree(d_stats);
         dfree(d_map);
@@ -576,23 +615,21 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
     *n_tokens_io = next;
     if (char_hist)
         for (int ch = 0; ch < 256; ++ch) char_hist[ch] = (int64_t)st[256 + ch];
-    if ((rc = ensure_slots(c, c->n_slots + n + n_smp))) {
-        cleanup();
-        return rc;
-    }
     if (hipMemcpyAsync(d_map, char_to_id, 256 * sizeof(int32_t), hipMemcpyHostToDevice, s) !=
         hipSuccess) {
         cleanup();
         return fail(BPE_ERR_HIP, "bpe native: map upload failed");
     }
-    k_expand_latin1<<<4096, 256, 0, s>>>(d_bytes, n, sample_bytes, d_map, c->d_ids + c->n_slots);
-    hipError_t e = hipStreamSynchronize(s);
+    k_expand_latin1<<<4096, 256, 0, s>>>(d_bytes, n, sample_bytes, d_map,
+                                         c->d_ids + c->live_slots);
+    hipError_t e = hipGetLastError();
     cleanup();
     if (e != hipSuccess) return fail(BPE_ERR_HIP, "bpe native: latin1 expand failed");
-    c->n_slots += n + n_smp;
+    c->live_slots += n + n_smp;
     c->n_samples += n_smp;
     c->n_live += n;
-    c->runs_valid = false;
+    if ((rc = seal_packed(c))) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
     return BPE_OK;
 }
 
@@ -600,12 +637,10 @@ int bpe_clear_corpus(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(c->d_ids, 0xFF, c->cap_slots * sizeof(int32_t), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_tmp, 0xFF, c->cap_slots * sizeof(int32_t), c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    c->n_slots = c->n_samples = c->n_live = 0;
+    c->live_slots = c->n_samples = c->n_live = 0;
     std::fill(c->h_count.begin(), c->h_count.end(), 0);
-    c->runs_valid = false;
+    if ((rc = seal_packed(c))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return BPE_OK;
 }
 
@@ -623,14 +658,22 @@ int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *samp
         return fail(BPE_ERR_ARG, "bpe native: read_corpus buffers too small");
     int rc = set_device(c);
     if (rc) return rc;
-    std::vector<int32_t> slots(c->n_slots);
-    if (c->n_slots)
-        HIP_TRY(hipMemcpy(slots.data(), c->d_ids, c->n_slots * sizeof(int32_t), hipMemcpyDeviceToHost));
+    const int64_t slots = c->n_chunks * CHUNK;
+    std::vector<int32_t> buf(slots);
+    if (slots)
+        HIP_TRY(hipMemcpy(buf.data(), c->d_ids, slots * sizeof(int32_t), hipMemcpyDeviceToHost));
     int64_t o = 0, sidx = 0;
     sample_off[0] = 0;
-    for (int64_t i = 0; i < c->n_slots; ++i) {
-        if (slots[i] == SEP) sample_off[++sidx] = o;
-        else ids_out[o++] = slots[i];
+    for (int64_t i = 0; i < slots; ++i) {
+        const int32_t v = buf[i];
+        if (v == TOMB) continue;
+        if (v == SEP) {
+            if (sidx >= c->n_samples) return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
+            sample_off[++sidx] = o;
+        } else {
+            if (o >= c->n_live) return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
+            ids_out[o++] = v;
+        }
     }
     if (sidx != c->n_samples || o != c->n_live)
         return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
@@ -696,6 +739,13 @@ int bpe_reset_stats(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     memset(&c->stats, 0, sizeof c->stats);
     return BPE_OK;
+}
+
+int bpe_recount(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return run_pass(c, false, 0, 0, 0, nullptr);
 }
 
 int bpe_get_stream(bpe_ctx *c, void **stream) {

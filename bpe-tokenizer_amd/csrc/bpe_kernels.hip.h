@@ -3,23 +3,29 @@
 // Reference semantics: /root/reference/core.ts findNextMerge (247-326) and applyMerge (332-360);
 // order-free restatement in SURVEY.md Appendix A (R1-R5).
 //
-// Corpus layout in HBM: one flat int32 slot array.  Every sample (one `corpus_in_code` element,
-// core.ts:106) is stored as its token ids followed by one SEP (-1) slot.  The array is padded with
-// SEP to a whole number of 256-slot chunks plus one spare chunk, so a chunk's "next token" load is
-// always in bounds.
+// Corpus layout in HBM: one int32 slot array cut into 256-slot *chunks*.  Every sample (one
+// `corpus_in_code` element, core.ts:106) is its token ids followed by one SEP (-1).  Every chunk is
+// LEFT-PACKED: its live slots (tokens and SEPs) come first, dead slots (TOMB, -2) fill the tail.
+// The logical corpus is the concatenation of the chunks' live prefixes.  A merge therefore never
+// moves data between chunks: it rewrites only the chunks that contain a match (1 KiB each).  A
+// spare all-SEP chunk follows the last chunk so "first slot of the next chunk" loads stay in range.
 //
-// Work decomposition: the chunks are cut into R contiguous *regions*; one wave (64 lanes) owns
-// one region and streams it chunk by chunk (lane L holds slots 4L..4L+3 of the chunk as one int4
-// — a 1 KiB fully coalesced load per wave-instruction).  The only state crossing chunk
-// boundaries is the open run of equal tokens (needed for the `X X X` skip rule, core.ts:285-290);
-// it is carried in wave-uniform registers inside a region and resolved between regions by k_runs.
+// Work decomposition: the chunks are cut into R contiguous *regions*; one wave (64 lanes) owns one
+// region and streams it chunk by chunk (lane L holds slots 4L..4L+3 as one int4: a 1 KiB fully
+// coalesced load per wave-instruction).  Inside a region the state that crosses chunks (the open
+// run of equal tokens behind the `X X X` skip rule, core.ts:285-290) lives in wave-uniform
+// registers.  Across regions nothing is shared during a pass: each wave writes a RegionSum and
+// k_runs stitches the boundaries (the pair straddling each boundary, runs crossing regions, and
+// the carries the next pass needs).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace bpe {
 
-constexpr int32_t SEP = -1;
+constexpr int32_t SEP = -1;                 // sample separator (live slot, never in a pair)
+constexpr int32_t TOMB = -2;                // dead slot in a chunk tail
+constexpr int32_t NONE = -3;                // "no token" (register sentinel only)
 constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x int4)
 constexpr int WAVES_PER_WG = 16;
 constexpr int WG = WAVES_PER_WG * 64;       // 1024 threads, one workgroup per CU (LDS-bound)
@@ -28,15 +34,29 @@ constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
 constexpr int HOT = 256;                    // ids < HOT form the dense LDS histogram
 constexpr int HOT_BINS = HOT * HOT;
 constexpr int HIST_WORDS = HOT_BINS / 2;    // two 16-bit counters per LDS dword (128 KiB)
-constexpr int MAX_CAND = 16;               // candidates resolved per tie pass
+constexpr int PACK_INTS = CHUNK;            // per-wave LDS staging for re-packing a chunk
+constexpr size_t STEP_LDS = HIST_WORDS * 4 + WAVES_PER_WG * PACK_INTS * 4;   // 144 KiB
+constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 
-struct RegionRun {
-    int64_t head_len;   // leading slots equal to the token before the region (continued run)
-    int64_t tail_len;   // length (inside the region) of a run still open at the region end
-    int32_t tail_x;     // token of that open run, -1 when none
-    int32_t uniform;    // 1 when the whole region continues the previous region's run
+// What one pass learned about its region of the (post-merge) corpus.  Live slots only.
+struct RegionSum {
+    int64_t n_live;      // live slots (tokens + SEPs)
+    int64_t lead_len;    // length of the first run (deferred to k_runs)
+    int64_t trail_len;   // length of the last run (deferred to k_runs)
+    int32_t first_tok;   // first live slot value (NONE when the region is empty)
+    int32_t last_tok;    // last live slot value
+    int32_t uniform;     // the region is one single run (lead == trail == whole region)
+    int32_t pad;
+};
+
+// Boundary facts k_runs derives for the NEXT pass over the same corpus.
+struct RegionCarry {
+    int64_t carry_off;   // run offset of the region's first live token (0 unless its run began
+                         // in an earlier region)
+    int32_t prev_tok;    // last live slot before the region (SEP at the corpus start)
+    int32_t next_tok;    // first live slot after the region (SEP at the corpus end)
 };
 
 // Sparse pair table for pairs with an id >= HOT: open addressing on key = a << 16 | b.
@@ -51,12 +71,12 @@ struct ColdTable {
 };
 
 struct Result {
-    unsigned long long best;     // packed (W << 17) | (0x1FFFF - c_index), 0 = no pair
+    unsigned long long best;             // packed (W << 17) | (0x1FFFF - c_index), 0 = none
     unsigned int n_cand;                 // pairs sharing the best packed key (list in `cand`)
     unsigned int pad0;
-    unsigned long long last[MAX_CAND];   // R3: position + 1 of the last counted occurrence
+    unsigned long long last[MAX_CAND];   // R3: slot + 1 of the last counted occurrence
     unsigned long long replaced;         // apply: replacement count
-    unsigned long long kept_total;       // apply: slots after compaction
+    unsigned long long pad1;
 };
 
 __device__ __forceinline__ unsigned long long pack_key(unsigned long long w, int32_t a, int32_t b) {
@@ -68,6 +88,15 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     for (int d = 32; d >= 1; d >>= 1) {
         unsigned long long o = __shfl_xor(v, d);
         v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int o = __shfl_up(v, d);
+        if (lane >= d) v += o;
     }
     return v;
 }
@@ -101,12 +130,12 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint
     }
 }
 
-// Adds n to count(x, x) for a run resolved outside the LDS histogram.
-__device__ __forceinline__ void add_run_pairs(int32_t x, unsigned long long n,
-                                              unsigned long long *spill, const ColdTable &ct) {
+// Adds n occurrences of (x, y) outside the LDS histogram (boundary pairs, resolved runs).
+__device__ __forceinline__ void add_pairs_global(int32_t x, int32_t y, unsigned long long n,
+                                                 unsigned long long *spill, const ColdTable &ct) {
     if (n == 0) return;
-    if (x < HOT) atomicAdd(&spill[x * HOT + x], n);
-    else cold_add(ct, ((uint32_t)x << 16) | (uint32_t)x, (uint32_t)n);
+    if ((uint32_t)x < HOT && (uint32_t)y < HOT) atomicAdd(&spill[x * HOT + y], n);
+    else cold_add(ct, ((uint32_t)x << 16) | (uint32_t)y, (uint32_t)n);
 }
 
 // One counted occurrence of (x, y).  Hot pairs go to the workgroup's packed 16-bit LDS counters;
@@ -127,37 +156,79 @@ __device__ __forceinline__ void count_pair(uint32_t *hist, int32_t x, int32_t y,
     }
 }
 
-// Per-chunk neighbourhood of one lane: t[0..3] its slots, t[4] the next slot, pm the previous.
-struct Chunk {
-    int32_t t[5];
-    bool eqn[4];   // t[e] == t[e+1], non-SEP  (an X X pair at e)
-    bool eqp[4];   // t[e] == t[e-1], non-SEP  (e continues a run)
+// ---------------------------------------------------------------------------------------------
+// A left-packed chunk as seen by one lane: slots k = 4*lane + e, live iff k < len.
+// ---------------------------------------------------------------------------------------------
+struct View {
+    int32_t t[4];
+    int len;
 };
 
-__device__ __forceinline__ void load_chunk(Chunk &ck, const int4 v, int32_t nxt, int32_t prev,
-                                           int lane) {
-    const int32_t up = __shfl_up(v.w, 1);
-    const int32_t dn = __shfl_down(v.x, 1);
-    ck.t[0] = v.x;
-    ck.t[1] = v.y;
-    ck.t[2] = v.z;
-    ck.t[3] = v.w;
-    ck.t[4] = lane == 63 ? nxt : dn;
-    const int32_t pm = lane == 0 ? prev : up;
-    ck.eqp[0] = ck.t[0] == pm && ck.t[0] != SEP;
-#pragma unroll
-    for (int e = 1; e < 4; ++e) ck.eqp[e] = ck.t[e] == ck.t[e - 1] && ck.t[e] != SEP;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ck.eqn[e] = ck.t[e] == ck.t[e + 1] && ck.t[e] != SEP;
+__device__ __forceinline__ View make_view(const int4 v) {
+    View w;
+    w.t[0] = v.x;
+    w.t[1] = v.y;
+    w.t[2] = v.z;
+    w.t[3] = v.w;
+    // chunks are left-packed, so len = number of non-TOMB slots
+    w.len = __popcll(__ballot(v.x != TOMB)) + __popcll(__ballot(v.y != TOMB)) +
+            __popcll(__ballot(v.z != TOMB)) + __popcll(__ballot(v.w != TOMB));
+    return w;
 }
 
-// Run-start scan: rs[e] = chunk index of the start of the run containing slot 4*lane+e, or -1
-// when that run began before the chunk.  Returns rs of slot 255 (broadcast).
-__device__ __forceinline__ int run_starts(const Chunk &ck, int lane, int rs[4]) {
+template <typename T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int e) {
+    return e == 0 ? a[0] : e == 1 ? a[1] : e == 2 ? a[2] : a[3];
+}
+
+// Broadcast of lane `src` (wave-uniform) through v_readlane.
+__device__ __forceinline__ int32_t bcast(int32_t v, int src) {
+    return __builtin_amdgcn_readlane(v, src);
+}
+
+__device__ __forceinline__ int64_t bcast64(int64_t v, int src) {
+    const int32_t lo = __builtin_amdgcn_readlane((int32_t)(v & 0xFFFFFFFF), src);
+    const int32_t hi = __builtin_amdgcn_readlane((int32_t)(v >> 32), src);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Token at chunk index k (wave-uniform k), broadcast.
+__device__ __forceinline__ int32_t view_at(const View &w, int k) {
+    return bcast(pick4(w.t, k & 3), k >> 2);
+}
+
+// Neighbourhood of each live slot: partner = next live token (the pair's right side), prev.
+struct Nbr {
+    int32_t partner[4];
+    bool live[4];
+    bool eqn[4];   // live, non-SEP, equal to partner  (an X X pair starts here)
+    bool eqp[4];   // live, non-SEP, equal to the previous live token (continues a run)
+};
+
+__device__ __forceinline__ void neighbours(const View &w, int32_t prev, int32_t nxt, int lane,
+                                           Nbr &n) {
+    const int32_t up = __shfl_up(w.t[3], 1);
+    const int32_t dn = __shfl_down(w.t[0], 1);
+    const int32_t pm = lane == 0 ? prev : up;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k = 4 * lane + e;
+        n.live[e] = k < w.len;
+        const int32_t right = e < 3 ? w.t[e + 1] : dn;
+        n.partner[e] = (k + 1 < w.len) ? right : nxt;
+        const int32_t left = e == 0 ? pm : w.t[e - 1];
+        n.eqp[e] = n.live[e] && w.t[e] >= 0 && w.t[e] == left;
+        n.eqn[e] = n.live[e] && w.t[e] >= 0 && w.t[e] == n.partner[e];
+    }
+}
+
+// Run-start scan over the live prefix: rs[e] = chunk index of the start of the run containing
+// slot 4*lane+e, or -1 when that run began before the chunk.
+__device__ __forceinline__ void run_starts(const Nbr &n, int lane, int rs[4]) {
     int lmax = -1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        if (!ck.eqp[e]) lmax = 4 * lane + e;
+        if (n.live[e] && !n.eqp[e]) lmax = 4 * lane + e;
         rs[e] = lmax;
     }
     int incl = lmax;
@@ -170,14 +241,13 @@ __device__ __forceinline__ int run_starts(const Chunk &ck, int lane, int rs[4]) 
     if (lane == 0) excl = -1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) rs[e] = rs[e] > excl ? rs[e] : excl;
-    return __shfl(rs[3], 63);
 }
 
-__device__ __forceinline__ int first_start(const Chunk &ck) {
-    int f = CHUNK;
+__device__ __forceinline__ int first_start(const Nbr &n, int len) {
+    int f = len;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        unsigned long long m = __ballot(!ck.eqp[e]);
+        unsigned long long m = __ballot(n.live[e] && !n.eqp[e]);
         if (m) {
             int k = 4 * __builtin_ctzll(m) + e;
             f = k < f ? k : f;
@@ -186,18 +256,192 @@ __device__ __forceinline__ int first_start(const Chunk &ck) {
     return f;
 }
 
+// Exact run offsets of the live slots (needed where X X pairs are matched / located exactly).
+// prev_off = offset of the live token before the chunk (valid when slot 0 continues its run).
+// Returns the offset of the last live slot (the next chunk's prev_off).
+__device__ __forceinline__ int64_t run_offsets(const View &w, const Nbr &n, int lane,
+                                               int64_t prev_off, int64_t (&off)[4]) {
+    bool slow = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) slow |= n.eqn[e] && n.eqp[e];
+    if (__ballot(slow) == 0ull) {
+        // every X X slot starts its run (offset 0); a run reaching the next chunk starts at the
+        // last live slot, so the carried offset is 0 whenever it is used
+#pragma unroll
+        for (int e = 0; e < 4; ++e) off[e] = 0;
+        return 0;
+    }
+    int rs[4];
+    run_starts(n, lane, rs);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k = 4 * lane + e;
+        off[e] = rs[e] >= 0 ? (int64_t)(k - rs[e]) : prev_off + 1 + k;
+    }
+    const int kl = w.len - 1;
+    return bcast64(pick4(off, kl & 3), kl >> 2);
+}
+
 // ---------------------------------------------------------------------------------------------
-// K1 pair count.  Counts every counted occurrence (R1) of every pair: hot pairs in LDS, cold
-// pairs in the sparse table.  X X pairs of runs that cross a chunk boundary are deferred and
-// added once when the run closes (floor(L/2), ≡ the skip rule core.ts:285-290); runs crossing a
-// region boundary are summarised in `runs` and resolved by k_runs.
+// Count-side state of one region (wave-uniform).
 // ---------------------------------------------------------------------------------------------
-template <bool FILTER>
+struct CountState {
+    int32_t prev;        // last live post-merge token counted so far (NONE at region start)
+    int32_t run_x;       // open run carried across chunks (-2: none)
+    int64_t run_len;
+    bool run_lead;       // the open run is the region's first run (deferred to k_runs)
+    bool started;
+    int64_t lead_len;
+    int64_t n_live;
+    int32_t first_tok;
+};
+
+// Counts the pairs of one post-merge chunk whose right side is inside the region: every pair
+// (k, next live) except X X pairs of the region's first and last run, which k_runs resolves.
+// nxt = first live token of the next non-empty chunk of the region, NONE for the region's last.
+__device__ __forceinline__ void lds_spill_fix(uint32_t *hist, int bin, uint32_t old,
+                                              unsigned long long *spill) {
+    const uint32_t sh = (bin & 1) << 4;
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+        atomicSub(&hist[bin >> 1], 0x8000u << sh);
+        atomicAdd(&spill[bin], 0x8000ull);
+    }
+}
+
+__device__ __forceinline__ uint32_t lds_inc(uint32_t *hist, int bin) {
+    return atomicAdd(&hist[bin >> 1], 1u << ((bin & 1) << 4));
+}
+
+__device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last, int lane,
+                                           CountState &s, uint32_t *hist,
+                                           unsigned long long *spill, const ColdTable &ct) {
+    if (!last && s.run_x == -2 && s.started && w.len == CHUNK) {
+        // Fast path: a full chunk with no run open across its start.  Valid when no slot is the
+        // middle of a run of >= 3 and no X X pair straddles the chunk end: then every X X pair
+        // starts its run and counts (core.ts:285-290 never skips).
+        const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
+        const int32_t up = __shfl_up(t3, 1);
+        const int32_t dn = __shfl_down(t0, 1);
+        const int32_t p = lane == 0 ? s.prev : up;
+        const int32_t t4 = lane == 63 ? nxt : dn;
+        const bool e01 = t0 == t1, e12 = t1 == t2, e23 = t2 == t3, e34 = t3 == t4;
+        const bool trip = (p == t0 && e01) || (e01 && e12) || (e12 && e23) || (e23 && e34) ||
+                          (lane == 63 && e34 && t3 >= 0);
+        if (__ballot(trip) == 0ull) {
+            const uint32_t all = (uint32_t)(t0 | t1 | t2 | t3 | t4);
+            if (__ballot(all >= (uint32_t)HOT) == 0ull) {
+                // all four pairs valid and hot: four LDS atomics in flight, one overflow test
+                const int b0 = t0 * HOT + t1, b1 = t1 * HOT + t2, b2 = t2 * HOT + t3,
+                          b3 = t3 * HOT + t4;
+                const uint32_t o0 = lds_inc(hist, b0), o1 = lds_inc(hist, b1),
+                               o2 = lds_inc(hist, b2), o3 = lds_inc(hist, b3);
+                const uint32_t lim = 0x7FFFu;
+                const bool ovf = ((o0 >> ((b0 & 1) << 4)) & 0xFFFFu) == lim ||
+                                 ((o1 >> ((b1 & 1) << 4)) & 0xFFFFu) == lim ||
+                                 ((o2 >> ((b2 & 1) << 4)) & 0xFFFFu) == lim ||
+                                 ((o3 >> ((b3 & 1) << 4)) & 0xFFFFu) == lim;
+                if (ovf) {
+                    lds_spill_fix(hist, b0, o0, spill);
+                    lds_spill_fix(hist, b1, o1, spill);
+                    lds_spill_fix(hist, b2, o2, spill);
+                    lds_spill_fix(hist, b3, o3, spill);
+                }
+            } else {
+                const int32_t x[5] = {t0, t1, t2, t3, t4};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if ((x[e] | x[e + 1]) >= 0) count_pair(hist, x[e], x[e + 1], spill, ct);
+            }
+            s.n_live += CHUNK;
+            s.prev = bcast(t3, 63);
+            return;
+        }
+    }
+    if (!s.started) {
+        s.started = true;
+        s.first_tok = view_at(w, 0);
+        if (s.first_tok >= 0) {
+            // the first run is carried from "before" the chunk so that it is never counted here
+            s.prev = s.first_tok;
+            s.run_x = s.first_tok;
+            s.run_len = 0;
+            s.run_lead = true;
+        } else {
+            s.lead_len = 1;   // a SEP: a run of its own that never pairs
+        }
+    }
+    Nbr n;
+    neighbours(w, s.prev, nxt, lane, n);
+    s.n_live += w.len;
+    const int kl = w.len - 1;
+    bool slow = last || s.run_x != -2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) slow |= n.eqn[e] && (n.eqp[e] || 4 * lane + e == kl);
+    bool counted[4];
+    if (__ballot(slow) == 0ull) {
+        // no run crosses the chunk and every run is <= 2 long: every valid pair counts
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            counted[e] = n.live[e] && w.t[e] >= 0 && n.partner[e] >= 0;
+    } else {
+        int rs[4];
+        run_starts(n, lane, rs);
+        const int rs_l = bcast(pick4(rs, kl & 3), kl >> 2);
+        const bool eqn_l = ((__ballot(pick4(n.eqn, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
+        const bool end_open = last || eqn_l;   // the last run continues past the chunk / is deferred
+        const int f = first_start(n, w.len);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            bool ok = n.live[e] && w.t[e] >= 0 && n.partner[e] >= 0;
+            if (ok && n.eqn[e]) {
+                const int k = 4 * lane + e;
+                if (rs[e] < 0) ok = false;                          // carried run
+                else if (end_open && rs[e] == rs_l) ok = false;     // open / deferred last run
+                else ok = ((k - rs[e]) & 1) == 0;
+            }
+            counted[e] = ok;
+        }
+        if (s.run_x != -2) {
+            int64_t L = -1;
+            if (f < w.len) L = s.run_len + f;
+            else if (!end_open) L = s.run_len + w.len;
+            else s.run_len += w.len;
+            if (L >= 0) {
+                if (s.run_lead) s.lead_len = L;
+                else if (lane == 0 && L >= 2)
+                    add_pairs_global(s.run_x, s.run_x, (unsigned long long)(L >> 1), spill, ct);
+                s.run_x = -2;
+                s.run_len = 0;
+                s.run_lead = false;
+            }
+        }
+        if (s.run_x == -2 && end_open) {
+            s.run_x = view_at(w, kl);
+            s.run_len = w.len - rs_l;
+            s.run_lead = false;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (counted[e]) count_pair(hist, w.t[e], n.partner[e], spill, ct);
+    s.prev = view_at(w, kl);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 (fused with K4): one streaming pass over the corpus.  With MERGE, first applies the pending
+// merge (a, b) -> c to every chunk (matches found on the pre-merge stream with the exact X X
+// parity; touched chunks are re-packed and written back), then counts every pair of the
+// post-merge stream (hot pairs in LDS, cold pairs in the sparse table).
+// ---------------------------------------------------------------------------------------------
+template <bool MERGE>
 __global__ void __launch_bounds__(WG)
-k_count(const int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
-        const int32_t *__restrict__ len16, int64_t max_length, uint32_t *__restrict__ partials,
-        unsigned long long *__restrict__ spill, ColdTable ct, RegionRun *__restrict__ runs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
+       const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
+       uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
+       RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t *hist = lds;
+    int32_t *pack = reinterpret_cast<int32_t *>(lds + HIST_WORDS) + (threadIdx.x >> 6) * PACK_INTS;
     {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
@@ -208,95 +452,159 @@ k_count(const int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     if (r < R) {
         const int64_t c0 = (int64_t)r * cpr;
         const int64_t c1 = min(c0 + cpr, n_chunks);
-        const int4 *v4 = reinterpret_cast<const int4 *>(ids);
-        int32_t prev = c0 > 0 ? ids[c0 * CHUNK - 1] : SEP;
-        // open run carried across chunks (wave-uniform).  Initially a pseudo-run continuing the
-        // previous region's last token; it closes at once when the region starts a new run.
-        int32_t run_x = prev >= 0 ? prev : -2;
-        int64_t run_len = 0;
-        bool run_cont = true;
-        int64_t head_len = 0;
-        int4 vnext = v4[c0 * 64 + lane];
+        int4 *v4 = reinterpret_cast<int4 *>(ids);
+        // pre-merge (apply) state
+        const RegionCarry rc = carry[r];
+        int32_t pre_prev = rc.prev_tok;
+        int64_t pre_prev_off = rc.carry_off - 1;
+        bool pre_prev_match = false;
+        bool pre_started = false;
+        unsigned long long n_match = 0;
+        // count state
+        CountState s;
+        s.prev = NONE;
+        s.run_x = -2;
+        s.run_len = 0;
+        s.run_lead = false;
+        s.started = false;
+        s.lead_len = 0;
+        s.n_live = 0;
+        s.first_tok = NONE;
+        View pend;               // post-merge chunk waiting for its right neighbour
+        bool have_pend = false;
+        // register ring: chunk c, c+1 (its first slot is the pre-merge "next token"), c+2 in flight
+        const int4 tomb4 = make_int4(TOMB, TOMB, TOMB, TOMB);
+        int4 r0 = v4[c0 * 64 + lane];
+        int4 r1 = c0 + 1 < c1 ? v4[(c0 + 1) * 64 + lane] : tomb4;
+        int4 r2 = c0 + 2 < c1 ? v4[(c0 + 2) * 64 + lane] : tomb4;
         for (int64_t c = c0; c < c1; ++c) {
-            const int4 v = vnext;
-            if (c + 1 < c1) vnext = v4[(c + 1) * 64 + lane];
-            const int32_t nxt = ids[(c + 1) * CHUNK];
-            Chunk ck;
-            load_chunk(ck, v, nxt, prev, lane);
-            prev = __shfl(v.w, 63);
-            bool slow = false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) slow |= ck.eqn[e] && ck.eqp[e];
-            slow |= (lane == 63 && ck.eqn[3]) || (lane == 0 && ck.eqp[0]);
-            bool counted[4];
-            if (__ballot(slow) == 0ull) {
-                // fast path: every X X pair starts a run of exactly two -> counted
-#pragma unroll
-                for (int e = 0; e < 4; ++e) counted[e] = ck.t[e] >= 0 && ck.t[e + 1] >= 0;
-                run_x = -2;
-                run_len = 0;
-                run_cont = false;
-            } else {
-                int rs[4];
-                const int rs_last = run_starts(ck, lane, rs);
-                const bool end_open = __shfl((int)ck.eqn[3], 63) != 0;
-                const int f = first_start(ck);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bool ok = ck.t[e] >= 0 && ck.t[e + 1] >= 0;
-                    if (ok && ck.eqn[e]) {
-                        const int k = 4 * lane + e;
-                        if (rs[e] < 0) ok = false;                          // carried run
-                        else if (end_open && rs[e] == rs_last) ok = false;  // open tail run
-                        else ok = ((k - rs[e]) & 1) == 0;
-                    }
-                    counted[e] = ok;
-                }
-                if (run_x != -2) {
-                    int64_t L = -1;
-                    if (f < CHUNK) L = run_len + f;
-                    else if (!end_open) L = run_len + CHUNK;
-                    else run_len += CHUNK;
-                    if (L >= 0) {
-                        if (run_cont) {
-                            head_len = L;
-                        } else if (lane == 0 && L >= 2 &&
-                                   (!FILTER || 2 * (int64_t)len16[run_x] <= max_length)) {
-                            add_run_pairs(run_x, (unsigned long long)(L >> 1), spill, ct);
-                        }
-                        run_x = -2;
-                        run_len = 0;
-                        run_cont = false;
-                    }
-                }
-                if (run_x == -2 && end_open) {
-                    run_x = __shfl(ck.t[3], 63);
-                    run_len = CHUNK - rs_last;
-                    run_cont = false;
-                }
+            const int4 v = r0;
+            r0 = r1;
+            r1 = r2;
+            if (c + 3 < c1) r2 = v4[(c + 3) * 64 + lane];
+            View w = make_view(v);
+            if (w.len == 0) continue;
+            // first live pre-merge token after this chunk inside the region (NONE: none).  The
+            // chunks of this region are not rewritten yet, so these loads see pre-merge data.
+            int32_t nxt = NONE;
+            if (c + 1 < c1) {
+                nxt = bcast(r0.x, 0);
+                for (int64_t q = c + 2; q < c1 && nxt == TOMB; ++q) nxt = ids[q * CHUNK];
+                if (nxt == TOMB) nxt = NONE;
             }
+            // the post-merge token after this chunk is known now unless the merge can touch it
+            bool nxt_known = true;
+            if (MERGE) {
+                const int32_t nxt_pre = nxt == NONE ? rc.next_tok : nxt;
+                const int kl = w.len - 1;
+                if (!pre_started) {
+                    pre_started = true;
+                    const int32_t t0 = view_at(w, 0);
+                    pre_prev_match = pre_prev == ma && t0 == mb &&
+                                     (ma != mb || ((rc.carry_off - 1) & 1) == 0);
+                }
+                bool m[4];
+                int64_t last_off = 0;
+                const int32_t dn = __shfl_down(w.t[0], 1);
+                if (w.len == CHUNK) {
+                    const int32_t t4 = lane == 63 ? nxt_pre : dn;
+                    m[0] = w.t[0] == ma && w.t[1] == mb;
+                    m[1] = w.t[1] == ma && w.t[2] == mb;
+                    m[2] = w.t[2] == ma && w.t[3] == mb;
+                    m[3] = w.t[3] == ma && t4 == mb;
+                } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (!counted[e]) continue;
-                const int32_t x = ck.t[e], y = ck.t[e + 1];
-                if (FILTER && (int64_t)len16[x] + len16[y] > max_length) continue;
-                count_pair(hist, x, y, spill, ct);
+                    for (int e = 0; e < 4; ++e) {
+                        const int k = 4 * lane + e;
+                        const int32_t partner = (k + 1 < w.len) ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
+                        m[e] = k < w.len && w.t[e] == ma && partner == mb;
+                    }
+                }
+                bool any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
+                const int32_t t_last = view_at(w, kl);
+                if (ma == mb && (any_m || t_last == ma)) {
+                    // X X merge: only even run offsets match (core.ts:285-290 == replaceAll)
+                    Nbr n;
+                    neighbours(w, pre_prev, nxt_pre, lane, n);
+                    int64_t off[4];
+                    last_off = run_offsets(w, n, lane, pre_prev_off, off);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m[e] = m[e] && (off[e] & 1) == 0;
+                    any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
+                }
+                const bool m_last = ((__ballot(pick4(m, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
+                if (pre_prev_match || any_m) {
+                    const bool m_up = __shfl_up((int)m[3], 1) != 0;
+                    bool keep[4];
+                    keep[0] = 4 * lane + 0 < w.len && !(lane == 0 ? pre_prev_match : m_up);
+                    keep[1] = 4 * lane + 1 < w.len && !m[0];
+                    keep[2] = 4 * lane + 2 < w.len && !m[1];
+                    keep[3] = 4 * lane + 3 < w.len && !m[2];
+                    const int nk = (int)keep[0] + keep[1] + keep[2] + keep[3];
+                    const int incl = wave_incl_sum(nk, lane);
+                    const int total = bcast(incl, 63);
+                    int pp = incl - nk;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (keep[e]) pack[pp++] = m[e] ? mc : w.t[e];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    int32_t y[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int k = 4 * lane + e;
+                        y[e] = k < total ? pack[k] : TOMB;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    v4[c * 64 + lane] = make_int4(y[0], y[1], y[2], y[3]);
+                    n_match += __popcll(__ballot(m[0])) + __popcll(__ballot(m[1])) +
+                               __popcll(__ballot(m[2])) + __popcll(__ballot(m[3]));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w.t[e] = y[e];
+                    w.len = total;
+                }
+                pre_prev = t_last;
+                pre_prev_off = last_off;
+                pre_prev_match = m_last;
+                // the next chunk's first token survives unchanged unless it is a or b
+                nxt_known = nxt == NONE || (nxt != ma && nxt != mb);
+                if (w.len == 0) continue;
+            }
+            if (have_pend) {
+                count_view(pend, view_at(w, 0), false, lane, s, hist, spill, ct);
+                have_pend = false;
+            }
+            if (nxt_known) {
+                count_view(w, nxt, nxt == NONE, lane, s, hist, spill, ct);
+            } else {
+                pend = w;
+                have_pend = true;
             }
         }
+        if (have_pend) count_view(pend, NONE, true, lane, s, hist, spill, ct);
         if (lane == 0) {
-            RegionRun rr;
-            if (run_x != -2) {
-                rr.tail_x = run_x;
-                rr.tail_len = run_len;
-                rr.uniform = run_cont ? 1 : 0;
-                rr.head_len = run_cont ? run_len : head_len;
+            RegionSum rs;
+            rs.n_live = s.n_live;
+            rs.first_tok = s.n_live ? s.first_tok : NONE;
+            rs.last_tok = s.n_live ? s.prev : NONE;
+            rs.pad = 0;
+            if (s.n_live == 0) {
+                rs.lead_len = rs.trail_len = 0;
+                rs.uniform = 0;
+            } else if (s.run_x != -2) {
+                rs.uniform = s.run_lead ? 1 : 0;
+                rs.trail_len = s.run_len;
+                rs.lead_len = s.run_lead ? s.run_len : s.lead_len;
             } else {
-                rr.tail_x = -1;
-                rr.tail_len = 0;
-                rr.uniform = 0;
-                rr.head_len = head_len;
+                rs.uniform = 0;
+                rs.trail_len = 0;
+                rs.lead_len = s.lead_len;
             }
-            runs[r] = rr;
+            sums[r] = rs;
+            if (MERGE && n_match) atomicAdd(replaced, n_match);
         }
     }
     __syncthreads();
@@ -305,30 +613,81 @@ k_count(const int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
 }
 
-// Resolves runs that cross region boundaries: the run offset at each region start (for the
-// exact passes) and floor(L/2) X X pairs of every crossing run (for the count).
-__global__ void k_runs(const RegionRun *__restrict__ runs, int R, int64_t *__restrict__ carry_off,
-                       const int32_t *__restrict__ len16, int64_t max_length, int filter,
-                       unsigned long long *__restrict__ spill, ColdTable ct, int add_counts) {
+__device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
+    while (q >= 0 && s[q].n_live == 0) --q;
+    return q;
+}
+
+__device__ __forceinline__ int next_nonempty(const RegionSum *s, int q, int R) {
+    while (q < R && s[q].n_live == 0) ++q;
+    return q;
+}
+
+// Stitches the regions: counts the pair straddling every boundary, floor(L/2) X X pairs of every
+// run that was deferred (a region's first and last run, possibly spanning regions), and derives
+// the RegionCarry the next pass over this corpus needs.
+__global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
+                       unsigned long long *__restrict__ spill, ColdTable ct) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
-    const RegionRun me = runs[r];
-    int64_t off = 0;
-    if (me.head_len > 0) {
-        for (int q = r - 1; q >= 0; --q) {
-            off += runs[q].tail_len;
-            if (!runs[q].uniform) break;
+    const int p = prev_nonempty(s, r - 1);
+    const int nx = next_nonempty(s, r + 1, R);
+    RegionCarry rc;
+    rc.prev_tok = p >= 0 ? s[p].last_tok : SEP;
+    rc.next_tok = nx < R ? s[nx].first_tok : SEP;
+    rc.carry_off = 0;
+    const RegionSum me = s[r];
+    if (me.n_live == 0) {
+        carry[r] = rc;
+        return;
+    }
+    const int32_t x0 = me.first_tok;
+    const bool linked = p >= 0 && x0 >= 0 && s[p].last_tok == x0;
+    if (linked) {
+        int64_t off = 0;
+        for (int q = p; q >= 0;) {
+            if (s[q].uniform) {
+                off += s[q].n_live;
+                const int q2 = prev_nonempty(s, q - 1);
+                if (q2 >= 0 && s[q2].last_tok == x0) q = q2;
+                else break;
+            } else {
+                off += s[q].trail_len;
+                break;
+            }
+        }
+        rc.carry_off = off;
+    } else if (p >= 0 && x0 >= 0 && s[p].last_tok >= 0) {
+        add_pairs_global(s[p].last_tok, x0, 1, spill, ct);          // the boundary pair
+    }
+    carry[r] = rc;
+    // runs that START in this region: the first run (if not continuing one) and the last run
+    int32_t wx = NONE;
+    int64_t L = 0;
+    if (me.uniform) {
+        if (!linked && x0 >= 0) {
+            wx = x0;
+            L = me.n_live;
+        }
+    } else {
+        if (!linked && x0 >= 0 && me.lead_len >= 2)
+            add_pairs_global(x0, x0, (unsigned long long)(me.lead_len >> 1), spill, ct);
+        if (me.last_tok >= 0 && me.trail_len > 0) {
+            wx = me.last_tok;
+            L = me.trail_len;
         }
     }
-    carry_off[r] = off;
-    if (add_counts && me.tail_x >= 0 && !me.uniform) {
-        int64_t L = me.tail_len;
-        int q = r + 1;
-        while (q < R && runs[q].uniform) L += runs[q].tail_len, ++q;
-        if (q < R) L += runs[q].head_len;
-        const int32_t x = me.tail_x;
-        if (L >= 2 && (!filter || 2 * (int64_t)len16[x] <= max_length))
-            add_run_pairs(x, (unsigned long long)(L >> 1), spill, ct);
+    if (wx >= 0) {
+        for (int q = nx; q < R && s[q].first_tok == wx;) {
+            if (s[q].uniform) {
+                L += s[q].n_live;
+                q = next_nonempty(s, q + 1, R);
+            } else {
+                L += s[q].lead_len;
+                break;
+            }
+        }
+        if (L >= 2) add_pairs_global(wx, wx, (unsigned long long)(L >> 1), spill, ct);
     }
 }
 
@@ -357,24 +716,35 @@ __global__ void k_reduce_hot(const uint32_t *__restrict__ partials, int G,
     hot_counts[2 * w + 1] = hi + spill[2 * w + 1];
 }
 
+// max_length filter (core.ts:270-273) applied at selection time: it depends only on the pair,
+// so excluding a pair here is equivalent to never counting it.
+__device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len16,
+                                        int64_t max_length) {
+    return !max_length || (int64_t)len16[a] + len16[b] <= max_length;
+}
+
 // argmax over the dense hot table: best = max packed key.
-__global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts, Result *res) {
+__global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
+                             const int32_t *__restrict__ len16, int64_t max_length, Result *res) {
     const int bin = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long k = 0;
-    if (bin < HOT_BINS) k = pack_key(hot_counts[bin], bin >> 8, bin & 255);
+    if (bin < HOT_BINS && pair_ok(bin >> 8, bin & 255, len16, max_length))
+        k = pack_key(hot_counts[bin], bin >> 8, bin & 255);
     k = wave_max_u64(k);
     if ((threadIdx.x & 63) == 0 && k) atomicMax(&res->best, k);
 }
 
 // argmax over the claimed cold slots.
-__global__ void k_argmax_cold(ColdTable ct, Result *res) {
+__global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, int64_t max_length,
+                              Result *res) {
     const uint32_t n = *ct.n_used;
     unsigned long long best = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t h = ct.used[i];
         const uint32_t key = ct.keys[h];
-        const unsigned long long k = pack_key(ct.counts[h], (int32_t)(key >> 16),
-                                              (int32_t)(key & 0xFFFFu));
+        const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
+        if (!pair_ok(a, b, len16, max_length)) continue;
+        const unsigned long long k = pack_key(ct.counts[h], a, b);
         best = k > best ? k : best;
     }
     best = wave_max_u64(best);
@@ -388,19 +758,23 @@ __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, in
 
 // Collects every pair whose packed key equals the best (same W and same a+b).
 __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, ColdTable ct,
-                          Result *res, int2 *cand) {
+                          const int32_t *__restrict__ len16, int64_t max_length, Result *res,
+                          int2 *cand) {
     const unsigned long long best = res->best;
     if (best == 0) return;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid < HOT_BINS) {
-        if (pack_key(hot_counts[tid], tid >> 8, tid & 255) == best) push_cand(res, cand, tid >> 8, tid & 255);
+        const int32_t a = tid >> 8, b = tid & 255;
+        if (pair_ok(a, b, len16, max_length) && pack_key(hot_counts[tid], a, b) == best)
+            push_cand(res, cand, a, b);
     }
     const uint32_t n = *ct.n_used;
     for (uint32_t i = tid; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t h = ct.used[i];
         const uint32_t key = ct.keys[h];
         const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        if (pack_key(ct.counts[h], a, b) == best) push_cand(res, cand, a, b);
+        if (pair_ok(a, b, len16, max_length) && pack_key(ct.counts[h], a, b) == best)
+            push_cand(res, cand, a, b);
     }
 }
 
@@ -414,158 +788,76 @@ __global__ void k_cold_clear(ColdTable ct) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Exact passes (tie-break R3, apply R5): need the true run offset of every X X slot, carried
-// across chunks in registers and across regions via carry_off (from k_runs).
+// K3 tie pass (rule R3): last counted occurrence (slot + 1) of up to MAX_CAND tied pairs on the
+// current corpus, with exact X X parity (carry from k_runs).
 // ---------------------------------------------------------------------------------------------
-enum ExactMode { TIE = 0, APPLY_COUNT = 1, APPLY_SCATTER = 2 };
-
-struct ExactArgs {
+struct TieArgs {
     const int32_t *ids;
-    int64_t n_chunks, cpr, n_slots;
+    int64_t n_chunks, cpr;
     int R;
-    const int64_t *carry_off;
-    // tie
     int n_cand;
+    const RegionCarry *carry;
     int32_t ca[MAX_CAND], cb[MAX_CAND];
-    // apply
-    int32_t a, b, c;
-    int64_t *kept;             // per region (APPLY_COUNT)
-    const int64_t *out_off;    // per region (APPLY_SCATTER)
-    int32_t *out;
     Result *res;
 };
 
-template <int MODE>
-__global__ void __launch_bounds__(256) k_exact(ExactArgs A) {
+__global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= A.R) return;
     const int64_t c0 = (int64_t)r * A.cpr;
     const int64_t c1 = min(c0 + A.cpr, A.n_chunks);
     const int4 *v4 = reinterpret_cast<const int4 *>(A.ids);
-    int32_t prev = c0 > 0 ? A.ids[c0 * CHUNK - 1] : SEP;
-    // offset (within its run) of the slot before the chunk; valid when slot 0 continues it
-    int64_t prev_off = A.carry_off[r] - 1;
-    bool prev_match = false;       // apply: match at the slot before the chunk
+    const RegionCarry rc = A.carry[r];
+    int32_t prev = rc.prev_tok;
+    int64_t prev_off = rc.carry_off - 1;
     unsigned long long last[MAX_CAND];
-    if (MODE == TIE)
-        for (int j = 0; j < MAX_CAND; ++j) last[j] = 0;
-    unsigned long long n_match = 0;
-    int64_t kept = 0;
-    int64_t out_pos = (MODE == APPLY_SCATTER) ? A.out_off[r] : 0;
+    for (int j = 0; j < MAX_CAND; ++j) last[j] = 0;
     for (int64_t c = c0; c < c1; ++c) {
-        const int4 v = v4[c * 64 + lane];
-        const int32_t nxt = A.ids[(c + 1) * CHUNK];
-        Chunk ck;
-        load_chunk(ck, v, nxt, prev, lane);
-        if (MODE != TIE && c == c0 && c0 > 0) {
-            // match at the last slot of the previous region (owned by it)
-            const int32_t t0 = __shfl(v.x, 0);
-            if (A.a != A.b) prev_match = prev == A.a && t0 == A.b;
-            else prev_match = prev == A.a && t0 == A.a && ((A.carry_off[r] - 1) & 1) == 0;
-        }
-        prev = __shfl(v.w, 63);
-        bool slow = false;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) slow |= ck.eqn[e] && ck.eqp[e];
+        View w = make_view(v4[c * 64 + lane]);
+        if (w.len == 0) continue;
+        int32_t nxt = TOMB;
+        for (int64_t q = c + 1; q < c1 && nxt == TOMB; ++q) nxt = A.ids[q * CHUNK];
+        if (nxt == TOMB) nxt = rc.next_tok;
+        Nbr n;
+        neighbours(w, prev, nxt, lane, n);
         int64_t off[4];
-        if (__ballot(slow) == 0ull) {
+        const int64_t lo = run_offsets(w, n, lane, prev_off, off);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) off[e] = 0;   // only read at X X slots: all run starts
-            prev_off = 0;
-        } else {
-            int rs[4];
-            run_starts(ck, lane, rs);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k = 4 * lane + e;
-                off[e] = rs[e] >= 0 ? (int64_t)(k - rs[e]) : prev_off + 1 + k;
-            }
-            prev_off = __shfl(off[3], 63);
-        }
-        const int64_t base = c * CHUNK + 4 * lane;
-        if (MODE == TIE) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int32_t x = ck.t[e], y = ck.t[e + 1];
-                if (x < 0 || y < 0) continue;
-                for (int j = 0; j < A.n_cand; ++j) {
-                    if (x == A.ca[j] && y == A.cb[j] && (x != y || (off[e] & 1) == 0)) {
-                        const unsigned long long p = (unsigned long long)(base + e) + 1;
-                        last[j] = p > last[j] ? p : last[j];
-                    }
+        for (int e = 0; e < 4; ++e) {
+            const int32_t x = w.t[e], y = n.partner[e];
+            if (!n.live[e] || x < 0 || y < 0) continue;
+            for (int j = 0; j < A.n_cand; ++j) {
+                if (x == A.ca[j] && y == A.cb[j] && (x != y || (off[e] & 1) == 0)) {
+                    const unsigned long long pos = (unsigned long long)(c * CHUNK + 4 * lane + e) + 1;
+                    last[j] = pos > last[j] ? pos : last[j];
                 }
             }
-        } else {
-            bool m[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (A.a != A.b) m[e] = ck.t[e] == A.a && ck.t[e + 1] == A.b;
-                else m[e] = ck.eqn[e] && ck.t[e] == A.a && (off[e] & 1) == 0;
-            }
-            const bool m_up = __shfl_up((int)m[3], 1) != 0;
-            bool keep[4];
-            keep[0] = !(lane == 0 ? prev_match : m_up);
-            keep[1] = !m[0];
-            keep[2] = !m[1];
-            keep[3] = !m[2];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (base + e >= A.n_slots) keep[e] = false;
-            prev_match = __shfl((int)m[3], 63) != 0;
-            int nk = (int)keep[0] + keep[1] + keep[2] + keep[3];
-            int nm = (int)m[0] + m[1] + m[2] + m[3];
-            // wave inclusive scan of nk
-            int incl = nk;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                int o = __shfl_up(incl, d);
-                if (lane >= d) incl += o;
-            }
-            const int total = __shfl(incl, 63);
-            if (MODE == APPLY_SCATTER) {
-                int64_t p = out_pos + incl - nk;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (keep[e]) A.out[p++] = m[e] ? A.c : ck.t[e];
-                }
-            }
-            out_pos += total;
-            kept += total;
-            n_match += nm;
         }
+        prev = view_at(w, w.len - 1);
+        prev_off = lo;
     }
-    if (MODE == TIE) {
-        for (int j = 0; j < A.n_cand; ++j) {
-            unsigned long long v = wave_max_u64(last[j]);
-            if (lane == 0 && v) atomicMax(&A.res->last[j], v);
-        }
-    } else {
-        // n_match summed over the wave
-        unsigned long long s = n_match;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-        if (lane == 0) {
-            if (MODE == APPLY_COUNT) {
-                A.kept[r] = kept;
-                if (s) atomicAdd(&A.res->replaced, s);
-            }
-        }
+    for (int j = 0; j < A.n_cand; ++j) {
+        unsigned long long v = wave_max_u64(last[j]);
+        if (lane == 0 && v) atomicMax(&A.res->last[j], v);
     }
 }
 
-// Exclusive scan of the per-region kept counts (R <= MAX_REGIONS), one workgroup.
-__global__ void __launch_bounds__(1024) k_scan_regions(const int64_t *__restrict__ kept, int R,
-                                                       int64_t *__restrict__ out_off, Result *res) {
+// ---------------------------------------------------------------------------------------------
+// Compaction (rare): moves every region's live slots to a dense prefix of a fresh buffer.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_scan_live(const RegionSum *__restrict__ s, int R,
+                                                    int64_t *__restrict__ out_off,
+                                                    unsigned long long *total) {
     __shared__ int64_t part[1024];
     const int per = (R + 1023) / 1024;
     const int t = threadIdx.x;
-    int64_t s = 0;
+    int64_t acc = 0;
     for (int i = 0; i < per; ++i) {
         const int r = t * per + i;
-        if (r < R) s += kept[r];
+        if (r < R) acc += s[r].n_live;
     }
-    part[t] = s;
+    part[t] = acc;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
         int64_t o = t >= d ? part[t - d] : 0;
@@ -573,15 +865,35 @@ __global__ void __launch_bounds__(1024) k_scan_regions(const int64_t *__restrict
         part[t] += o;
         __syncthreads();
     }
-    int64_t run = part[t] - s;
+    int64_t run = part[t] - acc;
     for (int i = 0; i < per; ++i) {
         const int r = t * per + i;
         if (r < R) {
             out_off[r] = run;
-            run += kept[r];
+            run += s[r].n_live;
         }
     }
-    if (t == 1023) res->kept_total = part[1023];
+    if (t == 1023) *total = (unsigned long long)part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_compact(const int32_t *__restrict__ ids, int64_t n_chunks,
+                                                 int64_t cpr, int R,
+                                                 const int64_t *__restrict__ out_off,
+                                                 int32_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int64_t c0 = (int64_t)r * cpr;
+    const int64_t c1 = min(c0 + cpr, n_chunks);
+    const int4 *v4 = reinterpret_cast<const int4 *>(ids);
+    int64_t o = out_off[r];
+    for (int64_t c = c0; c < c1; ++c) {
+        const View w = make_view(v4[c * 64 + lane]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (4 * lane + e < w.len) out[o + 4 * lane + e] = w.t[e];
+        o += w.len;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -110,16 +110,15 @@ int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_
 /* ---- measurement -------------------------------------------------------------------------------
  * HIP-event timings of the kernels, recorded on the context's own stream. */
 typedef struct {
-    double count_ms;          /* pair-count kernel (K1), summed over launches */
-    int64_t count_launches;
-    int64_t count_slots;      /* int32 slots streamed by K1, summed over launches */
-    double select_ms;         /* run resolution + reduce + argmax + tie kernels */
-    double apply_ms;          /* apply kernels (match/count + scan + scatter) */
-    int64_t apply_launches;
-    int64_t apply_slots;      /* int32 slots read by the apply scatter, summed */
-    int64_t tie_passes;       /* iterations that needed the R3 tie-break pass */
-    int64_t iterations;       /* findNextMerge calls that scanned the corpus */
+    double step_ms;           /* fused streaming pass (K1 count + K4 apply of the pending merge) */
+    int64_t step_launches;
+    int64_t step_slots;       /* int32 slots streamed by those passes (live + dead) */
+    int64_t step_live;        /* live corpus tokens at those passes (pair-scans) */
+    double select_ms;         /* boundary stitch + reduce + argmax + collect + R3 tie passes */
+    int64_t tie_passes;       /* R3 tie-break passes */
+    int64_t iterations;       /* findNextMerge calls */
     int64_t live_tokens;      /* sum over those calls of live corpus tokens (pair-scans) */
+    int64_t compactions;      /* dead-slot compactions */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -14,6 +14,11 @@ extern "C" {
 int bpe_synth_latin1(uint32_t seed, uint32_t A, uint32_t base, uint64_t skip, uint8_t *out,
                      int64_t n);
 
+/* Forces one plain streaming count pass over the current corpus (no merge applied): what
+ * findNextMerge does when no counts are cached.  For measuring K1 alone. */
+struct bpe_ctx;
+int bpe_recount(struct bpe_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -176,3 +176,53 @@ def test_config3_prefix_vs_oracle():
         st.apply_merge(want[0], want[1])
         assert e.apply_merge(got[0], got[1], c) == got[2]
     assert e.corpus_size()[1] == st.off[-1]
+
+
+def test_restore_style_apply_and_append_after_merges():
+    """applyMerge without findNextMerge (restoreMerge, core.ts:477-494), then addToCorpus on a
+    merged corpus (forces a compaction), then more merges — all against the oracle."""
+    rng = random.Random(11)
+    V = 40
+    samples = [np.array([rng.randrange(V) for _ in range(rng.randint(0, 3000))], np.int32)
+               for _ in range(9)]
+    len16 = [1] * V
+    st = OracleState(np.concatenate(samples), np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64), len16, V)
+    e = pkg.Engine(0)
+    for i in range(V):
+        e.set_token_len16(i, 1)
+    for s in samples:
+        e.add_sample(s)
+    # replay a merge log without counting (restoreMerge)
+    log = st.merge_until(0, 2, 8)
+    for k, (a, b, w) in enumerate(log):
+        assert e.apply_merge(a, b, V + k) == w
+    assert e.samples() == st.samples()
+    # append a new sample to the merged corpus, then keep merging from both sides
+    extra = np.array([rng.randrange(V) for _ in range(5000)], np.int32)
+    e.add_sample(extra)
+    flat, off = st.ids.copy(), st.off.copy()
+    st2 = OracleState(np.concatenate([flat, extra]), np.append(off, off[-1] + len(extra)),
+                      list(st.len16[:st.n_tokens]), st.n_tokens)
+    want = st2.merge_until(0, 2, 25)
+    got = []
+    n_tokens = st.n_tokens
+    for _ in range(25):
+        m = e.find_next_merge(0, 2)
+        if m is None:
+            break
+        assert e.apply_merge(m[0], m[1], n_tokens) == m[2]
+        n_tokens += 1
+        got.append(m)
+    assert got == want
+    assert e.samples() == st2.samples()
+
+
+def test_compaction_under_heavy_merging():
+    """'ab' * 1.5M: the first merge halves the corpus, which triggers the dead-slot compaction."""
+    n = 3_000_000
+    sample = np.tile(np.array([0, 1], np.int32), n // 2)
+    st = OracleState(sample, np.array([0, n], np.int64), [1, 1], 2, extra=64)
+    want = st.merge_until(0, 2, 0)
+    e, got = run_engine([sample], [1, 1], {})
+    assert got == want
+    assert e.samples() == st.samples()

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Kernel-level timing of the engine on the C3 corpus: plain count passes (K1 alone) and merge
+passes (fused K4+K1), from the engine's own HIP events.  Usage: python tools/microbench.py [MiB]"""
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module('bpe-tokenizer_amd')
+
+
+def main():
+    mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    A = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    data = pkg.synth_latin1(mib << 20, seed=12345, A=A, base=0 if A == 256 else 0x20)
+    e = pkg.Engine(0)
+    t0 = time.perf_counter()
+    cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    ingest = time.perf_counter() - t0
+    del data
+    e.stats_enable(True)
+    e.recount()
+    e.reset_stats()
+    for _ in range(5):
+        e.recount()
+    rc = e.stats()
+    e.reset_stats()
+    n_tokens = nt
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m = e.find_next_merge(0, 2)
+        e.apply_merge(m[0], m[1], n_tokens)
+        n_tokens += 1
+    dt = time.perf_counter() - t0
+    st = e.stats()
+    live = rc['step_live'] / rc['step_launches']
+    out = {
+        'corpus_mib': mib, 'ingest_s': ingest,
+        'recount_ms': rc['step_ms'] / rc['step_launches'],
+        'recount_GBps_alg': 4 * live / (rc['step_ms'] / rc['step_launches'] * 1e-3) / 1e9,
+        'merge_pass_ms': st['step_ms'] / max(1, st['step_launches']),
+        'merge_pass_GBps_alg': 4 * st['step_live'] / max(1, st['step_launches']) /
+                               (st['step_ms'] / max(1, st['step_launches']) * 1e-3) / 1e9,
+        'select_ms_per_iter': st['select_ms'] / steps,
+        'wall_ms_per_iter': dt * 1e3 / steps,
+        'tie_passes': st['tie_passes'],
+    }
+    print(json.dumps(out))
+
+
+if __name__ == '__main__':
+    main()
