@@ -1,0 +1,235 @@
+// bpe_napi.cc — Node N-API addon: the thin binding core.js uses to reach the C ABI of libbpe
+// (include/bpe.h).  Every function maps 1:1 onto a bpe_* entry point; errors become JS
+// `Error('bpe native: ...')` carrying bpe_last_error().
+#define NAPI_VERSION 6
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bpe.h"
+
+namespace {
+
+napi_value throw_native(napi_env env, const char *what) {
+    char buf[1024];
+    bpe_last_error(buf, sizeof buf);
+    std::string msg = buf[0] ? std::string(buf) : std::string("bpe native: ") + what + " failed";
+    napi_throw_error(env, nullptr, msg.c_str());
+    return nullptr;
+}
+
+napi_value throw_arg(napi_env env, const char *msg) {
+    napi_throw_type_error(env, nullptr, msg);
+    return nullptr;
+}
+
+bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
+    size_t argc = want;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok) return false;
+    return argc >= want;
+}
+
+void finalize_ctx(napi_env, void *data, void *) {
+    if (data) bpe_destroy(static_cast<bpe_ctx *>(data));
+}
+
+bpe_ctx *get_ctx(napi_env env, napi_value v) {
+    void *p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return nullptr;
+    return static_cast<bpe_ctx *>(p);
+}
+
+int64_t get_i64(napi_env env, napi_value v) {
+    int64_t x = 0;
+    napi_get_value_int64(env, v, &x);
+    return x;
+}
+
+napi_value num(napi_env env, double x) {
+    napi_value v;
+    napi_create_double(env, x, &v);
+    return v;
+}
+
+// createEngine(device) -> external handle (bpe_create, core.ts:77 `new BPETokenizer()`)
+napi_value CreateEngine(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    int device = 0;
+    size_t argc = 1;
+    napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+    if (argc >= 1) device = (int)get_i64(env, argv[0]);
+    bpe_ctx *ctx = nullptr;
+    if (bpe_create(&ctx, device) != BPE_OK) return throw_native(env, "bpe_create");
+    napi_value ext;
+    napi_create_external(env, ctx, finalize_ctx, nullptr, &ext);
+    return ext;
+}
+
+// deviceCount() -> number of HIP devices
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+    int n = 0;
+    bpe_device_count(&n);
+    return num(env, n);
+}
+
+// setTokenLen16(h, id, len16)
+napi_value SetTokenLen16(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return throw_arg(env, "setTokenLen16(h, id, len16)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    if (bpe_set_token_len16(ctx, (int32_t)get_i64(env, argv[1]), (int32_t)get_i64(env, argv[2])) < 0)
+        return throw_native(env, "bpe_set_token_len16");
+    return nullptr;
+}
+
+// addSample(h, Int32Array ids)  (addToCorpus / restoreToCorpus)
+napi_value AddSample(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_arg(env, "addSample(h, Int32Array)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    napi_typedarray_type type;
+    size_t length = 0, offset = 0;
+    void *data = nullptr;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[1], &type, &length, &data, &ab, &offset) != napi_ok ||
+        type != napi_int32_array)
+        return throw_arg(env, "addSample expects an Int32Array");
+    if (bpe_add_sample(ctx, static_cast<const int32_t *>(data), (int64_t)length) < 0)
+        return throw_native(env, "bpe_add_sample");
+    return nullptr;
+}
+
+// addLatin1(h, Buffer bytes, sampleBytes, Int32Array charToId[256], nTokens) -> [nTokens, hist]
+napi_value AddLatin1(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return throw_arg(env, "addLatin1(h, buf, sampleBytes, map, n)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    void *bytes = nullptr;
+    size_t n = 0;
+    if (napi_get_buffer_info(env, argv[1], &bytes, &n) != napi_ok)
+        return throw_arg(env, "addLatin1 expects a Buffer");
+    napi_typedarray_type type;
+    size_t mlen = 0, off = 0;
+    void *map = nullptr;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[3], &type, &mlen, &map, &ab, &off) != napi_ok ||
+        type != napi_int32_array || mlen != 256)
+        return throw_arg(env, "addLatin1 expects an Int32Array(256) char map");
+    int32_t nt = (int32_t)get_i64(env, argv[4]);
+    int64_t hist[256];
+    if (bpe_add_latin1(ctx, static_cast<const uint8_t *>(bytes), (int64_t)n, get_i64(env, argv[2]),
+                       static_cast<int32_t *>(map), &nt, hist) < 0)
+        return throw_native(env, "bpe_add_latin1");
+    napi_value out, h;
+    napi_create_array_with_length(env, 2, &out);
+    napi_set_element(env, out, 0, num(env, nt));
+    napi_create_array_with_length(env, 256, &h);
+    for (int i = 0; i < 256; ++i) napi_set_element(env, h, i, num(env, (double)hist[i]));
+    napi_set_element(env, out, 1, h);
+    return out;
+}
+
+// clearCorpus(h)   (corpus_in_code = [])
+napi_value ClearCorpus(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "clearCorpus(h)");
+    if (bpe_clear_corpus(get_ctx(env, argv[0])) < 0) return throw_native(env, "bpe_clear_corpus");
+    return nullptr;
+}
+
+// corpusSize(h) -> [samples, tokens]
+napi_value CorpusSize(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "corpusSize(h)");
+    int64_t s = 0, t = 0;
+    if (bpe_corpus_size(get_ctx(env, argv[0]), &s, &t) < 0) return throw_native(env, "bpe_corpus_size");
+    napi_value out;
+    napi_create_array_with_length(env, 2, &out);
+    napi_set_element(env, out, 0, num(env, (double)s));
+    napi_set_element(env, out, 1, num(env, (double)t));
+    return out;
+}
+
+// readCorpus(h) -> [Int32Array ids, Float64Array offsets]   (materialises corpus_in_code)
+napi_value ReadCorpus(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "readCorpus(h)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    int64_t ns = 0, nt = 0;
+    if (bpe_corpus_size(ctx, &ns, &nt) < 0) return throw_native(env, "bpe_corpus_size");
+    void *ids_data = nullptr, *off_data = nullptr;
+    napi_value ids_ab, off_ab, ids, offs;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(nt, 1) * 4, &ids_data, &ids_ab);
+    napi_create_arraybuffer(env, (size_t)(ns + 1) * 8, &off_data, &off_ab);
+    std::vector<int64_t> off(ns + 1);
+    if (bpe_read_corpus(ctx, static_cast<int32_t *>(ids_data), std::max<int64_t>(nt, 1), off.data(),
+                        ns + 1) < 0)
+        return throw_native(env, "bpe_read_corpus");
+    double *od = static_cast<double *>(off_data);
+    for (int64_t i = 0; i <= ns; ++i) od[i] = (double)off[i];
+    napi_create_typedarray(env, napi_int32_array, (size_t)nt, ids_ab, 0, &ids);
+    napi_create_typedarray(env, napi_float64_array, (size_t)(ns + 1), off_ab, 0, &offs);
+    napi_value out;
+    napi_create_array_with_length(env, 2, &out);
+    napi_set_element(env, out, 0, ids);
+    napi_set_element(env, out, 1, offs);
+    return out;
+}
+
+// findNextMerge(h, maxLength, minWeight) -> [a, b, W] | null   (core.ts:247-326)
+napi_value FindNextMerge(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return throw_arg(env, "findNextMerge(h, maxLength, minWeight)");
+    int32_t a = 0, b = 0;
+    int64_t w = 0;
+    int rc = bpe_find_next_merge(get_ctx(env, argv[0]), get_i64(env, argv[1]), get_i64(env, argv[2]),
+                                 &a, &b, &w);
+    if (rc < 0) return throw_native(env, "bpe_find_next_merge");
+    napi_value out;
+    if (rc == BPE_NO_MERGE) {
+        napi_get_null(env, &out);
+        return out;
+    }
+    napi_create_array_with_length(env, 3, &out);
+    napi_set_element(env, out, 0, num(env, a));
+    napi_set_element(env, out, 1, num(env, b));
+    napi_set_element(env, out, 2, num(env, (double)w));
+    return out;
+}
+
+// applyMerge(h, a, b, c) -> replaced   (core.ts:356-359)
+napi_value ApplyMerge(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return throw_arg(env, "applyMerge(h, a, b, c)");
+    int64_t rep = 0;
+    if (bpe_apply_merge(get_ctx(env, argv[0]), (int32_t)get_i64(env, argv[1]),
+                        (int32_t)get_i64(env, argv[2]), (int32_t)get_i64(env, argv[3]), &rep) < 0)
+        return throw_native(env, "bpe_apply_merge");
+    return num(env, (double)rep);
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+    struct {
+        const char *name;
+        napi_callback cb;
+    } fns[] = {
+        {"createEngine", CreateEngine}, {"deviceCount", DeviceCount},
+        {"setTokenLen16", SetTokenLen16}, {"addSample", AddSample},
+        {"addLatin1", AddLatin1}, {"clearCorpus", ClearCorpus},
+        {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},
+        {"findNextMerge", FindNextMerge}, {"applyMerge", ApplyMerge},
+    };
+    for (auto &f : fns) {
+        napi_value fn;
+        napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn);
+        napi_set_named_property(env, exports, f.name, fn);
+    }
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -73,6 +73,7 @@ struct bpe_ctx {
     bool len16_dirty = true;
     // pass state
     uint32_t *d_partials = nullptr;
+    int partials_wg = 0;         // workgroups the partial slab can hold
     unsigned long long *d_spill = nullptr, *d_hot = nullptr, *d_total = nullptr;
     RegionSum *d_sums = nullptr;
     RegionCarry *d_carry = nullptr;
@@ -222,6 +223,12 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     if (merge) extra = (uint64_t)std::max<int64_t>(0, std::min(c->h_count[a], c->h_count[b]));
     if ((rc = ensure_cold(c, extra))) return rc;
     geometry(c);
+    if (c->G > c->partials_wg) {   // one 128 KiB slab per workgroup of the pass
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        dfree(c->d_partials);
+        if ((rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS))) return rc;
+        c->partials_wg = c->G;
+    }
     hipStream_t s = c->stream;
     k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
     HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
@@ -454,7 +461,6 @@ int bpe_create(bpe_ctx **out, int device) {
         return bail(fail(BPE_ERR_HIP, "bpe native: hipStreamCreate failed"));
     for (auto &e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(fail(BPE_ERR_HIP, "bpe native: event"));
-    if ((rc = dev_alloc(&c->d_partials, (size_t)MAX_WG * HIST_WORDS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_spill, HOT_BINS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_hot, HOT_BINS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_total, 2))) return bail(rc);

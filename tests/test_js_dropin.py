@@ -1,0 +1,46 @@
+"""The Node drop-in (bpe-tokenizer_amd/js/core.js over the N-API addon): host logic on CPU, the
+reference's spec + golden cases through the full JS surface on the GPU."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from bpe_amd import ROOT
+
+NODE = shutil.which('node')
+ADDON_DIR = os.path.join(ROOT, 'bpe-tokenizer_amd', 'addon')
+
+pytestmark = pytest.mark.skipif(NODE is None, reason='node not installed')
+
+
+def build_addon():
+    subprocess.check_call(['make', '-s', '-C', ADDON_DIR])
+
+
+def run_node(script, *flags, timeout=600):
+    out = subprocess.run([NODE, *flags, os.path.join(ROOT, 'tests', 'js', script)],
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    return out.stdout
+
+
+def test_addon_builds_and_exports():
+    build_addon()
+    out = subprocess.check_output([NODE, '-e', "const a=require(process.argv[1]);"
+                                   "console.log(Object.keys(a).sort().join(','))",
+                                   os.path.join(ADDON_DIR, 'bpe_napi.node')], text=True)
+    assert out.strip() == ('addLatin1,addSample,applyMerge,clearCorpus,corpusSize,createEngine,'
+                           'deviceCount,findNextMerge,readCorpus,setTokenLen16')
+
+
+def test_host_logic_against_golden():
+    build_addon()
+    assert 'host_only ok' in run_node('host_only.js')
+
+
+@pytest.mark.gpu
+def test_reference_spec_and_golden_through_js():
+    build_addon()
+    out = run_node('spec_gpu.js', '--expose-gc')
+    assert 'spec_gpu ok' in out
