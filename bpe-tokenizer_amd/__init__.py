@@ -29,7 +29,8 @@ C_API = [
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
-    'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount',
+    'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount', 'bpe_export_counts',
+    'bpe_select_counts', 'bpe_tie_positions',
 ]
 
 
@@ -95,6 +96,11 @@ def lib():
         'bpe_reset_stats': ([vp], ctypes.c_int),
         'bpe_get_stream': ([vp, ctypes.POINTER(vp)], ctypes.c_int),
         'bpe_recount': ([vp], ctypes.c_int),
+        'bpe_export_counts': ([vp, vp, vp, vp, ctypes.c_int64, i64p], ctypes.c_int),
+        'bpe_select_counts': ([vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                               i32p, ctypes.c_int64, i64p, i64p], ctypes.c_int),
+        'bpe_tie_positions': ([vp, i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)],
+                              ctypes.c_int),
         'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                               ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     }
@@ -234,6 +240,41 @@ class Engine:
         s = Stats()
         _check(lib().bpe_get_stats(self._ctx, ctypes.byref(s)), 'bpe_get_stats')
         return s.as_dict()
+
+    # sharded corpus (device pointers, e.g. torch tensors' data_ptr()) ------------------------------
+    def export_counts(self, hot_ptr, keys_ptr, counts_ptr, cap):
+        """Copies this shard's counts into device buffers; returns the number of sparse entries
+        (which may exceed cap: then nothing was written and the caller must grow its buffers)."""
+        n = ctypes.c_int64()
+        rc = lib().bpe_export_counts(self._ctx, hot_ptr, keys_ptr, counts_ptr, cap, ctypes.byref(n))
+        if rc < 0 and n.value <= cap:
+            _check(rc, 'bpe_export_counts')
+        return n.value
+
+    def select_counts(self, hot_ptr, keys_ptr, counts_ptr, n_cold, max_length=0, min_weight=0,
+                      cap=4096):
+        """Selection over global tables: None, or (W, [(a, b), ...] candidates sorted)."""
+        cand = np.zeros(2 * cap, np.int32)
+        n, w = ctypes.c_int64(), ctypes.c_int64()
+        rc = _check(lib().bpe_select_counts(self._ctx, hot_ptr, keys_ptr, counts_ptr, n_cold,
+                                            int(max_length or 0), int(min_weight or 0),
+                                            cand.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                            cap, ctypes.byref(n), ctypes.byref(w)),
+                    'bpe_select_counts')
+        if rc == BPE_NO_MERGE:
+            return None
+        if n.value > cap:
+            raise BpeError('more than %d tied candidates' % cap)
+        return w.value, [(int(cand[2 * i]), int(cand[2 * i + 1])) for i in range(n.value)]
+
+    def tie_positions(self, cands):
+        """Shard-local last counted occurrence (+1, 0 = none) of each (a, b) candidate (R3)."""
+        c = np.ascontiguousarray(np.asarray(cands, np.int32).reshape(-1))
+        last = np.zeros(len(cands), np.uint64)
+        _check(lib().bpe_tie_positions(self._ctx, c.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       len(cands), last.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
+               'bpe_tie_positions')
+        return last
 
     def recount(self):
         """One plain streaming count pass (K1 alone; measurement helper)."""

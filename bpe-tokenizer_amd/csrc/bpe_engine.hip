@@ -312,6 +312,43 @@ int maybe_compact(bpe_ctx *c) {
     return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout
 }
 
+// R3 pass(es): last counted occurrence (slot + 1, 0 = none) of each candidate on this corpus.
+int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long long *last) {
+    int rc;
+    if (!c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    hipStream_t s = c->stream;
+    for (unsigned j0 = 0; j0 < n_cand; j0 += MAX_CAND) {
+        const unsigned nb = std::min<unsigned>(MAX_CAND, n_cand - j0);
+        TieArgs A;
+        memset(&A, 0, sizeof A);
+        A.ids = c->d_ids;
+        A.n_chunks = c->n_chunks;
+        A.cpr = c->cpr;
+        A.R = c->R;
+        A.n_cand = (int)nb;
+        A.carry = c->d_carry;
+        A.res = c->d_res;
+        for (unsigned j = 0; j < nb; ++j) {
+            A.ca[j] = cand[j0 + j].x;
+            A.cb[j] = cand[j0 + j].y;
+        }
+        HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+        if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
+        if (c->n_live > 0) k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+        if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (c->stats_on) {
+            c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
+            c->stats.tie_passes += 1;
+        }
+        for (unsigned j = 0; j < nb; ++j) last[j0 + j] = c->h_res->last[j];
+    }
+    return BPE_OK;
+}
+
 int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int32_t *b,
             int64_t *w) {
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
@@ -350,40 +387,14 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     if (n_cand > 1) {
         // R3: several pairs share W and a+b -> the one whose last counted occurrence is earliest
         // (the pair that reached W first in the reference's scan, core.ts:296-305)
+        std::vector<unsigned long long> last(n_cand);
+        if ((rc = tie_positions(c, cand.data(), n_cand, last.data()))) return rc;
         unsigned long long best_pos = ~0ull;
-        for (unsigned j0 = 0; j0 < n_cand; j0 += MAX_CAND) {
-            const unsigned nb = std::min<unsigned>(MAX_CAND, n_cand - j0);
-            TieArgs A;
-            memset(&A, 0, sizeof A);
-            A.ids = c->d_ids;
-            A.n_chunks = c->n_chunks;
-            A.cpr = c->cpr;
-            A.R = c->R;
-            A.n_cand = (int)nb;
-            A.carry = c->d_carry;
-            A.res = c->d_res;
-            for (unsigned j = 0; j < nb; ++j) {
-                A.ca[j] = cand[j0 + j].x;
-                A.cb[j] = cand[j0 + j].y;
-            }
-            HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-            if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
-            k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-            if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
-            HIP_TRY(hipStreamSynchronize(s));
-            if (c->stats_on) {
-                c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
-                c->stats.tie_passes += 1;
-            }
-            for (unsigned j = 0; j < nb; ++j) {
-                const unsigned long long p = c->h_res->last[j];
-                if (p && p < best_pos) {
-                    best_pos = p;
-                    ba = cand[j0 + j].x;
-                    bb = cand[j0 + j].y;
-                }
+        for (unsigned j = 0; j < n_cand; ++j) {
+            if (last[j] && last[j] < best_pos) {
+                best_pos = last[j];
+                ba = cand[j].x;
+                bb = cand[j].y;
             }
         }
         if (best_pos == ~0ull) return fail(BPE_ERR_STATE, "bpe native: tie pass found no occurrence");
@@ -727,6 +738,81 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     }
     *n_merges = n;
     return BPE_OK;
+}
+
+int bpe_export_counts(bpe_ctx *c, uint64_t *hot, uint32_t *cold_keys, uint64_t *cold_counts,
+                      int64_t cap, int64_t *n_cold) {
+    if (!c || !hot || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (!c->counts_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    uint32_t nu = 0;
+    HIP_TRY(hipMemcpy(&nu, c->cold.n_used, sizeof nu, hipMemcpyDeviceToHost));
+    *n_cold = nu;
+    if ((int64_t)nu > cap) return fail(BPE_ERR_ARG, "bpe native: export buffer too small");
+    hipStream_t s = c->stream;
+    HIP_TRY(hipMemcpyAsync(hot, c->d_hot, HOT_BINS * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    if (nu) {
+        if (!cold_keys || !cold_counts) return fail(BPE_ERR_ARG, "bpe native: null cold buffers");
+        k_export_cold<<<256, 256, 0, s>>>(c->cold, cold_keys, (unsigned long long *)cold_counts);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return BPE_OK;
+}
+
+int bpe_select_counts(bpe_ctx *c, const uint64_t *hot, const uint32_t *cold_keys,
+                      const uint64_t *cold_counts, int64_t n_cold, int64_t max_length,
+                      int64_t min_weight, int32_t *cand, int64_t cap, int64_t *n_cand,
+                      int64_t *w) {
+    if (!c || !hot || !n_cand || !w || n_cold < 0 || (n_cold && (!cold_keys || !cold_counts)) ||
+        (cap > 0 && !cand))
+        return fail(BPE_ERR_ARG, "bpe native: bad select arguments");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (min_weight == 0) min_weight = 2;                               // core.ts:256
+    if ((rc = sync_len16(c))) return rc;
+    hipStream_t s = c->stream;
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    const auto *h = (const unsigned long long *)hot;
+    const auto *cc = (const unsigned long long *)cold_counts;
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(h, c->d_len16, max_length, c->d_res);
+    if (n_cold)
+        k_argmax_list<<<256, 256, 0, s>>>(cold_keys, cc, n_cold, c->d_len16, max_length, c->d_res);
+    k_collect_list<<<HOT_BINS / 256, 256, 0, s>>>(h, cold_keys, cc, n_cold, c->d_len16, max_length,
+                                                  c->d_res, c->d_cand);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const Result res = *c->h_res;
+    *n_cand = 0;
+    if (res.best == 0) return BPE_NO_MERGE;                            // core.ts:312
+    const int64_t W = (int64_t)(res.best >> 17);
+    if (W < min_weight) return BPE_NO_MERGE;                           // core.ts:313
+    const int64_t nc = std::min<int64_t>(res.n_cand, CAND_CAP);
+    std::vector<int2> buf(nc);
+    HIP_TRY(hipMemcpy(buf.data(), c->d_cand, nc * sizeof(int2), hipMemcpyDeviceToHost));
+    std::sort(buf.begin(), buf.end(), [](const int2 &x, const int2 &y) {
+        return x.x != y.x ? x.x < y.x : x.y < y.y;
+    });
+    for (int64_t i = 0; i < std::min(nc, cap); ++i) {
+        cand[2 * i] = buf[i].x;
+        cand[2 * i + 1] = buf[i].y;
+    }
+    *n_cand = res.n_cand;
+    *w = W;
+    return BPE_OK;
+}
+
+int bpe_tie_positions(bpe_ctx *c, const int32_t *cand, int64_t n, uint64_t *last) {
+    if (!c || n < 0 || (n > 0 && (!cand || !last)))
+        return fail(BPE_ERR_ARG, "bpe native: bad tie arguments");
+    int rc = set_device(c);
+    if (rc) return rc;
+    std::vector<int2> cv(n);
+    for (int64_t i = 0; i < n; ++i) cv[i] = make_int2(cand[2 * i], cand[2 * i + 1]);
+    return tie_positions(c, cv.data(), (unsigned)n, (unsigned long long *)last);
 }
 
 int bpe_stats_enable(bpe_ctx *c, int on) {

@@ -778,6 +778,51 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
     }
 }
 
+// ---- sharded selection over caller-provided (global) tables ----------------------------------
+__global__ void k_export_cold(ColdTable ct, uint32_t *keys, unsigned long long *counts) {
+    const uint32_t n = *ct.n_used;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t h = ct.used[i];
+        keys[i] = ct.keys[h];
+        counts[i] = ct.counts[h];
+    }
+}
+
+__global__ void k_argmax_list(const uint32_t *__restrict__ keys,
+                              const unsigned long long *__restrict__ counts, int64_t n,
+                              const int32_t *__restrict__ len16, int64_t max_length, Result *res) {
+    unsigned long long best = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t a = (int32_t)(keys[i] >> 16), b = (int32_t)(keys[i] & 0xFFFFu);
+        if (!pair_ok(a, b, len16, max_length)) continue;
+        const unsigned long long k = pack_key(counts[i], a, b);
+        best = k > best ? k : best;
+    }
+    best = wave_max_u64(best);
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(&res->best, best);
+}
+
+__global__ void k_collect_list(const unsigned long long *__restrict__ hot,
+                               const uint32_t *__restrict__ keys,
+                               const unsigned long long *__restrict__ counts, int64_t n,
+                               const int32_t *__restrict__ len16, int64_t max_length, Result *res,
+                               int2 *cand) {
+    const unsigned long long best = res->best;
+    if (best == 0) return;
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (tid < HOT_BINS) {
+        const int32_t a = (int32_t)(tid >> 8), b = (int32_t)(tid & 255);
+        if (pair_ok(a, b, len16, max_length) && pack_key(hot[tid], a, b) == best)
+            push_cand(res, cand, a, b);
+    }
+    for (int64_t i = tid; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t a = (int32_t)(keys[i] >> 16), b = (int32_t)(keys[i] & 0xFFFFu);
+        if (pair_ok(a, b, len16, max_length) && pack_key(counts[i], a, b) == best)
+            push_cand(res, cand, a, b);
+    }
+}
+
 __global__ void k_cold_clear(ColdTable ct) {
     const uint32_t n = *ct.n_used;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {

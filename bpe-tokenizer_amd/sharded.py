@@ -1,18 +1,27 @@
-"""One-rank-per-GPU driver of the merge loop (mergeUntil, core.ts:365-383) over a corpus sharded at
-sample boundaries.
+"""One-rank-per-GPU driver of the merge loop (mergeUntil, core.ts:365-383) over a corpus sharded
+at sample boundaries.
 
 Pairs never cross samples (core.ts:265-267), so rank r owns a contiguous run of whole samples and
-counts its pairs locally; the only exchange per iteration is the pair-count table (an all-reduce
-over RCCL/xGMI) plus, when several pairs tie on (W, a+b), an all-reduce(MAX) of their last counted
-positions (rule R3).  Every rank then applies the same merge to its shard.
+counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exchange:
+  1. the dense hot table (pairs of ids < 256, 65536 x u64): one all-reduce(SUM) over RCCL/xGMI;
+  2. the sparse remainder: all-gather of (key, count) lists, duplicates summed on device;
+  3. only when several pairs tie on (W, a+b): an all-reduce(MAX) of their last counted positions
+     (rule R3; rank r's positions order after rank r-1's).
+Every rank then selects the same merge (libbpe's argmax over the global tables) and applies it to
+its own shard.  world == 1 is the plain single-GPU loop.
 
-world == 1 is the plain single-GPU loop.
+The protocol only needs a `shard` object with export()/select()/tie_positions()/apply(); GpuShard
+wraps libbpe on a HIP device, and tests/test_sharded_gloo.py drives the same protocol on CPU
+with gloo.
 """
 import importlib
 
 import numpy as np
 
 pkg = importlib.import_module('bpe-tokenizer_amd')
+
+HOT_BINS = 256 * 256
+RANK_SHIFT = 40          # global position = rank << 40 | shard-local position
 
 
 def first_appearance(data, alphabet_size=256):
@@ -31,9 +40,100 @@ def first_appearance(data, alphabet_size=256):
     return first
 
 
-class ShardedTrainer:
-    def __init__(self, engine, rank, world, dist, n_tokens, live_global):
+class GpuShard:
+    """libbpe engine on one HIP device, exporting/selecting through torch device tensors."""
+
+    def __init__(self, engine, device_index):
+        import torch
         self.engine = engine
+        self.torch = torch
+        self.device = torch.device('cuda', device_index)
+        self.hot = torch.zeros(HOT_BINS, dtype=torch.int64, device=self.device)
+        self.cap = 1 << 16
+        self.keys = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+        self.counts = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
+
+    def export(self):
+        torch = self.torch
+        n = self.engine.export_counts(self.hot.data_ptr(), self.keys.data_ptr(),
+                                      self.counts.data_ptr(), self.cap)
+        if n > self.cap:
+            self.cap = 1 << max(16, int(n - 1).bit_length())
+            self.keys = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+            self.counts = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
+            n = self.engine.export_counts(self.hot.data_ptr(), self.keys.data_ptr(),
+                                          self.counts.data_ptr(), self.cap)
+        return self.hot, self.keys[:n], self.counts[:n]
+
+    def select(self, hot, keys, counts, max_length, min_weight):
+        keys = keys.contiguous()
+        counts = counts.contiguous()
+        return self.engine.select_counts(hot.data_ptr(), keys.data_ptr() if keys.numel() else None,
+                                         counts.data_ptr() if counts.numel() else None,
+                                         keys.numel(), max_length, min_weight)
+
+    def tie_positions(self, cands):
+        return self.engine.tie_positions(cands)
+
+    def apply(self, a, b, c):
+        return self.engine.apply_merge(a, b, c)
+
+
+def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
+    """The per-iteration collective protocol.  Returns (a, b, W) or None, identical on every rank.
+    Collectives run on the tables' device (RCCL); with the gloo backend on host copies."""
+    import torch
+    hot, keys, counts = shard.export()
+    dev = torch.device('cpu') if dist.get_backend() == 'gloo' else hot.device
+    hot = hot.to(dev, copy=True)
+    keys = keys.to(dev)
+    counts = counts.to(dev)
+    dist.all_reduce(hot)
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(x.item()) for x in sizes]
+    m = max(sizes)
+    if m:
+        kp = torch.full((m,), -1, dtype=torch.int32, device=dev)
+        cp = torch.zeros(m, dtype=torch.int64, device=dev)
+        kp[:keys.numel()] = keys
+        cp[:counts.numel()] = counts
+        gk = [torch.empty_like(kp) for _ in range(world)]
+        gc = [torch.empty_like(cp) for _ in range(world)]
+        dist.all_gather(gk, kp)
+        dist.all_gather(gc, cp)
+        all_k = torch.cat([g[:s] for g, s in zip(gk, sizes)])
+        all_c = torch.cat([g[:s] for g, s in zip(gc, sizes)])
+        ukeys, inv = torch.unique(all_k, return_inverse=True)
+        ucounts = torch.zeros(ukeys.numel(), dtype=torch.int64, device=dev).index_add_(0, inv, all_c)
+    else:
+        ukeys = torch.zeros(0, dtype=torch.int32, device=dev)
+        ucounts = torch.zeros(0, dtype=torch.int64, device=dev)
+    sdev = getattr(shard, 'device', dev)
+    sel = shard.select(hot.to(sdev), ukeys.to(sdev), ucounts.to(sdev), max_length, min_weight)
+    if sel is None:
+        return None
+    w, cands = sel
+    a, b = cands[0]
+    if len(cands) > 1:
+        last = np.asarray(shard.tie_positions(cands), dtype=np.int64)
+        glob = np.where(last > 0, (np.int64(rank) << RANK_SHIFT) | last, 0)
+        g = torch.tensor(glob, dtype=torch.int64, device=dev)
+        dist.all_reduce(g, op=dist.ReduceOp.MAX)
+        g = g.cpu().numpy()
+        best = None
+        for (ca, cb), pos in zip(cands, g):
+            if pos > 0 and (best is None or pos < best[0]):
+                best = (pos, ca, cb)
+        a, b = best[1], best[2]
+    return a, b, w
+
+
+class ShardedTrainer:
+    def __init__(self, shard, rank, world, dist, n_tokens, live_global):
+        self.shard = shard
+        self.engine = getattr(shard, 'engine', shard)
         self.rank = rank
         self.world = world
         self.dist = dist
@@ -54,18 +154,19 @@ class ShardedTrainer:
         # global first-appearance order (core.ts:186-199) across the shards, in corpus order
         import torch
         first = first_appearance(data, alphabet)
-        key = np.where(first >= 0, rank * (1 << 40) + first, np.iinfo(np.int64).max)
-        t = torch.tensor(key, dtype=torch.int64, device='cuda')
+        big = np.iinfo(np.int64).max
+        key = np.where(first >= 0, (np.int64(rank) << RANK_SHIFT) + first, big)
+        t = torch.tensor(key, dtype=torch.int64, device=torch.device('cuda', device))
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gkey = t.cpu().numpy()
-        order = [int(ch) for ch in np.argsort(gkey, kind='stable') if gkey[ch] != np.iinfo(np.int64).max]
+        order = [int(ch) for ch in np.argsort(gkey, kind='stable') if gkey[ch] != big]
         cmap = np.full(256, -1, np.int32)
         for i, ch in enumerate(order):
             cmap[ch] = i
         for i in range(len(order)):
             eng.set_token_len16(i, 1)
         eng.add_latin1(data, sample_bytes=sample_bytes, char_to_id=cmap, n_tokens=len(order))
-        return cls(eng, rank, world, dist, len(order), bytes_per_rank * world)
+        return cls(GpuShard(eng, device), rank, world, dist, len(order), bytes_per_rank * world)
 
     def live_tokens_global(self):
         return self.live
@@ -73,7 +174,8 @@ class ShardedTrainer:
     def find_next_merge(self, max_length=0, min_weight=0):
         if self.world == 1:
             return self.engine.find_next_merge(max_length, min_weight)
-        raise NotImplementedError('multi-rank exchange')
+        return exchange_and_select(self.shard, self.dist, self.rank, self.world, max_length,
+                                   min_weight)
 
     def step(self, max_length=0, min_weight=0):
         """One findNextMerge + applyMerge on every rank; returns (a, b, W) or None."""
@@ -81,7 +183,10 @@ class ShardedTrainer:
         if m is None:
             return None
         a, b, w = m
-        self.engine.apply_merge(a, b, self.n_tokens)
+        if self.world == 1:
+            self.engine.apply_merge(a, b, self.n_tokens)
+        else:
+            self.shard.apply(a, b, self.n_tokens)
         self.n_tokens += 1
         self.live -= w
         self.merges.append(m)

@@ -107,6 +107,33 @@ int bpe_apply_merge(bpe_ctx *ctx, int32_t a, int32_t b, int32_t c, int64_t *repl
 int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_t max_iterations,
                     int64_t *out_abw, int64_t cap, int64_t *n_merges);
 
+/* ---- sharded corpus (one process per GPU) ------------------------------------------------------
+ * Pairs never cross samples (core.ts:265-267), so a corpus split at sample boundaries is counted
+ * shard by shard; the caller sums the shards' tables (all-reduce / all-gather over RCCL) and
+ * selects from the global table.  All table pointers below are DEVICE pointers on this context's
+ * device (e.g. torch tensors); host pointers are marked.
+ *
+ * bpe_export_counts: this shard's pair counts for the current corpus (one streaming pass if none
+ * are cached): hot[65536] u64 counts of pairs with both ids < 256 at a*256+b, and the sparse rest
+ * as cold_keys[i] = a<<16|b (u32) with cold_counts[i] (u64).  *n_cold receives the number of
+ * sparse entries; when it exceeds cap nothing is written and BPE_ERR_ARG is returned (retry with
+ * a bigger buffer). */
+int bpe_export_counts(bpe_ctx *ctx, uint64_t *hot, uint32_t *cold_keys, uint64_t *cold_counts,
+                      int64_t cap, int64_t *n_cold);
+
+/* findNextMerge's selection (core.ts:294-313) over GLOBAL tables (hot as above; cold entries with
+ * distinct keys).  Writes W and the candidate pairs sharing the best (W, a+b) as host int32
+ * (a, b) pairs into cand (capacity cap pairs); *n_cand may exceed cap (then only cap written).
+ * BPE_NO_MERGE when the reference would return null. */
+int bpe_select_counts(bpe_ctx *ctx, const uint64_t *hot, const uint32_t *cold_keys,
+                      const uint64_t *cold_counts, int64_t n_cold, int64_t max_length,
+                      int64_t min_weight, int32_t *cand, int64_t cap, int64_t *n_cand,
+                      int64_t *w);
+
+/* Rule R3 on this shard: for each host (a, b) pair in cand, the shard-local position + 1 of its
+ * last counted occurrence (0 when none) into host last[n].  Positions grow in corpus order. */
+int bpe_tie_positions(bpe_ctx *ctx, const int32_t *cand, int64_t n, uint64_t *last);
+
 /* ---- measurement -------------------------------------------------------------------------------
  * HIP-event timings of the kernels, recorded on the context's own stream. */
 typedef struct {

@@ -1,0 +1,133 @@
+"""Multi-rank merge protocol (bpe-tokenizer_amd/sharded.py) on CPU: world_size 2 over gloo.
+
+Each rank holds a contiguous run of whole samples.  The per-shard counting, selection, R3
+positions and apply are provided by an oracle-backed stand-in (the HIP engine needs a GPU); the
+collectives (all-reduce of the hot table, all-gather + device-side merge of the sparse lists,
+all-reduce(MAX) of tie positions) are the production code.  The merge sequence of the 2-rank run
+must equal the single-process oracle's on the whole corpus.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from bpe_amd import pkg  # noqa: F401  (package import: sharded.py lives in it)
+from oracle import OracleState
+
+sharded = __import__('importlib').import_module('bpe-tokenizer_amd.sharded')
+
+
+class OracleShard:
+    """Stand-in for GpuShard with the same interface, computed by the C restatement."""
+
+    def __init__(self, samples, len16, n_tokens):
+        off = np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64)
+        ids = np.concatenate(samples).astype(np.int32) if samples else np.zeros(0, np.int32)
+        self.st = OracleState(ids, off, len16, n_tokens)
+
+    def export(self):
+        pa, pb, pc, self._last = self.st.count_pairs()
+        self._pairs = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(pa, pb))}
+        hot = torch.zeros(256 * 256, dtype=torch.int64)
+        hm = (pa < 256) & (pb < 256)
+        hot[torch.from_numpy((pa[hm] * 256 + pb[hm]).astype(np.int64))] = torch.from_numpy(pc[hm])
+        keys = torch.from_numpy(((pa[~hm].astype(np.int64) << 16) | pb[~hm]).astype(np.uint32).view(np.int32))
+        return hot, keys, torch.from_numpy(pc[~hm].astype(np.int64))
+
+    def select(self, hot, keys, counts, max_length, min_weight):
+        # selection rule of core.ts:294-313 over the global tables (restated for the test)
+        ent = [(i >> 8, i & 255, int(c)) for i, c in enumerate(hot.tolist()) if c]
+        ku = keys.numpy().view(np.uint32)
+        ent += [(int(k >> 16), int(k & 0xFFFF), int(c)) for k, c in zip(ku, counts.tolist())]
+        L = self.st.len16
+        if max_length:
+            ent = [e for e in ent if L[e[0]] + L[e[1]] <= max_length]
+        if not ent:
+            return None
+        key = lambda e: (e[2], -(e[0] + e[1]))
+        best = max(key(e) for e in ent)
+        if best[0] < (min_weight or 2):
+            return None
+        return best[0], sorted((e[0], e[1]) for e in ent if key(e) == best)
+
+    def tie_positions(self, cands):
+        out = np.zeros(len(cands), np.uint64)
+        for j, c in enumerate(cands):
+            i = self._pairs.get(tuple(c))
+            if i is not None:
+                out[j] = self._last[i] + 1
+        return out
+
+    def apply(self, a, b, c):
+        return self.st.apply_merge(a, b, c)
+
+
+def make_corpus(seed):
+    rng = random.Random(seed)
+    V = rng.choice([3, 12, 300])
+    samples = []
+    for _ in range(rng.randint(2, 12)):
+        L = rng.randint(0, 4000)
+        s, i = [], 0
+        while i < L:
+            t = rng.randrange(V)
+            k = 1 if rng.random() > 0.2 else rng.randint(2, 9)
+            s += [t] * k
+            i += k
+        samples.append(np.array(s[:L], np.int32))
+    len16 = [rng.choice([1, 1, 2]) for _ in range(V)]
+    opts = {'max_length': rng.choice([0, 0, 4]), 'min_weight': rng.choice([0, 2, -1])}
+    return samples, len16, V, opts
+
+
+def worker(rank, world, port, seed, n_iter, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        samples, len16, V, opts = make_corpus(seed)
+        cut = len(samples) // 2
+        mine = samples[:cut] if rank == 0 else samples[cut:]
+        shard = OracleShard(mine, len16, V)
+        tr = sharded.ShardedTrainer(shard, rank, world, dist, V, sum(len(s) for s in samples))
+        for _ in range(n_iter):
+            if tr.step(opts['max_length'], opts['min_weight']) is None:
+                break
+        q.put((rank, tr.merges, shard.st.samples()))
+    finally:
+        dist.destroy_process_group()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('seed', [1, 2, 3, 4])
+def test_two_rank_merges_equal_single_process(seed):
+    n_iter = 40
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, seed, n_iter, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (m, s)) for r, m, s in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    samples, len16, V, opts = make_corpus(seed)
+    off = np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64)
+    st = OracleState(np.concatenate(samples), off, len16, V)
+    want = st.merge_until(opts['max_length'], opts['min_weight'], n_iter)
+    assert [tuple(m) for m in res[0][0]] == want
+    assert [tuple(m) for m in res[1][0]] == want
+    assert res[0][1] + res[1][1] == st.samples()
