@@ -312,6 +312,10 @@ __device__ __forceinline__ uint32_t lds_inc(uint32_t *hist, int bin) {
     return atomicAdd(&hist[bin >> 1], 1u << ((bin & 1) << 4));
 }
 
+__device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
+                                                      CountState s, uint32_t *hist,
+                                                      unsigned long long *spill, ColdTable ct);
+
 __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last, int lane,
                                            CountState &s, uint32_t *hist,
                                            unsigned long long *spill, const ColdTable &ct) {
@@ -336,10 +340,10 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
                 const uint32_t o0 = lds_inc(hist, b0), o1 = lds_inc(hist, b1),
                                o2 = lds_inc(hist, b2), o3 = lds_inc(hist, b3);
                 const uint32_t lim = 0x7FFFu;
-                const bool ovf = ((o0 >> ((b0 & 1) << 4)) & 0xFFFFu) == lim ||
-                                 ((o1 >> ((b1 & 1) << 4)) & 0xFFFFu) == lim ||
-                                 ((o2 >> ((b2 & 1) << 4)) & 0xFFFFu) == lim ||
-                                 ((o3 >> ((b3 & 1) << 4)) & 0xFFFFu) == lim;
+                const int ovf = (int)(((o0 >> ((b0 & 1) << 4)) & 0xFFFFu) == lim) |
+                                (int)(((o1 >> ((b1 & 1) << 4)) & 0xFFFFu) == lim) |
+                                (int)(((o2 >> ((b2 & 1) << 4)) & 0xFFFFu) == lim) |
+                                (int)(((o3 >> ((b3 & 1) << 4)) & 0xFFFFu) == lim);
                 if (ovf) {
                     lds_spill_fix(hist, b0, o0, spill);
                     lds_spill_fix(hist, b1, o1, spill);
@@ -357,6 +361,13 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
             return;
         }
     }
+    s = count_view_general(w, nxt, last, lane, s, hist, spill, ct);
+}
+
+// The general case: partial chunks, runs crossing chunk or region edges, SEPs, cold ids.
+__device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
+                                                      CountState s, uint32_t *hist,
+                                                      unsigned long long *spill, ColdTable ct) {
     if (!s.started) {
         s.started = true;
         s.first_tok = view_at(w, 0);
@@ -425,6 +436,7 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
     for (int e = 0; e < 4; ++e)
         if (counted[e]) count_pair(hist, w.t[e], n.partner[e], spill, ct);
     s.prev = view_at(w, kl);
+    return s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -472,16 +484,21 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
         s.first_tok = NONE;
         View pend;               // post-merge chunk waiting for its right neighbour
         bool have_pend = false;
-        // register ring: chunk c, c+1 (its first slot is the pre-merge "next token"), c+2 in flight
+        // register ring: chunk c (r0), c+1 (r1: its first slot is the "next token"), and
+        // c+2..c+4 in flight — 4 KiB per wave, 64 KiB per CU of HBM reads outstanding
         const int4 tomb4 = make_int4(TOMB, TOMB, TOMB, TOMB);
         int4 r0 = v4[c0 * 64 + lane];
         int4 r1 = c0 + 1 < c1 ? v4[(c0 + 1) * 64 + lane] : tomb4;
         int4 r2 = c0 + 2 < c1 ? v4[(c0 + 2) * 64 + lane] : tomb4;
+        int4 r3 = c0 + 3 < c1 ? v4[(c0 + 3) * 64 + lane] : tomb4;
+        int4 r4 = c0 + 4 < c1 ? v4[(c0 + 4) * 64 + lane] : tomb4;
         for (int64_t c = c0; c < c1; ++c) {
             const int4 v = r0;
             r0 = r1;
             r1 = r2;
-            if (c + 3 < c1) r2 = v4[(c + 3) * 64 + lane];
+            r2 = r3;
+            r3 = r4;
+            if (c + 5 < c1) r4 = v4[(c + 5) * 64 + lane];
             View w = make_view(v);
             if (w.len == 0) continue;
             // first live pre-merge token after this chunk inside the region (NONE: none).  The
