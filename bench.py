@@ -166,6 +166,7 @@ def main():
                 'select': st['select_ms'] / max(1, args.steps),
                 'tie_passes': st['tie_passes'],
                 'compactions': st['compactions'],
+                'exact_passes': st['exact_passes'],
             },
         }
         if world == 1 and not args.no_cpu_baseline:

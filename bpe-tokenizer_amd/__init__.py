@@ -30,8 +30,10 @@ C_API = [
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
     'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount', 'bpe_export_counts',
-    'bpe_select_counts', 'bpe_tie_positions',
+    'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions',
 ]
+HOT_BINS = 65536
+TABLE_BINS = 131072
 
 
 class BpeError(RuntimeError):
@@ -44,7 +46,7 @@ class Stats(ctypes.Structure):
         ('step_slots', ctypes.c_int64), ('step_live', ctypes.c_int64),
         ('select_ms', ctypes.c_double), ('tie_passes', ctypes.c_int64),
         ('iterations', ctypes.c_int64), ('live_tokens', ctypes.c_int64),
-        ('compactions', ctypes.c_int64),
+        ('compactions', ctypes.c_int64), ('exact_passes', ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -96,7 +98,8 @@ def lib():
         'bpe_reset_stats': ([vp], ctypes.c_int),
         'bpe_get_stream': ([vp, ctypes.POINTER(vp)], ctypes.c_int),
         'bpe_recount': ([vp], ctypes.c_int),
-        'bpe_export_counts': ([vp, vp, vp, vp, ctypes.c_int64, i64p], ctypes.c_int),
+        'bpe_export_counts': ([vp, vp], ctypes.c_int),
+        'bpe_heavy_counts': ([vp, vp, ctypes.c_int64, vp, vp, ctypes.c_int64, i64p], ctypes.c_int),
         'bpe_select_counts': ([vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                i32p, ctypes.c_int64, i64p, i64p], ctypes.c_int),
         'bpe_tie_positions': ([vp, i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)],
@@ -242,21 +245,26 @@ class Engine:
         return s.as_dict()
 
     # sharded corpus (device pointers, e.g. torch tensors' data_ptr()) ------------------------------
-    def export_counts(self, hot_ptr, keys_ptr, counts_ptr, cap):
-        """Copies this shard's counts into device buffers; returns the number of sparse entries
-        (which may exceed cap: then nothing was written and the caller must grow its buffers)."""
+    def export_counts(self, table_ptr):
+        """Copies this shard's [TABLE_BINS] u64 table (hot bins + cold sketch) to device memory."""
+        _check(lib().bpe_export_counts(self._ctx, table_ptr), 'bpe_export_counts')
+
+    def heavy_counts(self, table_ptr, keys_ptr, counts_ptr, cap, max_length=0):
+        """Exact shard counts of the cold pairs whose GLOBAL sketch bucket could still win.
+        Returns the entry count (> cap means nothing was written: grow and retry)."""
         n = ctypes.c_int64()
-        rc = lib().bpe_export_counts(self._ctx, hot_ptr, keys_ptr, counts_ptr, cap, ctypes.byref(n))
+        rc = lib().bpe_heavy_counts(self._ctx, table_ptr, int(max_length or 0), keys_ptr,
+                                    counts_ptr, cap, ctypes.byref(n))
         if rc < 0 and n.value <= cap:
-            _check(rc, 'bpe_export_counts')
+            _check(rc, 'bpe_heavy_counts')
         return n.value
 
-    def select_counts(self, hot_ptr, keys_ptr, counts_ptr, n_cold, max_length=0, min_weight=0,
+    def select_counts(self, table_ptr, keys_ptr, counts_ptr, n_cold, max_length=0, min_weight=0,
                       cap=4096):
         """Selection over global tables: None, or (W, [(a, b), ...] candidates sorted)."""
         cand = np.zeros(2 * cap, np.int32)
         n, w = ctypes.c_int64(), ctypes.c_int64()
-        rc = _check(lib().bpe_select_counts(self._ctx, hot_ptr, keys_ptr, counts_ptr, n_cold,
+        rc = _check(lib().bpe_select_counts(self._ctx, table_ptr, keys_ptr, counts_ptr, n_cold,
                                             int(max_length or 0), int(min_weight or 0),
                                             cand.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                             cap, ctypes.byref(n), ctypes.byref(w)),

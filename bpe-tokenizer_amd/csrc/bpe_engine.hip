@@ -74,7 +74,8 @@ struct bpe_ctx {
     // pass state
     uint32_t *d_partials = nullptr;
     int partials_wg = 0;         // workgroups the partial slab can hold
-    unsigned long long *d_spill = nullptr, *d_hot = nullptr, *d_total = nullptr;
+    unsigned long long *d_spill = nullptr, *d_hot = nullptr, *d_total = nullptr;   // d_hot: TABLE_BINS
+    uint32_t *d_heavy = nullptr;
     RegionSum *d_sums = nullptr;
     RegionCarry *d_carry = nullptr;
     int64_t *d_outoff = nullptr;
@@ -219,9 +220,6 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 // With a merge, *replaced receives the number of replacements.
 int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
-    uint64_t extra = 0;
-    if (merge) extra = (uint64_t)std::max<int64_t>(0, std::min(c->h_count[a], c->h_count[b]));
-    if ((rc = ensure_cold(c, extra))) return rc;
     geometry(c);
     if (c->G > c->partials_wg) {   // one 128 KiB slab per workgroup of the pass
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -230,30 +228,26 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         c->partials_wg = c->G;
     }
     hipStream_t s = c->stream;
-    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(c->d_spill, 0, HOT_BINS * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(c->d_spill, 0, TABLE_BINS * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
     if (merge)
-        k_step<true><<<c->G, WG, STEP_LDS, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a,
-                                                b, cc, c->d_partials, c->d_spill, c->cold,
-                                                c->d_sums, &c->d_res->replaced);
+        k_step<true, MODE_TABLE><<<c->G, WG, STEP_LDS, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
+            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     else
-        k_step<false><<<c->G, WG, STEP_LDS, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
-                                                 -1, -1, -1, c->d_partials, c->d_spill, c->cold,
-                                                 c->d_sums, &c->d_res->replaced);
+        k_step<false, MODE_TABLE><<<c->G, WG, STEP_LDS, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
+            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     HIP_TRY(hipGetLastError());
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
-    k_runs<<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill, c->cold);
-    k_reduce_hot<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
+    k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
+                                                          c->cold, c->d_heavy);
+    k_reduce_table<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
     HIP_TRY(hipGetLastError());
-    uint32_t flags[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[2], s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
     if (c->stats_on) {
         c->stats.step_ms += ev_ms(c->ev[0], c->ev[1]);
         c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
@@ -312,6 +306,63 @@ int maybe_compact(bpe_ctx *c) {
     return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout
 }
 
+// Exact counts of the cold pairs in the sketch buckets marked in d_heavy, into the sparse table
+// (one more streaming pass; only when some bucket could still reach the best hot count).
+int exact_pass(bpe_ctx *c) {
+    int rc;
+    if ((rc = ensure_cold(c, 0))) return rc;
+    if (!c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    geometry(c);
+    hipStream_t s = c->stream;
+    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
+    k_step<false, MODE_EXACT><<<c->G, WG, STEP_LDS, s>>>(
+        c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
+        c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+    k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
+                                                          c->cold, c->d_heavy);
+    HIP_TRY(hipGetLastError());
+    uint32_t flags[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    if (c->stats_on) c->stats.exact_passes += 1;
+    return BPE_OK;
+}
+
+// Best hot pair + heavy sketch buckets for `table` (a [TABLE_BINS] u64 table on the device);
+// then, when some bucket is heavy, the exact pass; then every pair sharing the best key.
+// Leaves the Result in h_res and the candidates in `cand`.
+int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_length,
+                      bool local, std::vector<int2> &cand) {
+    int rc;
+    if ((rc = sync_len16(c))) return rc;
+    hipStream_t s = c->stream;
+    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(table, c->d_len16, max_length, c->d_res);
+    k_heavy<<<SKETCH_BINS / 256, 256, 0, s>>>(table, c->d_res, c->d_heavy);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (c->h_res->n_heavy && local) {
+        if ((rc = exact_pass(c))) return rc;
+        k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
+    }
+    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
+                                             c->d_cand);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const unsigned n_cand = std::min<unsigned>(c->h_res->n_cand, CAND_CAP);
+    cand.resize(n_cand);
+    if (n_cand)
+        HIP_TRY(hipMemcpy(cand.data(), c->d_cand, n_cand * sizeof(int2), hipMemcpyDeviceToHost));
+    return BPE_OK;
+}
+
 // R3 pass(es): last counted occurrence (slot + 1, 0 = none) of each candidate on this corpus.
 int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long long *last) {
     int rc;
@@ -356,20 +407,16 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     int rc;
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    if ((rc = sync_len16(c))) return rc;
     hipStream_t s = c->stream;
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
-    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res);
-    k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
-    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length, c->d_res,
-                                             c->d_cand);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[5], s));
+    std::vector<int2> cand;
+    if ((rc = select_from_table(c, c->d_hot, max_length, true, cand))) return rc;
     if (c->stats_on) {
-        c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
+        float ms = 0.f;
+        HIP_TRY(hipEventRecord(c->ev[2], s));
+        HIP_TRY(hipEventSynchronize(c->ev[2]));
+        ms = ev_ms(c->ev[5], c->ev[2]);
+        c->stats.select_ms += ms;
         c->stats.iterations += 1;
         c->stats.live_tokens += c->n_live;
     }
@@ -377,12 +424,9 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     if (res.best == 0) return BPE_NO_MERGE;                            // core.ts:312
     const int64_t W = (int64_t)(res.best >> 17);
     if (W < min_weight) return BPE_NO_MERGE;                           // core.ts:313
-    const unsigned n_cand = res.n_cand;
-    if (n_cand == 0 || n_cand > (unsigned)CAND_CAP)
+    const unsigned n_cand = (unsigned)cand.size();
+    if (n_cand == 0 || res.n_cand > (unsigned)CAND_CAP)
         return fail(BPE_ERR_STATE, "bpe native: bad candidate count");
-    std::vector<int2> cand(n_cand);
-    HIP_TRY(hipMemcpyAsync(cand.data(), c->d_cand, n_cand * sizeof(int2), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
     int32_t ba = cand[0].x, bb = cand[0].y;
     if (n_cand > 1) {
         // R3: several pairs share W and a+b -> the one whose last counted occurrence is earliest
@@ -472,8 +516,9 @@ int bpe_create(bpe_ctx **out, int device) {
         return bail(fail(BPE_ERR_HIP, "bpe native: hipStreamCreate failed"));
     for (auto &e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(fail(BPE_ERR_HIP, "bpe native: event"));
-    if ((rc = dev_alloc(&c->d_spill, HOT_BINS))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_hot, HOT_BINS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_spill, TABLE_BINS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_hot, TABLE_BINS))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_heavy, HEAVY_WORDS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_total, 2))) return bail(rc);
     if ((rc = dev_alloc(&c->d_sums, MAX_REGIONS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_carry, MAX_REGIONS))) return bail(rc);
@@ -488,10 +533,12 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = ensure_chunks(c, 1))) return bail(rc);
     if ((rc = ensure_vocab(c, 0))) return bail(rc);
     if ((rc = ensure_cold(c, 0))) return bail(rc);
-    if (hipFuncSetAttribute((const void *)k_step<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)STEP_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_step<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)STEP_LDS) != hipSuccess)
+    if (hipFuncSetAttribute((const void *)k_step<true, MODE_TABLE>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_step<false, MODE_TABLE>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_step<false, MODE_EXACT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: cannot reserve 144 KiB of LDS"));
     if ((rc = seal_packed(c))) return bail(rc);
     *out = c;
@@ -504,7 +551,7 @@ int bpe_destroy(bpe_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
-                    c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used};
+                    c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     for (auto &e : c->ev)
@@ -740,32 +787,53 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     return BPE_OK;
 }
 
-int bpe_export_counts(bpe_ctx *c, uint64_t *hot, uint32_t *cold_keys, uint64_t *cold_counts,
-                      int64_t cap, int64_t *n_cold) {
-    if (!c || !hot || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
+int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
+    if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return BPE_OK;
+}
+
+int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint32_t *cold_keys,
+                     uint64_t *cold_counts, int64_t cap, int64_t *n_cold) {
+    if (!c || !table || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if ((rc = sync_len16(c))) return rc;
+    hipStream_t s = c->stream;
+    const auto *t = (const unsigned long long *)table;
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(t, c->d_len16, max_length, c->d_res);
+    k_heavy<<<SKETCH_BINS / 256, 256, 0, s>>>(t, c->d_res, c->d_heavy);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_cold = 0;
+    if (!c->h_res->n_heavy) return BPE_OK;
+    if ((rc = exact_pass(c))) return rc;
     uint32_t nu = 0;
     HIP_TRY(hipMemcpy(&nu, c->cold.n_used, sizeof nu, hipMemcpyDeviceToHost));
     *n_cold = nu;
     if ((int64_t)nu > cap) return fail(BPE_ERR_ARG, "bpe native: export buffer too small");
-    hipStream_t s = c->stream;
-    HIP_TRY(hipMemcpyAsync(hot, c->d_hot, HOT_BINS * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     if (nu) {
         if (!cold_keys || !cold_counts) return fail(BPE_ERR_ARG, "bpe native: null cold buffers");
         k_export_cold<<<256, 256, 0, s>>>(c->cold, cold_keys, (unsigned long long *)cold_counts);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(s));
     }
-    HIP_TRY(hipStreamSynchronize(s));
     return BPE_OK;
 }
 
-int bpe_select_counts(bpe_ctx *c, const uint64_t *hot, const uint32_t *cold_keys,
+int bpe_select_counts(bpe_ctx *c, const uint64_t *table, const uint32_t *cold_keys,
                       const uint64_t *cold_counts, int64_t n_cold, int64_t max_length,
                       int64_t min_weight, int32_t *cand, int64_t cap, int64_t *n_cand,
                       int64_t *w) {
+    const uint64_t *hot = table;
     if (!c || !hot || !n_cand || !w || n_cold < 0 || (n_cold && (!cold_keys || !cold_counts)) ||
         (cap > 0 && !cand))
         return fail(BPE_ERR_ARG, "bpe native: bad select arguments");

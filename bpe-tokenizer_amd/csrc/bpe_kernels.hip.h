@@ -33,7 +33,11 @@ constexpr int MAX_WG = 256;                 // one per CU on MI355X
 constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
 constexpr int HOT = 256;                    // ids < HOT form the dense LDS histogram
 constexpr int HOT_BINS = HOT * HOT;
-constexpr int HIST_WORDS = HOT_BINS / 2;    // two 16-bit counters per LDS dword (128 KiB)
+constexpr int SKETCH_BINS = 65536;          // count sketch of the cold pairs (ids >= HOT)
+constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, [64K, 128K) sketch
+constexpr int HIST_WORDS = TABLE_BINS / 4;  // four 8-bit counters per LDS dword (128 KiB)
+constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
+enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1 };
 constexpr int PACK_INTS = CHUNK;            // per-wave LDS staging for re-packing a chunk
 constexpr size_t STEP_LDS = HIST_WORDS * 4 + WAVES_PER_WG * PACK_INTS * 4;   // 144 KiB
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
@@ -73,7 +77,7 @@ struct ColdTable {
 struct Result {
     unsigned long long best;             // packed (W << 17) | (0x1FFFF - c_index), 0 = none
     unsigned int n_cand;                 // pairs sharing the best packed key (list in `cand`)
-    unsigned int pad0;
+    unsigned int n_heavy;                // sketch buckets that need exact cold counts
     unsigned long long last[MAX_CAND];   // R3: slot + 1 of the last counted occurrence
     unsigned long long replaced;         // apply: replacement count
     unsigned long long pad1;
@@ -130,29 +134,66 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint
     }
 }
 
-// Adds n occurrences of (x, y) outside the LDS histogram (boundary pairs, resolved runs).
-__device__ __forceinline__ void add_pairs_global(int32_t x, int32_t y, unsigned long long n,
-                                                 unsigned long long *spill, const ColdTable &ct) {
-    if (n == 0) return;
-    if ((uint32_t)x < HOT && (uint32_t)y < HOT) atomicAdd(&spill[x * HOT + y], n);
-    else cold_add(ct, ((uint32_t)x << 16) | (uint32_t)y, (uint32_t)n);
+__device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
+    return ((uint32_t)x << 16) | (uint32_t)y;
 }
 
-// One counted occurrence of (x, y).  Hot pairs go to the workgroup's packed 16-bit LDS counters;
-// a counter reaching 0x8000 spills 0x8000 to the global u64 spill table (exactly one lane
-// observes each 0x7FFF -> 0x8000 transition, so nothing is lost or double counted).
-__device__ __forceinline__ void count_pair(uint32_t *hist, int32_t x, int32_t y,
-                                           unsigned long long *spill, const ColdTable &ct) {
-    if ((uint32_t)x < HOT && (uint32_t)y < HOT) {
-        const int bin = x * HOT + y;
-        const uint32_t sh = (bin & 1) << 4;
-        const uint32_t old = atomicAdd(&hist[bin >> 1], 1u << sh);
-        if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-            atomicSub(&hist[bin >> 1], 0x8000u << sh);
-            atomicAdd(&spill[bin], 0x8000ull);
-        }
-    } else {
-        cold_add(ct, ((uint32_t)x << 16) | (uint32_t)y, 1u);
+// Table index of a pair: its exact bin when both ids are hot, else its sketch bucket.
+__device__ __forceinline__ int table_index(int32_t x, int32_t y) {
+    if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) return (x << 8) | y;
+    return HOT_BINS + (int)((pair_key(x, y) * 0x9E3779B1u) >> 16);
+}
+
+// Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup 8-bit LDS table (hot bins
+// exact + cold sketch) with a global u64 spill.  MODE_EXACT: exact counts of the cold pairs whose
+// sketch bucket is marked heavy, into the sparse table; everything else is ignored.
+struct Sink {
+    uint32_t *hist;                  // LDS table (MODE_TABLE)
+    unsigned long long *spill;       // global u64 [TABLE_BINS]
+    ColdTable ct;
+    const uint32_t *heavy;           // LDS bitmap [HEAVY_WORDS] (MODE_EXACT)
+};
+
+template <int MODE>
+__device__ __forceinline__ bool exact_wanted(const Sink &k, int32_t x, int32_t y) {
+    const int idx = table_index(x, y);
+    if (idx < HOT_BINS) return false;
+    const int b = idx - HOT_BINS;
+    return (k.heavy[b >> 5] >> (b & 31)) & 1u;
+}
+
+// Adds n occurrences of (x, y) from outside the LDS table (boundary pairs, resolved runs).
+template <int MODE>
+__device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32_t y,
+                                                 unsigned long long n) {
+    if (n == 0) return;
+    if (MODE == MODE_TABLE) atomicAdd(&k.spill[table_index(x, y)], n);
+    else if (exact_wanted<MODE>(k, x, y)) cold_add(k.ct, pair_key(x, y), (uint32_t)n);
+}
+
+// LDS 8-bit counter increment; a counter reaching 0x80 spills 0x80 to the global table (exactly
+// one lane observes each 0x7F -> 0x80 transition, so nothing is lost or double counted).
+__device__ __forceinline__ uint32_t lds_inc8(uint32_t *hist, int idx) {
+    return atomicAdd(&hist[idx >> 2], 1u << ((idx & 3) << 3));
+}
+
+__device__ __forceinline__ void lds_fix8(uint32_t *hist, int idx, uint32_t old,
+                                         unsigned long long *spill) {
+    const uint32_t sh = (idx & 3) << 3;
+    if (((old >> sh) & 0xFFu) == 0x7Fu) {
+        atomicSub(&hist[idx >> 2], 0x80u << sh);
+        atomicAdd(&spill[idx], 0x80ull);
+    }
+}
+
+// One counted occurrence of (x, y).
+template <int MODE>
+__device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
+    if (MODE == MODE_TABLE) {
+        const int idx = table_index(x, y);
+        lds_fix8(k.hist, idx, lds_inc8(k.hist, idx), k.spill);
+    } else if (exact_wanted<MODE>(k, x, y)) {
+        cold_add(k.ct, pair_key(x, y), 1u);
     }
 }
 
@@ -299,26 +340,13 @@ struct CountState {
 // Counts the pairs of one post-merge chunk whose right side is inside the region: every pair
 // (k, next live) except X X pairs of the region's first and last run, which k_runs resolves.
 // nxt = first live token of the next non-empty chunk of the region, NONE for the region's last.
-__device__ __forceinline__ void lds_spill_fix(uint32_t *hist, int bin, uint32_t old,
-                                              unsigned long long *spill) {
-    const uint32_t sh = (bin & 1) << 4;
-    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-        atomicSub(&hist[bin >> 1], 0x8000u << sh);
-        atomicAdd(&spill[bin], 0x8000ull);
-    }
-}
-
-__device__ __forceinline__ uint32_t lds_inc(uint32_t *hist, int bin) {
-    return atomicAdd(&hist[bin >> 1], 1u << ((bin & 1) << 4));
-}
-
+template <int MODE>
 __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
-                                                      CountState s, uint32_t *hist,
-                                                      unsigned long long *spill, ColdTable ct);
+                                                      CountState s, Sink k);
 
+template <int MODE>
 __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last, int lane,
-                                           CountState &s, uint32_t *hist,
-                                           unsigned long long *spill, const ColdTable &ct) {
+                                           CountState &s, const Sink &k) {
     if (!last && s.run_x == -2 && s.started && w.len == CHUNK) {
         // Fast path: a full chunk with no run open across its start.  Valid when no slot is the
         // middle of a run of >= 3 and no X X pair straddles the chunk end: then every X X pair
@@ -332,42 +360,41 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
         const bool trip = (p == t0 && e01) || (e01 && e12) || (e12 && e23) || (e23 && e34) ||
                           (lane == 63 && e34 && t3 >= 0);
         if (__ballot(trip) == 0ull) {
-            const uint32_t all = (uint32_t)(t0 | t1 | t2 | t3 | t4);
-            if (__ballot(all >= (uint32_t)HOT) == 0ull) {
-                // all four pairs valid and hot: four LDS atomics in flight, one overflow test
-                const int b0 = t0 * HOT + t1, b1 = t1 * HOT + t2, b2 = t2 * HOT + t3,
-                          b3 = t3 * HOT + t4;
-                const uint32_t o0 = lds_inc(hist, b0), o1 = lds_inc(hist, b1),
-                               o2 = lds_inc(hist, b2), o3 = lds_inc(hist, b3);
-                const uint32_t lim = 0x7FFFu;
-                const int ovf = (int)(((o0 >> ((b0 & 1) << 4)) & 0xFFFFu) == lim) |
-                                (int)(((o1 >> ((b1 & 1) << 4)) & 0xFFFFu) == lim) |
-                                (int)(((o2 >> ((b2 & 1) << 4)) & 0xFFFFu) == lim) |
-                                (int)(((o3 >> ((b3 & 1) << 4)) & 0xFFFFu) == lim);
+            if (MODE == MODE_TABLE && __ballot((t0 | t1 | t2 | t3 | t4) < 0) == 0ull) {
+                // four valid pairs (hot bins or sketch buckets): four LDS atomics in flight,
+                // one overflow test
+                const int i0 = table_index(t0, t1), i1 = table_index(t1, t2),
+                          i2 = table_index(t2, t3), i3 = table_index(t3, t4);
+                const uint32_t o0 = lds_inc8(k.hist, i0), o1 = lds_inc8(k.hist, i1),
+                               o2 = lds_inc8(k.hist, i2), o3 = lds_inc8(k.hist, i3);
+                const int ovf = (int)(((o0 >> ((i0 & 3) << 3)) & 0xFFu) == 0x7Fu) |
+                                (int)(((o1 >> ((i1 & 3) << 3)) & 0xFFu) == 0x7Fu) |
+                                (int)(((o2 >> ((i2 & 3) << 3)) & 0xFFu) == 0x7Fu) |
+                                (int)(((o3 >> ((i3 & 3) << 3)) & 0xFFu) == 0x7Fu);
                 if (ovf) {
-                    lds_spill_fix(hist, b0, o0, spill);
-                    lds_spill_fix(hist, b1, o1, spill);
-                    lds_spill_fix(hist, b2, o2, spill);
-                    lds_spill_fix(hist, b3, o3, spill);
+                    lds_fix8(k.hist, i0, o0, k.spill);
+                    lds_fix8(k.hist, i1, o1, k.spill);
+                    lds_fix8(k.hist, i2, o2, k.spill);
+                    lds_fix8(k.hist, i3, o3, k.spill);
                 }
             } else {
                 const int32_t x[5] = {t0, t1, t2, t3, t4};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if ((x[e] | x[e + 1]) >= 0) count_pair(hist, x[e], x[e + 1], spill, ct);
+                    if ((x[e] | x[e + 1]) >= 0) count_pair<MODE>(k, x[e], x[e + 1]);
             }
             s.n_live += CHUNK;
             s.prev = bcast(t3, 63);
             return;
         }
     }
-    s = count_view_general(w, nxt, last, lane, s, hist, spill, ct);
+    s = count_view_general<MODE>(w, nxt, last, lane, s, k);
 }
 
-// The general case: partial chunks, runs crossing chunk or region edges, SEPs, cold ids.
+// The general case: partial chunks, runs crossing chunk or region edges, SEPs.
+template <int MODE>
 __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
-                                                      CountState s, uint32_t *hist,
-                                                      unsigned long long *spill, ColdTable ct) {
+                                                      CountState s, Sink k) {
     if (!s.started) {
         s.started = true;
         s.first_tok = view_at(w, 0);
@@ -420,7 +447,7 @@ __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool 
             if (L >= 0) {
                 if (s.run_lead) s.lead_len = L;
                 else if (lane == 0 && L >= 2)
-                    add_pairs_global(s.run_x, s.run_x, (unsigned long long)(L >> 1), spill, ct);
+                    add_pairs_global<MODE>(k, s.run_x, s.run_x, (unsigned long long)(L >> 1));
                 s.run_x = -2;
                 s.run_len = 0;
                 s.run_lead = false;
@@ -434,7 +461,7 @@ __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool 
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        if (counted[e]) count_pair(hist, w.t[e], n.partner[e], spill, ct);
+        if (counted[e]) count_pair<MODE>(k, w.t[e], n.partner[e]);
     s.prev = view_at(w, kl);
     return s;
 }
@@ -445,20 +472,28 @@ __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool 
 // parity; touched chunks are re-packed and written back), then counts every pair of the
 // post-merge stream (hot pairs in LDS, cold pairs in the sparse table).
 // ---------------------------------------------------------------------------------------------
-template <bool MERGE>
+template <bool MERGE, int MODE>
 __global__ void __launch_bounds__(WG)
 k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
        const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
        uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
-       RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced) {
+       const uint32_t *__restrict__ heavy_g, RegionSum *__restrict__ sums,
+       unsigned long long *__restrict__ replaced) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t *hist = lds;
     int32_t *pack = reinterpret_cast<int32_t *>(lds + HIST_WORDS) + (threadIdx.x >> 6) * PACK_INTS;
-    {
+    if (MODE == MODE_TABLE) {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int i = threadIdx.x; i < HEAVY_WORDS; i += WG) hist[i] = heavy_g[i];
     }
     __syncthreads();
+    Sink k;
+    k.hist = hist;
+    k.spill = spill;
+    k.ct = ct;
+    k.heavy = hist;
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
     if (r < R) {
@@ -591,17 +626,17 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
                 if (w.len == 0) continue;
             }
             if (have_pend) {
-                count_view(pend, view_at(w, 0), false, lane, s, hist, spill, ct);
+                count_view<MODE>(pend, view_at(w, 0), false, lane, s, k);
                 have_pend = false;
             }
             if (nxt_known) {
-                count_view(w, nxt, nxt == NONE, lane, s, hist, spill, ct);
+                count_view<MODE>(w, nxt, nxt == NONE, lane, s, k);
             } else {
                 pend = w;
                 have_pend = true;
             }
         }
-        if (have_pend) count_view(pend, NONE, true, lane, s, hist, spill, ct);
+        if (have_pend) count_view<MODE>(pend, NONE, true, lane, s, k);
         if (lane == 0) {
             RegionSum rs;
             rs.n_live = s.n_live;
@@ -624,10 +659,12 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             if (MERGE && n_match) atomicAdd(replaced, n_match);
         }
     }
-    __syncthreads();
-    uint4 *out = reinterpret_cast<uint4 *>(partials + (size_t)blockIdx.x * HIST_WORDS);
-    const uint4 *h4 = reinterpret_cast<const uint4 *>(hist);
-    for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
+    if (MODE == MODE_TABLE) {
+        __syncthreads();
+        uint4 *out = reinterpret_cast<uint4 *>(partials + (size_t)blockIdx.x * HIST_WORDS);
+        const uint4 *h4 = reinterpret_cast<const uint4 *>(hist);
+        for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
+    }
 }
 
 __device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
@@ -643,10 +680,17 @@ __device__ __forceinline__ int next_nonempty(const RegionSum *s, int q, int R) {
 // Stitches the regions: counts the pair straddling every boundary, floor(L/2) X X pairs of every
 // run that was deferred (a region's first and last run, possibly spanning regions), and derives
 // the RegionCarry the next pass over this corpus needs.
+template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
-                       unsigned long long *__restrict__ spill, ColdTable ct) {
+                       unsigned long long *__restrict__ spill, ColdTable ct,
+                       const uint32_t *__restrict__ heavy) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
+    Sink k;
+    k.hist = nullptr;
+    k.spill = spill;
+    k.ct = ct;
+    k.heavy = heavy;
     const int p = prev_nonempty(s, r - 1);
     const int nx = next_nonempty(s, r + 1, R);
     RegionCarry rc;
@@ -675,7 +719,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
         }
         rc.carry_off = off;
     } else if (p >= 0 && x0 >= 0 && s[p].last_tok >= 0) {
-        add_pairs_global(s[p].last_tok, x0, 1, spill, ct);          // the boundary pair
+        add_pairs_global<MODE>(k, s[p].last_tok, x0, 1);            // the boundary pair
     }
     carry[r] = rc;
     // runs that START in this region: the first run (if not continuing one) and the last run
@@ -688,7 +732,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
         }
     } else {
         if (!linked && x0 >= 0 && me.lead_len >= 2)
-            add_pairs_global(x0, x0, (unsigned long long)(me.lead_len >> 1), spill, ct);
+            add_pairs_global<MODE>(k, x0, x0, (unsigned long long)(me.lead_len >> 1));
         if (me.last_tok >= 0 && me.trail_len > 0) {
             wx = me.last_tok;
             L = me.trail_len;
@@ -704,33 +748,43 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
                 break;
             }
         }
-        if (L >= 2) add_pairs_global(wx, wx, (unsigned long long)(L >> 1), spill, ct);
+        if (L >= 2) add_pairs_global<MODE>(k, wx, wx, (unsigned long long)(L >> 1));
     }
 }
 
-// Sums the per-workgroup packed LDS partials and the spill table into u64 hot counts.
-__global__ void k_reduce_hot(const uint32_t *__restrict__ partials, int G,
-                             const unsigned long long *__restrict__ spill,
-                             unsigned long long *__restrict__ hot_counts) {
+// Sums the per-workgroup 8-bit LDS partials and the spill table into the u64 table
+// (hot bins [0, 64K), sketch buckets [64K, 128K)).
+__global__ void k_reduce_table(const uint32_t *__restrict__ partials, int G,
+                               const unsigned long long *__restrict__ spill,
+                               unsigned long long *__restrict__ table) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= HIST_WORDS) return;
-    unsigned long long lo = 0, hi = 0;
-    int g = 0;
-    for (; g + 4 <= G; g += 4) {
-        uint32_t p0 = partials[(size_t)(g + 0) * HIST_WORDS + w];
-        uint32_t p1 = partials[(size_t)(g + 1) * HIST_WORDS + w];
-        uint32_t p2 = partials[(size_t)(g + 2) * HIST_WORDS + w];
-        uint32_t p3 = partials[(size_t)(g + 3) * HIST_WORDS + w];
-        lo += (p0 & 0xFFFFu) + (p1 & 0xFFFFu) + (p2 & 0xFFFFu) + (p3 & 0xFFFFu);
-        hi += (p0 >> 16) + (p1 >> 16) + (p2 >> 16) + (p3 >> 16);
+    uint32_t acc[4] = {0, 0, 0, 0};   // < 2^24 per byte lane: G <= 256 slabs of < 256 each
+    for (int g = 0; g < G; ++g) {
+        const uint32_t p = partials[(size_t)g * HIST_WORDS + w];
+        acc[0] += p & 0xFFu;
+        acc[1] += (p >> 8) & 0xFFu;
+        acc[2] += (p >> 16) & 0xFFu;
+        acc[3] += p >> 24;
     }
-    for (; g < G; ++g) {
-        uint32_t p = partials[(size_t)g * HIST_WORDS + w];
-        lo += p & 0xFFFFu;
-        hi += p >> 16;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) table[4 * w + b] = acc[b] + spill[4 * w + b];
+}
+
+// Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there
+// can still reach W, so only they need exact counts.  T = max(W_hot, 1).
+__global__ void k_heavy(const unsigned long long *__restrict__ table, Result *res,
+                        uint32_t *__restrict__ heavy) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;   // one thread per bucket
+    const unsigned long long w_hot = res->best >> 17;
+    const unsigned long long T = w_hot ? w_hot : 1;
+    const bool h = b < SKETCH_BINS && table[HOT_BINS + b] >= T;
+    const unsigned long long m = __ballot(h);
+    if ((threadIdx.x & 31) == 0 && b < SKETCH_BINS) {
+        const uint32_t word = (uint32_t)(m >> (threadIdx.x & 32));
+        heavy[b >> 5] = word;
+        if (word) atomicAdd(&res->n_heavy, (unsigned)__popc(word));
     }
-    hot_counts[2 * w] = lo + spill[2 * w];
-    hot_counts[2 * w + 1] = hi + spill[2 * w + 1];
 }
 
 // max_length filter (core.ts:270-273) applied at selection time: it depends only on the pair,

@@ -3,8 +3,11 @@ at sample boundaries.
 
 Pairs never cross samples (core.ts:265-267), so rank r owns a contiguous run of whole samples and
 counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exchange:
-  1. the dense hot table (pairs of ids < 256, 65536 x u64): one all-reduce(SUM) over RCCL/xGMI;
-  2. the sparse remainder: all-gather of (key, count) lists, duplicates summed on device;
+  1. the pair table (131072 x u64: exact counts of the pairs of ids < 256 + a count sketch of
+     every other pair): one all-reduce(SUM) over RCCL/xGMI;
+  2. only when a sketch bucket could still reach the best hot count: every rank counts those cold
+     pairs exactly (one more streaming pass), then an all-gather of the (key, count) lists with
+     duplicates summed on device;
   3. only when several pairs tie on (W, a+b): an all-reduce(MAX) of their last counted positions
      (rule R3; rank r's positions order after rank r-1's).
 Every rank then selects the same merge (libbpe's argmax over the global tables) and applies it to
@@ -21,6 +24,7 @@ import numpy as np
 pkg = importlib.import_module('bpe-tokenizer_amd')
 
 HOT_BINS = 256 * 256
+TABLE_BINS = 2 * HOT_BINS
 RANK_SHIFT = 40          # global position = rank << 40 | shard-local position
 
 
@@ -48,27 +52,33 @@ class GpuShard:
         self.engine = engine
         self.torch = torch
         self.device = torch.device('cuda', device_index)
-        self.hot = torch.zeros(HOT_BINS, dtype=torch.int64, device=self.device)
+        self.table = torch.zeros(TABLE_BINS, dtype=torch.int64, device=self.device)
         self.cap = 1 << 16
         self.keys = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
         self.counts = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
 
     def export(self):
+        self.engine.export_counts(self.table.data_ptr())
+        return self.table
+
+    def heavy(self, table, max_length):
         torch = self.torch
-        n = self.engine.export_counts(self.hot.data_ptr(), self.keys.data_ptr(),
-                                      self.counts.data_ptr(), self.cap)
+        table = table.contiguous()
+        n = self.engine.heavy_counts(table.data_ptr(), self.keys.data_ptr(), self.counts.data_ptr(),
+                                     self.cap, max_length)
         if n > self.cap:
             self.cap = 1 << max(16, int(n - 1).bit_length())
             self.keys = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
             self.counts = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
-            n = self.engine.export_counts(self.hot.data_ptr(), self.keys.data_ptr(),
-                                          self.counts.data_ptr(), self.cap)
-        return self.hot, self.keys[:n], self.counts[:n]
+            n = self.engine.heavy_counts(table.data_ptr(), self.keys.data_ptr(),
+                                         self.counts.data_ptr(), self.cap, max_length)
+        return self.keys[:n], self.counts[:n]
 
-    def select(self, hot, keys, counts, max_length, min_weight):
+    def select(self, table, keys, counts, max_length, min_weight):
+        table = table.contiguous()
         keys = keys.contiguous()
         counts = counts.contiguous()
-        return self.engine.select_counts(hot.data_ptr(), keys.data_ptr() if keys.numel() else None,
+        return self.engine.select_counts(table.data_ptr(), keys.data_ptr() if keys.numel() else None,
                                          counts.data_ptr() if counts.numel() else None,
                                          keys.numel(), max_length, min_weight)
 
@@ -83,12 +93,15 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
     """The per-iteration collective protocol.  Returns (a, b, W) or None, identical on every rank.
     Collectives run on the tables' device (RCCL); with the gloo backend on host copies."""
     import torch
-    hot, keys, counts = shard.export()
-    dev = torch.device('cpu') if dist.get_backend() == 'gloo' else hot.device
-    hot = hot.to(dev, copy=True)
+    table = shard.export()
+    dev = torch.device('cpu') if dist.get_backend() == 'gloo' else table.device
+    sdev = getattr(shard, 'device', dev)
+    table = table.to(dev, copy=True)
+    dist.all_reduce(table)
+    gtable = table.to(sdev)
+    keys, counts = shard.heavy(gtable, max_length)           # identical decision on every rank
     keys = keys.to(dev)
     counts = counts.to(dev)
-    dist.all_reduce(hot)
     n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
@@ -110,8 +123,7 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
     else:
         ukeys = torch.zeros(0, dtype=torch.int32, device=dev)
         ucounts = torch.zeros(0, dtype=torch.int64, device=dev)
-    sdev = getattr(shard, 'device', dev)
-    sel = shard.select(hot.to(sdev), ukeys.to(sdev), ucounts.to(sdev), max_length, min_weight)
+    sel = shard.select(gtable, ukeys.to(sdev), ucounts.to(sdev), max_length, min_weight)
     if sel is None:
         return None
     w, cands = sel

@@ -113,19 +113,28 @@ int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_
  * selects from the global table.  All table pointers below are DEVICE pointers on this context's
  * device (e.g. torch tensors); host pointers are marked.
  *
- * bpe_export_counts: this shard's pair counts for the current corpus (one streaming pass if none
- * are cached): hot[65536] u64 counts of pairs with both ids < 256 at a*256+b, and the sparse rest
- * as cold_keys[i] = a<<16|b (u32) with cold_counts[i] (u64).  *n_cold receives the number of
- * sparse entries; when it exceeds cap nothing is written and BPE_ERR_ARG is returned (retry with
- * a bigger buffer). */
-int bpe_export_counts(bpe_ctx *ctx, uint64_t *hot, uint32_t *cold_keys, uint64_t *cold_counts,
-                      int64_t cap, int64_t *n_cold);
+ * The pair-count table has BPE_TABLE_BINS u64 entries: [0, 65536) exact counts of the pairs with
+ * both ids < 256 at a*256+b, [65536, 131072) a count sketch of every other pair (bucket =
+ * ((a<<16|b) * 0x9E3779B1 mod 2^32) >> 16): an upper bound of each such pair's count. */
+#define BPE_HOT_BINS 65536
+#define BPE_TABLE_BINS 131072
 
-/* findNextMerge's selection (core.ts:294-313) over GLOBAL tables (hot as above; cold entries with
- * distinct keys).  Writes W and the candidate pairs sharing the best (W, a+b) as host int32
- * (a, b) pairs into cand (capacity cap pairs); *n_cand may exceed cap (then only cap written).
- * BPE_NO_MERGE when the reference would return null. */
-int bpe_select_counts(bpe_ctx *ctx, const uint64_t *hot, const uint32_t *cold_keys,
+/* This shard's table for the current corpus (one streaming pass if none is cached). */
+int bpe_export_counts(bpe_ctx *ctx, uint64_t *table);
+
+/* Given the GLOBAL (summed) table: the cold pairs whose sketch bucket reaches the best hot count
+ * (the only ones that can still win) are counted exactly on this shard (one streaming pass) and
+ * written as cold_keys[i] = a<<16|b (u32), cold_counts[i] (u64).  *n_cold = entries (0 and no
+ * pass when no bucket qualifies); when *n_cold > cap nothing is written and BPE_ERR_ARG is
+ * returned (retry with a bigger buffer). */
+int bpe_heavy_counts(bpe_ctx *ctx, const uint64_t *table, int64_t max_length, uint32_t *cold_keys,
+                     uint64_t *cold_counts, int64_t cap, int64_t *n_cold);
+
+/* findNextMerge's selection (core.ts:294-313) over the GLOBAL table's exact hot bins plus the
+ * GLOBAL exact cold entries (distinct keys).  Writes W and the candidate pairs sharing the best
+ * (W, a+b) as host int32 (a, b) pairs into cand (capacity cap pairs); *n_cand may exceed cap
+ * (then only cap written).  BPE_NO_MERGE when the reference would return null. */
+int bpe_select_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *cold_keys,
                       const uint64_t *cold_counts, int64_t n_cold, int64_t max_length,
                       int64_t min_weight, int32_t *cand, int64_t cap, int64_t *n_cand,
                       int64_t *w);
@@ -146,6 +155,7 @@ typedef struct {
     int64_t iterations;       /* findNextMerge calls */
     int64_t live_tokens;      /* sum over those calls of live corpus tokens (pair-scans) */
     int64_t compactions;      /* dead-slot compactions */
+    int64_t exact_passes;     /* extra streaming passes for cold pairs whose sketch bucket could win */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

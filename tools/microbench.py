@@ -47,7 +47,7 @@ def main():
                                (st['step_ms'] / max(1, st['step_launches']) * 1e-3) / 1e9,
         'select_ms_per_iter': st['select_ms'] / steps,
         'wall_ms_per_iter': dt * 1e3 / steps,
-        'tie_passes': st['tie_passes'],
+        'tie_passes': st['tie_passes'], 'exact_passes': st['exact_passes'], 'compactions': st['compactions'],
     }
     print(json.dumps(out))
 
