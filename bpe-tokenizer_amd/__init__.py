@@ -220,7 +220,12 @@ class Engine:
                     'bpe_find_next_merge')
         return None if rc == BPE_NO_MERGE else (a.value, b.value, w.value)
 
-    def apply_merge(self, a, b, c):
+    def apply_merge(self, a, b, c, sync=True):
+        """applyMerge's corpus rewrite.  With sync=False the replacement count stays on the device
+        (settled at the next engine call; no host round trip) and None is returned."""
+        if not sync:
+            _check(lib().bpe_apply_merge(self._ctx, a, b, c, None), 'bpe_apply_merge')
+            return None
         r = ctypes.c_int64()
         _check(lib().bpe_apply_merge(self._ctx, a, b, c, ctypes.byref(r)), 'bpe_apply_merge')
         return r.value

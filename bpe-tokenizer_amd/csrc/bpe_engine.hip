@@ -84,10 +84,16 @@ struct bpe_ctx {
     ColdTable cold{};
     uint32_t *d_cold_flags = nullptr;   // [0] n_used, [1] overflow
     uint64_t cold_cap = 0;
+    // an applied merge whose replacement count is still on the device (settled at the next sync)
+    bool pending = false;
+    int32_t pend_a = 0, pend_b = 0, pend_c = 0;
+    int64_t pend_expect = -1;    // W the replacement count must equal (mergeUntil), -1 = any
+    int2 *h_cand = nullptr;      // pinned: first MAX_CAND candidates come back with the Result
     bool counts_valid = false;   // d_hot + cold table describe the current corpus
     bool carry_valid = false;    // d_sums / d_carry describe the current corpus and geometry
     int64_t cpr = 0;
     int R = 0, G = 0;
+    int64_t last_replaced = 0;
     // stats
     bool stats_on = false;
     bpe_stats stats{};
@@ -218,8 +224,14 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 // One streaming pass: (optionally apply the merge a,b -> cc, then) count every pair, stitch the
 // region boundaries and reduce the hot table.  Leaves counts + carries valid for the new corpus.
 // With a merge, *replaced receives the number of replacements.
+int settle(bpe_ctx *c);
+int settle_with(bpe_ctx *c, unsigned long long R);
+int maybe_compact(bpe_ctx *c);
+
 int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
+    if (merge && c->pending)
+        if ((rc = settle(c))) return rc;
     geometry(c);
     if (c->G > c->partials_wg) {   // one 128 KiB slab per workgroup of the pass
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -245,10 +257,9 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
                                                           c->cold, c->d_heavy);
     k_reduce_table<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[2], s));
-    HIP_TRY(hipStreamSynchronize(s));
     if (c->stats_on) {
+        HIP_TRY(hipEventRecord(c->ev[2], s));
+        HIP_TRY(hipEventSynchronize(c->ev[2]));
         c->stats.step_ms += ev_ms(c->ev[0], c->ev[1]);
         c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
         c->stats.step_launches += 1;
@@ -256,18 +267,46 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         c->stats.step_live += c->n_live;
     }
     if (merge) {
-        const int64_t R = (int64_t)c->h_res->replaced;
-        c->n_live -= R;
-        c->live_slots -= R;
-        c->h_count[a] -= R;
-        c->h_count[b] -= R;
-        c->h_count[cc] += R;
-        if (R) c->packed = false;
-        if (replaced) *replaced = R;
+        // the replacement count stays on the device until the next sync point (settle)
+        c->pending = true;
+        c->pend_a = a;
+        c->pend_b = b;
+        c->pend_c = cc;
+        c->pend_expect = -1;
+        if (replaced) {
+            int rc2 = settle(c);
+            if (rc2) return rc2;
+            *replaced = c->last_replaced;
+        }
     }
     c->counts_valid = true;
     c->carry_valid = true;
     return BPE_OK;
+}
+
+// Host accounting of an applied merge once its replacement count R is known.
+int settle_with(bpe_ctx *c, unsigned long long Ru) {
+    if (!c->pending) return BPE_OK;
+    c->pending = false;
+    const int64_t R = (int64_t)Ru;
+    c->last_replaced = R;
+    c->n_live -= R;
+    c->live_slots -= R;
+    c->h_count[c->pend_a] -= R;
+    c->h_count[c->pend_b] -= R;
+    c->h_count[c->pend_c] += R;
+    if (R) c->packed = false;
+    if (c->pend_expect >= 0 && R != c->pend_expect)
+        return fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+    return BPE_OK;
+}
+
+int settle(bpe_ctx *c) {
+    if (!c->pending) return BPE_OK;
+    unsigned long long R = 0;
+    HIP_TRY(hipMemcpyAsync(&R, &c->d_res->replaced, sizeof R, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return settle_with(c, R);
 }
 
 // Moves the live slots to a dense prefix (when dead slots waste too much of the stream, and
@@ -339,27 +378,30 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     int rc;
     if ((rc = sync_len16(c))) return rc;
     hipStream_t s = c->stream;
-    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(table, c->d_len16, max_length, c->d_res);
-    k_heavy<<<SKETCH_BINS / 256, 256, 0, s>>>(table, c->d_res, c->d_heavy);
+    k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand, c->d_heavy);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if ((rc = settle_with(c, c->h_res->replaced))) return rc;   // a pending apply's R came along
     if (c->h_res->n_heavy && local) {
+        // some cold pair may still reach W: count those exactly, then recollect hot + cold
         if ((rc = exact_pass(c))) return rc;
+        HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
         k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
+        k_collect<<<HOT_BINS / 256, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
+                                                 c->d_cand);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
     }
-    k_collect<<<HOT_BINS / 256, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
-                                             c->d_cand);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
     const unsigned n_cand = std::min<unsigned>(c->h_res->n_cand, CAND_CAP);
-    cand.resize(n_cand);
-    if (n_cand)
+    cand.assign(c->h_cand, c->h_cand + std::min<unsigned>(n_cand, MAX_CAND));
+    if (n_cand > (unsigned)MAX_CAND) {
+        cand.resize(n_cand);
         HIP_TRY(hipMemcpy(cand.data(), c->d_cand, n_cand * sizeof(int2), hipMemcpyDeviceToHost));
+    }
     return BPE_OK;
 }
 
@@ -403,8 +445,9 @@ int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long l
 int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int32_t *b,
             int64_t *w) {
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
-    if (c->n_live < 2) return BPE_NO_MERGE;
     int rc;
+    if ((rc = settle(c))) return rc;
+    if (c->n_live < 2) return BPE_NO_MERGE;
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     hipStream_t s = c->stream;
@@ -460,15 +503,17 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                   // core.ts:318
     c->len16_dirty = true;
     if (replaced) *replaced = 0;
+    if ((rc = settle(c))) return rc;
+    if ((rc = maybe_compact(c))) return rc;
     if (c->n_live < 2) return BPE_OK;
     if (!c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    if ((rc = run_pass(c, true, a, b, cc, replaced))) return rc;
-    return maybe_compact(c);
+    return run_pass(c, true, a, b, cc, replaced);
 }
 
 int append_begin(bpe_ctx *c, int64_t extra_slots) {
     int rc;
+    if ((rc = settle(c))) return rc;
     if (!c->packed)
         if ((rc = compact(c))) return rc;
     return ensure_chunks(c, (c->live_slots + extra_slots + CHUNK - 1) / CHUNK);
@@ -526,6 +571,8 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = dev_alloc(&c->d_res, 1))) return bail(rc);
     if ((rc = dev_alloc(&c->d_cand, CAND_CAP))) return bail(rc);
     if ((rc = dev_alloc(&c->d_cold_flags, 4))) return bail(rc);
+    if (hipHostMalloc((void **)&c->h_cand, MAX_CAND * sizeof(int2), hipHostMallocDefault) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipMemset(c->d_cold_flags, 0, 16) != hipSuccess)
@@ -554,6 +601,7 @@ int bpe_destroy(bpe_ctx *c) {
                     c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
+    if (c->h_cand) (void)hipHostFree(c->h_cand);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -701,6 +749,7 @@ int bpe_clear_corpus(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     c->live_slots = c->n_samples = c->n_live = 0;
     std::fill(c->h_count.begin(), c->h_count.end(), 0);
     if ((rc = seal_packed(c))) return rc;
@@ -710,6 +759,9 @@ int bpe_clear_corpus(bpe_ctx *c) {
 
 int bpe_corpus_size(bpe_ctx *c, int64_t *n_samples, int64_t *n_tokens) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     if (n_samples) *n_samples = c->n_samples;
     if (n_tokens) *n_tokens = c->n_live;
     return BPE_OK;
@@ -722,6 +774,7 @@ int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *samp
         return fail(BPE_ERR_ARG, "bpe native: read_corpus buffers too small");
     int rc = set_device(c);
     if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     const int64_t slots = c->n_chunks * CHUNK;
     std::vector<int32_t> buf(slots);
     if (slots)
@@ -773,9 +826,8 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
         if (rc == BPE_NO_MERGE) break;
         if (rc) return rc;
         const int32_t cc = (int32_t)c->h_len16.size();
-        int64_t rep = 0;
-        if ((rc = do_apply(c, a, b, cc, &rep))) return rc;
-        if (rep != w) return fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+        if ((rc = do_apply(c, a, b, cc, nullptr))) return rc;
+        if (c->pending) c->pend_expect = w;    // checked when the count comes back
         if (n < cap) {
             out_abw[3 * n] = a;
             out_abw[3 * n + 1] = b;
@@ -784,13 +836,14 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
         ++n;
     }
     *n_merges = n;
-    return BPE_OK;
+    return settle(c);
 }
 
 int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
     if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(uint64_t), hipMemcpyDeviceToDevice,
@@ -804,6 +857,7 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     if (!c || !table || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     if ((rc = sync_len16(c))) return rc;
     hipStream_t s = c->stream;
     const auto *t = (const unsigned long long *)table;
@@ -905,6 +959,7 @@ int bpe_recount(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
+    if ((rc = settle(c))) return rc;
     return run_pass(c, false, 0, 0, 0, nullptr);
 }
 

@@ -755,7 +755,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
 // Sums the per-workgroup 8-bit LDS partials and the spill table into the u64 table
 // (hot bins [0, 64K), sketch buckets [64K, 128K)).
 __global__ void k_reduce_table(const uint32_t *__restrict__ partials, int G,
-                               const unsigned long long *__restrict__ spill,
+                               unsigned long long *__restrict__ spill,
                                unsigned long long *__restrict__ table) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= HIST_WORDS) return;
@@ -768,7 +768,10 @@ __global__ void k_reduce_table(const uint32_t *__restrict__ partials, int G,
         acc[3] += p >> 24;
     }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) table[4 * w + b] = acc[b] + spill[4 * w + b];
+    for (int b = 0; b < 4; ++b) {
+        table[4 * w + b] = acc[b] + spill[4 * w + b];
+        spill[4 * w + b] = 0;   // ready for the next pass (no memset launch)
+    }
 }
 
 // Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there
@@ -820,6 +823,55 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
     }
     best = wave_max_u64(best);
     if ((threadIdx.x & 63) == 0 && best) atomicMax(&res->best, best);
+}
+
+// One workgroup: best hot key (wave + LDS max), the hot pairs sharing it, and the heavy sketch
+// buckets (sum >= max(W_hot, 1)).  Replaces three launches and their atomics on the fast path.
+__global__ void __launch_bounds__(1024) k_select(const unsigned long long *__restrict__ table,
+                                                 const int32_t *__restrict__ len16,
+                                                 int64_t max_length, Result *res, int2 *cand,
+                                                 uint32_t *__restrict__ heavy) {
+    __shared__ unsigned long long s_best[16];
+    __shared__ unsigned int s_n, s_heavy;
+    const int t = threadIdx.x;
+    unsigned long long best = 0;
+    for (int bin = t; bin < HOT_BINS; bin += 1024) {
+        const int32_t a = bin >> 8, b = bin & 255;
+        if (!pair_ok(a, b, len16, max_length)) continue;
+        const unsigned long long k = pack_key(table[bin], a, b);
+        best = k > best ? k : best;
+    }
+    best = wave_max_u64(best);
+    if ((t & 63) == 0) s_best[t >> 6] = best;
+    if (t == 0) s_n = s_heavy = 0;
+    __syncthreads();
+    best = 0;
+    for (int i = 0; i < 16; ++i) best = s_best[i] > best ? s_best[i] : best;
+    if (best)
+        for (int bin = t; bin < HOT_BINS; bin += 1024) {
+            const int32_t a = bin >> 8, b = bin & 255;
+            if (pair_ok(a, b, len16, max_length) && pack_key(table[bin], a, b) == best) {
+                const unsigned i = atomicAdd(&s_n, 1u);
+                if (i < CAND_CAP) cand[i] = make_int2(a, b);
+            }
+        }
+    const unsigned long long w_hot = best >> 17;
+    const unsigned long long T = w_hot ? w_hot : 1;
+    for (int b0 = 0; b0 < SKETCH_BINS; b0 += 1024) {
+        const int b = b0 + t;
+        const unsigned long long m = __ballot(table[HOT_BINS + b] >= T);
+        if ((t & 31) == 0) {
+            const uint32_t word = (uint32_t)(m >> (t & 32));
+            heavy[b >> 5] = word;
+            if (word) atomicAdd(&s_heavy, (unsigned)__popc(word));
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        res->best = best;
+        res->n_cand = s_n;
+        res->n_heavy = s_heavy;
+    }
 }
 
 __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, int32_t b) {

@@ -196,7 +196,7 @@ class ShardedTrainer:
             return None
         a, b, w = m
         if self.world == 1:
-            self.engine.apply_merge(a, b, self.n_tokens)
+            self.engine.apply_merge(a, b, self.n_tokens, sync=False)
         else:
             self.shard.apply(a, b, self.n_tokens)
         self.n_tokens += 1
