@@ -33,7 +33,7 @@ C_API = [
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions',
 ]
 HOT_BINS = 65536
-TABLE_BINS = 131072
+TABLE_BINS = 81920
 
 
 class BpeError(RuntimeError):

@@ -41,6 +41,8 @@ inline void dfree(void *p) {
     if (p) (void)hipFree(p);
 }
 
+static_assert(TABLE_BINS == BPE_TABLE_BINS && HOT_BINS == BPE_HOT_BINS, "include/bpe.h table layout");
+
 template <typename T>
 int dev_alloc(T **p, size_t n) {
     *p = nullptr;
@@ -233,14 +235,14 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     if (merge && c->pending)
         if ((rc = settle(c))) return rc;
     geometry(c);
-    if (c->G > c->partials_wg) {   // one 128 KiB slab per workgroup of the pass
+    if (c->G > c->partials_wg) {   // one 160 KiB slab per workgroup of the pass
         HIP_TRY(hipStreamSynchronize(c->stream));
         dfree(c->d_partials);
         if ((rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS))) return rc;
         c->partials_wg = c->G;
     }
     hipStream_t s = c->stream;
-    HIP_TRY(hipMemsetAsync(c->d_spill, 0, TABLE_BINS * sizeof(unsigned long long), s));
+    // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
     if (merge)
@@ -562,6 +564,8 @@ int bpe_create(bpe_ctx **out, int device) {
     for (auto &e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(fail(BPE_ERR_HIP, "bpe native: event"));
     if ((rc = dev_alloc(&c->d_spill, TABLE_BINS))) return bail(rc);
+    if (hipMemset(c->d_spill, 0, TABLE_BINS * sizeof(unsigned long long)) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipMemset failed"));
     if ((rc = dev_alloc(&c->d_hot, TABLE_BINS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_heavy, HEAVY_WORDS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_total, 2))) return bail(rc);

@@ -33,13 +33,13 @@ constexpr int MAX_WG = 256;                 // one per CU on MI355X
 constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
 constexpr int HOT = 256;                    // ids < HOT form the dense LDS histogram
 constexpr int HOT_BINS = HOT * HOT;
-constexpr int SKETCH_BINS = 65536;          // count sketch of the cold pairs (ids >= HOT)
-constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, [64K, 128K) sketch
-constexpr int HIST_WORDS = TABLE_BINS / 4;  // four 8-bit counters per LDS dword (128 KiB)
+constexpr int SKETCH_BINS = 16384;          // count sketch of the cold pairs (an id >= HOT)
+constexpr int SKETCH_SHIFT = 18;            // bucket = (key * golden) >> SKETCH_SHIFT
+constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, then the sketch
+constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword: 160 KiB, all of it
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
 enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1 };
-constexpr int PACK_INTS = CHUNK;            // per-wave LDS staging for re-packing a chunk
-constexpr size_t STEP_LDS = HIST_WORDS * 4 + WAVES_PER_WG * PACK_INTS * 4;   // 144 KiB
+constexpr size_t STEP_LDS = HIST_WORDS * 4;
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -141,12 +141,12 @@ __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
 // Table index of a pair: its exact bin when both ids are hot, else its sketch bucket.
 __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
     if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) return (x << 8) | y;
-    return HOT_BINS + (int)((pair_key(x, y) * 0x9E3779B1u) >> 16);
+    return HOT_BINS + (int)((pair_key(x, y) * 0x9E3779B1u) >> SKETCH_SHIFT);
 }
 
-// Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup 8-bit LDS table (hot bins
-// exact + cold sketch) with a global u64 spill.  MODE_EXACT: exact counts of the cold pairs whose
-// sketch bucket is marked heavy, into the sparse table; everything else is ignored.
+// Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup LDS table (exact hot bins +
+// cold sketch buckets, 16-bit counters) with a global u64 spill.  MODE_EXACT: exact counts of the
+// cold pairs whose sketch bucket is marked heavy, into the sparse table; the rest is ignored.
 struct Sink {
     uint32_t *hist;                  // LDS table (MODE_TABLE)
     unsigned long long *spill;       // global u64 [TABLE_BINS]
@@ -171,19 +171,22 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
     else if (exact_wanted<MODE>(k, x, y)) cold_add(k.ct, pair_key(x, y), (uint32_t)n);
 }
 
-// LDS 8-bit counter increment; a counter reaching 0x80 spills 0x80 to the global table (exactly
-// one lane observes each 0x7F -> 0x80 transition, so nothing is lost or double counted).
-__device__ __forceinline__ uint32_t lds_inc8(uint32_t *hist, int idx) {
-    return atomicAdd(&hist[idx >> 2], 1u << ((idx & 3) << 3));
+// 16-bit LDS counters, two per dword.  A counter reaching 0x8000 spills 0x8000 to the global u64
+// table: exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom
+// absorbs every add that lands before its subtraction (a CU issues far fewer in flight), so no
+// field ever carries into its neighbour.
+__device__ __forceinline__ uint32_t lds_inc(uint32_t *hist, int idx) {
+    return atomicAdd(&hist[idx >> 1], 1u << ((idx & 1) << 4));
 }
 
-__device__ __forceinline__ void lds_fix8(uint32_t *hist, int idx, uint32_t old,
-                                         unsigned long long *spill) {
-    const uint32_t sh = (idx & 3) << 3;
-    if (((old >> sh) & 0xFFu) == 0x7Fu) {
-        atomicSub(&hist[idx >> 2], 0x80u << sh);
-        atomicAdd(&spill[idx], 0x80ull);
-    }
+__device__ __forceinline__ bool lds_needs_fix(int idx, uint32_t old) {
+    return ((old >> ((idx & 1) << 4)) & 0xFFFFu) == 0x7FFFu;
+}
+
+__device__ __forceinline__ void lds_fix(const Sink &k, int idx, uint32_t old) {
+    if (!lds_needs_fix(idx, old)) return;
+    atomicSub(&k.hist[idx >> 1], 0x8000u << ((idx & 1) << 4));
+    atomicAdd(&k.spill[idx], 0x8000ull);
 }
 
 // One counted occurrence of (x, y).
@@ -191,7 +194,7 @@ template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
     if (MODE == MODE_TABLE) {
         const int idx = table_index(x, y);
-        lds_fix8(k.hist, idx, lds_inc8(k.hist, idx), k.spill);
+        lds_fix(k, idx, lds_inc(k.hist, idx));
     } else if (exact_wanted<MODE>(k, x, y)) {
         cold_add(k.ct, pair_key(x, y), 1u);
     }
@@ -365,17 +368,15 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
                 // one overflow test
                 const int i0 = table_index(t0, t1), i1 = table_index(t1, t2),
                           i2 = table_index(t2, t3), i3 = table_index(t3, t4);
-                const uint32_t o0 = lds_inc8(k.hist, i0), o1 = lds_inc8(k.hist, i1),
-                               o2 = lds_inc8(k.hist, i2), o3 = lds_inc8(k.hist, i3);
-                const int ovf = (int)(((o0 >> ((i0 & 3) << 3)) & 0xFFu) == 0x7Fu) |
-                                (int)(((o1 >> ((i1 & 3) << 3)) & 0xFFu) == 0x7Fu) |
-                                (int)(((o2 >> ((i2 & 3) << 3)) & 0xFFu) == 0x7Fu) |
-                                (int)(((o3 >> ((i3 & 3) << 3)) & 0xFFu) == 0x7Fu);
-                if (ovf) {
-                    lds_fix8(k.hist, i0, o0, k.spill);
-                    lds_fix8(k.hist, i1, o1, k.spill);
-                    lds_fix8(k.hist, i2, o2, k.spill);
-                    lds_fix8(k.hist, i3, o3, k.spill);
+                const uint32_t o0 = lds_inc(k.hist, i0), o1 = lds_inc(k.hist, i1),
+                               o2 = lds_inc(k.hist, i2), o3 = lds_inc(k.hist, i3);
+                const int fix = (int)lds_needs_fix(i0, o0) | (int)lds_needs_fix(i1, o1) |
+                                (int)lds_needs_fix(i2, o2) | (int)lds_needs_fix(i3, o3);
+                if (fix) {
+                    lds_fix(k, i0, o0);
+                    lds_fix(k, i1, o1);
+                    lds_fix(k, i2, o2);
+                    lds_fix(k, i3, o3);
                 }
             } else {
                 const int32_t x[5] = {t0, t1, t2, t3, t4};
@@ -481,7 +482,6 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
        unsigned long long *__restrict__ replaced) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t *hist = lds;
-    int32_t *pack = reinterpret_cast<int32_t *>(lds + HIST_WORDS) + (threadIdx.x >> 6) * PACK_INTS;
     if (MODE == MODE_TABLE) {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
@@ -595,23 +595,23 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
                     const int nk = (int)keep[0] + keep[1] + keep[2] + keep[3];
                     const int incl = wave_incl_sum(nk, lane);
                     const int total = bcast(incl, 63);
+                    // re-pack through the chunk itself (the LDS is all pair table): kept values
+                    // go to their packed slots, vacated slots become TOMB, then the wave reads the
+                    // chunk back.  Same-CU global stores are visible to the CU's later loads once
+                    // the workgroup-scope release (s_waitcnt vmcnt(0)) has completed them.
+                    int32_t *cp = ids + c * CHUNK;
                     int pp = incl - nk;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (keep[e]) pack[pp++] = m[e] ? mc : w.t[e];
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    int32_t y[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int k = 4 * lane + e;
-                        y[e] = k < total ? pack[k] : TOMB;
+                        if (keep[e]) cp[pp++] = m[e] ? mc : w.t[e];
+                        if (k >= total && k < w.len) cp[k] = TOMB;
                     }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    v4[c * 64 + lane] = make_int4(y[0], y[1], y[2], y[3]);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    const int4 yv = v4[c * 64 + lane];
+                    const int32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
                     n_match += __popcll(__ballot(m[0])) + __popcll(__ballot(m[1])) +
                                __popcll(__ballot(m[2])) + __popcll(__ballot(m[3]));
 #pragma unroll
@@ -752,26 +752,23 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     }
 }
 
-// Sums the per-workgroup 8-bit LDS partials and the spill table into the u64 table
-// (hot bins [0, 64K), sketch buckets [64K, 128K)).
+// Sums the per-workgroup 16-bit LDS partials and the spill table into the u64 table
+// (hot bins [0, 64K), sketch buckets [64K, TABLE_BINS)), and zeroes the spill for the next pass.
 __global__ void k_reduce_table(const uint32_t *__restrict__ partials, int G,
                                unsigned long long *__restrict__ spill,
                                unsigned long long *__restrict__ table) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= HIST_WORDS) return;
-    uint32_t acc[4] = {0, 0, 0, 0};   // < 2^24 per byte lane: G <= 256 slabs of < 256 each
+    unsigned long long lo = 0, hi = 0;   // G <= 256 slabs of < 2^15 each
     for (int g = 0; g < G; ++g) {
         const uint32_t p = partials[(size_t)g * HIST_WORDS + w];
-        acc[0] += p & 0xFFu;
-        acc[1] += (p >> 8) & 0xFFu;
-        acc[2] += (p >> 16) & 0xFFu;
-        acc[3] += p >> 24;
+        lo += p & 0xFFFFu;
+        hi += p >> 16;
     }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        table[4 * w + b] = acc[b] + spill[4 * w + b];
-        spill[4 * w + b] = 0;   // ready for the next pass (no memset launch)
-    }
+    table[2 * w] = lo + spill[2 * w];
+    table[2 * w + 1] = hi + spill[2 * w + 1];
+    spill[2 * w] = 0;
+    spill[2 * w + 1] = 0;
 }
 
 // Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there

@@ -3,7 +3,7 @@ at sample boundaries.
 
 Pairs never cross samples (core.ts:265-267), so rank r owns a contiguous run of whole samples and
 counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exchange:
-  1. the pair table (131072 x u64: exact counts of the pairs of ids < 256 + a count sketch of
+  1. the pair table (81920 x u64: exact counts of the pairs of ids < 256 + a count sketch of
      every other pair): one all-reduce(SUM) over RCCL/xGMI;
   2. only when a sketch bucket could still reach the best hot count: every rank counts those cold
      pairs exactly (one more streaming pass), then an all-gather of the (key, count) lists with
@@ -24,7 +24,7 @@ import numpy as np
 pkg = importlib.import_module('bpe-tokenizer_amd')
 
 HOT_BINS = 256 * 256
-TABLE_BINS = 2 * HOT_BINS
+TABLE_BINS = HOT_BINS + 16384
 RANK_SHIFT = 40          # global position = rank << 40 | shard-local position
 
 

@@ -114,10 +114,10 @@ int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_
  * device (e.g. torch tensors); host pointers are marked.
  *
  * The pair-count table has BPE_TABLE_BINS u64 entries: [0, 65536) exact counts of the pairs with
- * both ids < 256 at a*256+b, [65536, 131072) a count sketch of every other pair (bucket =
- * ((a<<16|b) * 0x9E3779B1 mod 2^32) >> 16): an upper bound of each such pair's count. */
+ * both ids < 256 at a*256+b, [65536, 81920) a count sketch of every other pair (bucket =
+ * ((a<<16|b) * 0x9E3779B1 mod 2^32) >> 18): an upper bound of each such pair's count. */
 #define BPE_HOT_BINS 65536
-#define BPE_TABLE_BINS 131072
+#define BPE_TABLE_BINS 81920
 
 /* This shard's table for the current corpus (one streaming pass if none is cached). */
 int bpe_export_counts(bpe_ctx *ctx, uint64_t *table);

@@ -26,7 +26,7 @@ def index(a, b):
     """Table index of libbpe's pair table (include/bpe.h): hot bin, or cold sketch bucket."""
     if a < 256 and b < 256:
         return (a << 8) | b
-    return 65536 + ((((a << 16) | b) * 0x9E3779B1) & 0xFFFFFFFF) >> 16
+    return 65536 + ((((a << 16) | b) * 0x9E3779B1) & 0xFFFFFFFF) >> 18
 
 
 class OracleShard:
@@ -41,7 +41,7 @@ class OracleShard:
         pa, pb, pc, self._last = self.st.count_pairs()
         self._pairs = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(pa, pb))}
         self._cold = [(int(a), int(b), int(c)) for a, b, c in zip(pa, pb, pc) if a >= 256 or b >= 256]
-        table = np.zeros(2 * 65536, np.int64)
+        table = np.zeros(65536 + 16384, np.int64)
         for a, b, c in zip(pa.tolist(), pb.tolist(), pc.tolist()):
             table[index(a, b)] += c
         return torch.from_numpy(table)
