@@ -17,7 +17,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libbpe.so')
+# BPE_LIB selects an experimental build of the same C ABI (tools/ kernel experiments)
+LIB_PATH = os.environ.get('BPE_LIB') or os.path.join(HERE, 'libbpe.so')
 
 BPE_OK = 0
 BPE_NO_MERGE = 1

@@ -246,11 +246,11 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
     if (merge)
-        k_step<true, MODE_TABLE><<<c->G, WG, STEP_LDS, s>>>(
+        k_step<true, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     else
-        k_step<false, MODE_TABLE><<<c->G, WG, STEP_LDS, s>>>(
+        k_step<false, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     HIP_TRY(hipGetLastError());
@@ -358,7 +358,7 @@ int exact_pass(bpe_ctx *c) {
     hipStream_t s = c->stream;
     k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
     HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
-    k_step<false, MODE_EXACT><<<c->G, WG, STEP_LDS, s>>>(
+    k_step<false, MODE_EXACT><<<c->G, WG, 0, s>>>(
         c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
         c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
@@ -584,13 +584,6 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = ensure_chunks(c, 1))) return bail(rc);
     if ((rc = ensure_vocab(c, 0))) return bail(rc);
     if ((rc = ensure_cold(c, 0))) return bail(rc);
-    if (hipFuncSetAttribute((const void *)k_step<true, MODE_TABLE>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_step<false, MODE_TABLE>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_step<false, MODE_EXACT>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)STEP_LDS) != hipSuccess)
-        return bail(fail(BPE_ERR_HIP, "bpe native: cannot reserve 144 KiB of LDS"));
     if ((rc = seal_packed(c))) return bail(rc);
     *out = c;
     return BPE_OK;

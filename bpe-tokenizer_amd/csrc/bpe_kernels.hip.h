@@ -39,7 +39,6 @@ constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs
 constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword: 160 KiB, all of it
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
 enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1 };
-constexpr size_t STEP_LDS = HIST_WORDS * 4;
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -105,6 +104,17 @@ __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
     return v;
 }
 
+// DPP wavefront shifts by one lane (a VALU modifier: no LDS crossbar round trip, unlike
+// __shfl_*).  from_next: lane i gets lane i+1's x, lane 63 gets fill.  from_prev: lane i gets lane
+// i-1's x, lane 0 gets fill.
+__device__ __forceinline__ int32_t from_next(int32_t x, int32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, x, 0x130, 0xF, 0xF, false);   // wave_shl:1
+}
+
+__device__ __forceinline__ int32_t from_prev(int32_t x, int32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);   // wave_shr:1
+}
+
 __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint32_t inc) {
     uint32_t h = (key * 0x9E3779B1u) >> ct.shift;
     for (uint32_t probes = 0;; ++probes) {
@@ -139,9 +149,16 @@ __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
 }
 
 // Table index of a pair: its exact bin when both ids are hot, else its sketch bucket.
+// Branch-free: both forms are computed and selected (the sketch hash uses the full-rate 24-bit
+// multiplier; ids < 2^16).
+constexpr uint32_t SKETCH_MUL_A = 0x9E3779u, SKETCH_MUL_B = 0x85EBCBu;
 __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
-    if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) return (x << 8) | y;
-    return HOT_BINS + (int)((pair_key(x, y) * 0x9E3779B1u) >> SKETCH_SHIFT);
+    const uint32_t hot = ((uint32_t)x << 8) | (uint32_t)y;
+    // (HIP's __umul24 returns int: the sum must be shifted as unsigned)
+    const uint32_t h = (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) +
+                       (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
+    const uint32_t cold = HOT_BINS + (h >> SKETCH_SHIFT);
+    return ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT ? (int)hot : (int)cold;
 }
 
 // Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup LDS table (exact hot bins +
@@ -214,9 +231,13 @@ __device__ __forceinline__ View make_view(const int4 v) {
     w.t[1] = v.y;
     w.t[2] = v.z;
     w.t[3] = v.w;
-    // chunks are left-packed, so len = number of non-TOMB slots
-    w.len = __popcll(__ballot(v.x != TOMB)) + __popcll(__ballot(v.y != TOMB)) +
-            __popcll(__ballot(v.z != TOMB)) + __popcll(__ballot(v.w != TOMB));
+    // chunks are left-packed, so len = number of non-TOMB slots (256 iff the last slot is live)
+    if (__builtin_amdgcn_readlane(v.w, 63) != TOMB) {
+        w.len = CHUNK;
+    } else {
+        w.len = __popcll(__ballot(v.x != TOMB)) + __popcll(__ballot(v.y != TOMB)) +
+                __popcll(__ballot(v.z != TOMB)) + __popcll(__ballot(v.w != TOMB));
+    }
     return w;
 }
 
@@ -251,9 +272,8 @@ struct Nbr {
 
 __device__ __forceinline__ void neighbours(const View &w, int32_t prev, int32_t nxt, int lane,
                                            Nbr &n) {
-    const int32_t up = __shfl_up(w.t[3], 1);
-    const int32_t dn = __shfl_down(w.t[0], 1);
-    const int32_t pm = lane == 0 ? prev : up;
+    const int32_t dn = from_next(w.t[0], nxt);
+    const int32_t pm = from_prev(w.t[3], prev);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int k = 4 * lane + e;
@@ -350,42 +370,95 @@ __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool 
 template <int MODE>
 __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last, int lane,
                                            CountState &s, const Sink &k) {
-    if (!last && s.run_x == -2 && s.started && w.len == CHUNK) {
-        // Fast path: a full chunk with no run open across its start.  Valid when no slot is the
-        // middle of a run of >= 3 and no X X pair straddles the chunk end: then every X X pair
-        // starts its run and counts (core.ts:285-290 never skips).
+    if (!last && s.run_x == -2 && s.started) {
+        // Fast path: no run open across the chunk start.  Valid when no slot is the middle of a
+        // run of >= 3 and no X X pair ends the chunk: then every X X pair starts its run and
+        // counts (core.ts:285-290 never skips), so every valid pair (k, next live) counts.
         const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
-        const int32_t up = __shfl_up(t3, 1);
-        const int32_t dn = __shfl_down(t0, 1);
-        const int32_t p = lane == 0 ? s.prev : up;
-        const int32_t t4 = lane == 63 ? nxt : dn;
-        const bool e01 = t0 == t1, e12 = t1 == t2, e23 = t2 == t3, e34 = t3 == t4;
-        const bool trip = (p == t0 && e01) || (e01 && e12) || (e12 && e23) || (e23 && e34) ||
-                          (lane == 63 && e34 && t3 >= 0);
+        const int32_t p = from_prev(t3, s.prev);
+        const int kl = w.len - 1;
+        int32_t r0 = t1, r1 = t2, r2 = t3, r3 = from_next(t0, nxt);
+        if (MODE == MODE_TABLE && w.len == CHUNK) {
+            // Hottest path: a full chunk whose 256 pairs are all valid hot pairs (every id in
+            // [0, 256), so no SEP either) and no X X pair continues a run or ends the chunk.
+            const uint32_t u = (uint32_t)(t0 | t1 | t2 | t3 | r3);
+            const bool q0 = t0 == t1, q1 = t1 == t2, q2 = t2 == t3, q3 = t3 == r3;
+            const bool bad = u >= (uint32_t)HOT || (p == t0 && q0) || (q0 && q1) || (q1 && q2) ||
+                             (q2 && q3) || (lane == 63 && q3);
+            if (__ballot(bad) == 0ull) {
+                // bin b = x*256 + y: dword b/2 (byte (b*2) & ~3), half (y & 1)
+                const uint32_t b0 = ((uint32_t)t0 << 8) | (uint32_t)r0, b1 = ((uint32_t)t1 << 8) | (uint32_t)r1,
+                               b2 = ((uint32_t)t2 << 8) | (uint32_t)r2, b3 = ((uint32_t)t3 << 8) | (uint32_t)r3;
+                const uint32_t o0 = atomicAdd(&k.hist[b0 >> 1], 1u << ((b0 & 1) << 4));
+                const uint32_t o1 = atomicAdd(&k.hist[b1 >> 1], 1u << ((b1 & 1) << 4));
+                const uint32_t o2 = atomicAdd(&k.hist[b2 >> 1], 1u << ((b2 & 1) << 4));
+                const uint32_t o3 = atomicAdd(&k.hist[b3 >> 1], 1u << ((b3 & 1) << 4));
+                // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
+#ifdef BPE_EXP_NOCHECK
+                if (false) {
+#else
+                if (__ballot(((o0 | o1 | o2 | o3) & 0x40004000u) != 0u) != 0ull) {
+#endif
+                    const bool f0 = lds_needs_fix((int)b0, o0), f1 = lds_needs_fix((int)b1, o1),
+                               f2 = lds_needs_fix((int)b2, o2), f3 = lds_needs_fix((int)b3, o3);
+                    if (f0) lds_fix(k, (int)b0, o0);
+                    if (f1) lds_fix(k, (int)b1, o1);
+                    if (f2) lds_fix(k, (int)b2, o2);
+                    if (f3) lds_fix(k, (int)b3, o3);
+                }
+                s.n_live += CHUNK;
+                s.prev = bcast(t3, 63);
+                return;
+            }
+        }
+        bool end0 = false, end1 = false, end2 = false, end3 = lane == 63;
+        if (w.len != CHUNK) {
+            // left-packed partial chunk: the last live slot pairs with nxt, dead slots are TOMB
+            const bool ll = lane == (kl >> 2);
+            const int el = kl & 3;
+            end0 = ll && el == 0;
+            end1 = ll && el == 1;
+            end2 = ll && el == 2;
+            end3 = ll && el == 3;
+            r0 = end0 ? nxt : r0;
+            r1 = end1 ? nxt : r1;
+            r2 = end2 ? nxt : r2;
+            r3 = end3 ? nxt : r3;
+        }
+        const bool n0 = t0 >= 0 && t0 == r0, n1 = t1 >= 0 && t1 == r1, n2 = t2 >= 0 && t2 == r2,
+                   n3 = t3 >= 0 && t3 == r3;
+        const bool trip = (n0 && (t0 == p || end0)) || (n1 && (t1 == t0 || end1)) ||
+                          (n2 && (t2 == t1 || end2)) || (n3 && (t3 == t2 || end3));
         if (__ballot(trip) == 0ull) {
-            if (MODE == MODE_TABLE && __ballot((t0 | t1 | t2 | t3 | t4) < 0) == 0ull) {
-                // four valid pairs (hot bins or sketch buckets): four LDS atomics in flight,
-                // one overflow test
-                const int i0 = table_index(t0, t1), i1 = table_index(t1, t2),
-                          i2 = table_index(t2, t3), i3 = table_index(t3, t4);
-                const uint32_t o0 = lds_inc(k.hist, i0), o1 = lds_inc(k.hist, i1),
-                               o2 = lds_inc(k.hist, i2), o3 = lds_inc(k.hist, i3);
-                const int fix = (int)lds_needs_fix(i0, o0) | (int)lds_needs_fix(i1, o1) |
-                                (int)lds_needs_fix(i2, o2) | (int)lds_needs_fix(i3, o3);
-                if (fix) {
-                    lds_fix(k, i0, o0);
-                    lds_fix(k, i1, o1);
-                    lds_fix(k, i2, o2);
-                    lds_fix(k, i3, o3);
+            const bool v0 = (t0 | r0) >= 0, v1 = (t1 | r1) >= 0, v2 = (t2 | r2) >= 0,
+                       v3 = (t3 | r3) >= 0;
+            if (MODE == MODE_TABLE) {
+                // four LDS atomics in flight, one overflow test; an invalid pair (SEP, dead
+                // slot) adds 0 to a lane-private word instead of branching
+                const int i0 = v0 ? table_index(t0, r0) : 8 * lane + 0;
+                const int i1 = v1 ? table_index(t1, r1) : 8 * lane + 2;
+                const int i2 = v2 ? table_index(t2, r2) : 8 * lane + 4;
+                const int i3 = v3 ? table_index(t3, r3) : 8 * lane + 6;
+                const uint32_t o0 = atomicAdd(&k.hist[i0 >> 1], (uint32_t)v0 << ((i0 & 1) << 4));
+                const uint32_t o1 = atomicAdd(&k.hist[i1 >> 1], (uint32_t)v1 << ((i1 & 1) << 4));
+                const uint32_t o2 = atomicAdd(&k.hist[i2 >> 1], (uint32_t)v2 << ((i2 & 1) << 4));
+                const uint32_t o3 = atomicAdd(&k.hist[i3 >> 1], (uint32_t)v3 << ((i3 & 1) << 4));
+                const bool f0 = v0 && lds_needs_fix(i0, o0), f1 = v1 && lds_needs_fix(i1, o1),
+                           f2 = v2 && lds_needs_fix(i2, o2), f3 = v3 && lds_needs_fix(i3, o3);
+                if (f0 || f1 || f2 || f3) {
+                    if (f0) lds_fix(k, i0, o0);
+                    if (f1) lds_fix(k, i1, o1);
+                    if (f2) lds_fix(k, i2, o2);
+                    if (f3) lds_fix(k, i3, o3);
                 }
             } else {
-                const int32_t x[5] = {t0, t1, t2, t3, t4};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if ((x[e] | x[e + 1]) >= 0) count_pair<MODE>(k, x[e], x[e + 1]);
+                if (v0) count_pair<MODE>(k, t0, r0);
+                if (v1) count_pair<MODE>(k, t1, r1);
+                if (v2) count_pair<MODE>(k, t2, r2);
+                if (v3) count_pair<MODE>(k, t3, r3);
             }
-            s.n_live += CHUNK;
-            s.prev = bcast(t3, 63);
+            s.n_live += w.len;
+            s.prev = w.len == CHUNK ? bcast(t3, 63) : view_at(w, kl);
             return;
         }
     }
@@ -468,10 +541,175 @@ __device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Chunk re-packing in registers (no LDS: it is all pair table).  Each kept slot moves left by
+// D = the number of dropped slots before it, one binary digit of D per step, least significant
+// first; that order never lands two slots on one position.  A slot travels as one dword:
+// value+1 (17 bits) | D << 17 (8 bits) | kept << 25.  Returns the new live length.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&keep)[4], int len,
+                                             int lane) {
+    const unsigned long long K0 = __ballot(keep[0]), K1 = __ballot(keep[1]),
+                             K2 = __ballot(keep[2]), K3 = __ballot(keep[3]);
+    const int total = __popcll(K0) + __popcll(K1) + __popcll(K2) + __popcll(K3);
+    int kb = (int)(__builtin_amdgcn_mbcnt_hi((uint32_t)(K0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K0, 0)) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(K1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K1, 0)) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(K2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K2, 0)) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(K3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)K3, 0)));
+    constexpr uint32_t KEPT = 1u << 25;
+    uint32_t pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t d = (uint32_t)(4 * lane + e - kb);
+        pk[e] = keep[e] ? ((uint32_t)(val[e] + 1) | (d << 17) | KEPT) : 0u;
+        kb += keep[e];
+    }
+    const int dmax = len - total;   // dropped live slots; dead slots all follow the live ones
+    for (int sh = 1; sh <= dmax; sh <<= 1) {
+        uint32_t nb[4];   // the slot sh positions to the right
+        if (sh == 1) {
+            nb[0] = pk[1];
+            nb[1] = pk[2];
+            nb[2] = pk[3];
+            nb[3] = (uint32_t)from_next((int32_t)pk[0], 0);
+        } else if (sh == 2) {
+            nb[0] = pk[2];
+            nb[1] = pk[3];
+            nb[2] = (uint32_t)from_next((int32_t)pk[0], 0);
+            nb[3] = (uint32_t)from_next((int32_t)pk[1], 0);
+        } else {
+            const int dl = sh >> 2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t x = __shfl_down(pk[e], dl);
+                nb[e] = lane + dl < 64 ? x : 0u;
+            }
+        }
+        const uint32_t bit = (uint32_t)sh << 17;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool mv = (nb[e] & KEPT) && (nb[e] & bit);
+            const bool stay = (pk[e] & KEPT) && !(pk[e] & bit);
+            pk[e] = mv ? nb[e] : stay ? pk[e] : 0u;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        val[e] = 4 * lane + e < total ? (int32_t)(pk[e] & 0x1FFFFu) - 1 : TOMB;
+    return total;
+}
+
+// Per-region state of the fused pass.
+struct StepState {
+    int32_t pre_prev;          // last pre-merge live token before the current chunk
+    int64_t pre_prev_off;      // its run offset
+    bool pre_prev_match;       // it is an `a` matched with the current chunk's first token
+    bool pre_started;
+    unsigned long long n_match;
+    CountState s;
+    View pend;                 // post-merge chunk waiting for its right neighbour
+    bool have_pend;
+};
+
+// One chunk of the fused pass.  v = chunk c (pre-merge), nxt = lane-0 slot of chunk c+1
+// (pre-merge; NONE past the region).
+template <bool MERGE, int MODE>
+__device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c, int64_t c1,
+                                           int32_t *ids, int32_t ma, int32_t mb, int32_t mc,
+                                           const RegionCarry &rc, int lane, StepState &st,
+                                           const Sink &k) {
+    View w = make_view(v);
+    if (w.len == 0) return;
+    // first live pre-merge token after this chunk inside the region (NONE: none).  The chunks
+    // after c are not rewritten yet, so these loads see pre-merge data.
+    if (nxt == TOMB) {
+        for (int64_t q = c + 2; q < c1 && nxt == TOMB; ++q) nxt = ids[q * CHUNK];
+        if (nxt == TOMB) nxt = NONE;
+    }
+    // the post-merge token after this chunk is known now unless the merge can touch it
+    bool nxt_known = true;
+    if (MERGE) {
+        const int32_t nxt_pre = nxt == NONE ? rc.next_tok : nxt;
+        const int kl = w.len - 1;
+        if (!st.pre_started) {
+            st.pre_started = true;
+            const int32_t t0 = view_at(w, 0);
+            st.pre_prev_match = st.pre_prev == ma && t0 == mb &&
+                                (ma != mb || ((rc.carry_off - 1) & 1) == 0);
+        }
+        bool m[4];
+        int64_t last_off = 0;
+        const int32_t dn = from_next(w.t[0], nxt_pre);
+        if (w.len == CHUNK) {
+            const int32_t t4 = dn;
+            m[0] = w.t[0] == ma && w.t[1] == mb;
+            m[1] = w.t[1] == ma && w.t[2] == mb;
+            m[2] = w.t[2] == ma && w.t[3] == mb;
+            m[3] = w.t[3] == ma && t4 == mb;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = 4 * lane + e;
+                const int32_t partner = (q + 1 < w.len) ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
+                m[e] = q < w.len && w.t[e] == ma && partner == mb;
+            }
+        }
+        bool any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
+        const int32_t t_last = view_at(w, kl);
+        if (ma == mb && (any_m || t_last == ma)) {
+            // X X merge: only even run offsets match (core.ts:285-290 == replaceAll)
+            Nbr n;
+            neighbours(w, st.pre_prev, nxt_pre, lane, n);
+            int64_t off[4];
+            last_off = run_offsets(w, n, lane, st.pre_prev_off, off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m[e] = m[e] && (off[e] & 1) == 0;
+            any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
+        }
+        const bool m_last = ((__ballot(pick4(m, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
+        if (st.pre_prev_match || any_m) {
+            const bool m_up = from_prev((int)m[3], (int)st.pre_prev_match) != 0;
+            bool keep[4];
+            keep[0] = 4 * lane + 0 < w.len && !m_up;
+            keep[1] = 4 * lane + 1 < w.len && !m[0];
+            keep[2] = 4 * lane + 2 < w.len && !m[1];
+            keep[3] = 4 * lane + 3 < w.len && !m[2];
+            int32_t y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
+            const int total = compact_chunk(y, keep, w.len, lane);
+            reinterpret_cast<int4 *>(ids)[c * 64 + lane] = make_int4(y[0], y[1], y[2], y[3]);
+            st.n_match += __popcll(__ballot(m[0])) + __popcll(__ballot(m[1])) +
+                          __popcll(__ballot(m[2])) + __popcll(__ballot(m[3]));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w.t[e] = y[e];
+            w.len = total;
+        }
+        st.pre_prev = t_last;
+        st.pre_prev_off = last_off;
+        st.pre_prev_match = m_last;
+        // the next chunk's first token survives unchanged unless it is a or b
+        nxt_known = nxt == NONE || (nxt != ma && nxt != mb);
+        if (w.len == 0) return;
+    }
+    if (st.have_pend) {
+        count_view<MODE>(st.pend, view_at(w, 0), false, lane, st.s, k);
+        st.have_pend = false;
+    }
+    if (nxt_known) {
+        count_view<MODE>(w, nxt, nxt == NONE, lane, st.s, k);
+    } else {
+        st.pend = w;
+        st.have_pend = true;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // K1 (fused with K4): one streaming pass over the corpus.  With MERGE, first applies the pending
 // merge (a, b) -> c to every chunk (matches found on the pre-merge stream with the exact X X
 // parity; touched chunks are re-packed and written back), then counts every pair of the
-// post-merge stream (hot pairs in LDS, cold pairs in the sparse table).
+// post-merge stream (hot pairs and sketch buckets in LDS; MODE_EXACT: heavy cold pairs in the
+// sparse table).  One wave streams one region through a 4-deep register ring (the loop is
+// unrolled by the ring depth so no register rotation waits on an in-flight load).
 // ---------------------------------------------------------------------------------------------
 template <bool MERGE, int MODE>
 __global__ void __launch_bounds__(WG)
@@ -480,8 +718,8 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
        uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
        const uint32_t *__restrict__ heavy_g, RegionSum *__restrict__ sums,
        unsigned long long *__restrict__ replaced) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t *hist = lds;
+    // static, so LDS addresses are plain constants (no symbol base to add per access)
+    __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
     if (MODE == MODE_TABLE) {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
@@ -495,168 +733,77 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     k.ct = ct;
     k.heavy = hist;
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
+    const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6)));
     if (r < R) {
         const int64_t c0 = (int64_t)r * cpr;
         const int64_t c1 = min(c0 + cpr, n_chunks);
-        int4 *v4 = reinterpret_cast<int4 *>(ids);
-        // pre-merge (apply) state
         const RegionCarry rc = carry[r];
-        int32_t pre_prev = rc.prev_tok;
-        int64_t pre_prev_off = rc.carry_off - 1;
-        bool pre_prev_match = false;
-        bool pre_started = false;
-        unsigned long long n_match = 0;
-        // count state
-        CountState s;
-        s.prev = NONE;
-        s.run_x = -2;
-        s.run_len = 0;
-        s.run_lead = false;
-        s.started = false;
-        s.lead_len = 0;
-        s.n_live = 0;
-        s.first_tok = NONE;
-        View pend;               // post-merge chunk waiting for its right neighbour
-        bool have_pend = false;
-        // register ring: chunk c (r0), c+1 (r1: its first slot is the "next token"), and
-        // c+2..c+4 in flight — 4 KiB per wave, 64 KiB per CU of HBM reads outstanding
-        const int4 tomb4 = make_int4(TOMB, TOMB, TOMB, TOMB);
-        int4 r0 = v4[c0 * 64 + lane];
-        int4 r1 = c0 + 1 < c1 ? v4[(c0 + 1) * 64 + lane] : tomb4;
-        int4 r2 = c0 + 2 < c1 ? v4[(c0 + 2) * 64 + lane] : tomb4;
-        int4 r3 = c0 + 3 < c1 ? v4[(c0 + 3) * 64 + lane] : tomb4;
-        int4 r4 = c0 + 4 < c1 ? v4[(c0 + 4) * 64 + lane] : tomb4;
-        for (int64_t c = c0; c < c1; ++c) {
-            const int4 v = r0;
-            r0 = r1;
-            r1 = r2;
-            r2 = r3;
-            r3 = r4;
-            if (c + 5 < c1) r4 = v4[(c + 5) * 64 + lane];
-            View w = make_view(v);
-            if (w.len == 0) continue;
-            // first live pre-merge token after this chunk inside the region (NONE: none).  The
-            // chunks of this region are not rewritten yet, so these loads see pre-merge data.
-            int32_t nxt = NONE;
-            if (c + 1 < c1) {
-                nxt = bcast(r0.x, 0);
-                for (int64_t q = c + 2; q < c1 && nxt == TOMB; ++q) nxt = ids[q * CHUNK];
-                if (nxt == TOMB) nxt = NONE;
+        StepState st;
+        st.pre_prev = rc.prev_tok;
+        st.pre_prev_off = rc.carry_off - 1;
+        st.pre_prev_match = false;
+        st.pre_started = false;
+        st.n_match = 0;
+        st.s.prev = NONE;
+        st.s.run_x = -2;
+        st.s.run_len = 0;
+        st.s.run_lead = false;
+        st.s.started = false;
+        st.s.lead_len = 0;
+        st.s.n_live = 0;
+        st.s.first_tok = NONE;
+        st.have_pend = false;
+        if (c0 < c1) {
+            // the region through a range-checked buffer descriptor: loads past its end return 0
+            // and are never consumed
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                ids + c0 * CHUNK, 0, (int)((c1 - c0) * CHUNK * 4), 0x00020000);
+            const int lo = lane * 16;
+            auto load = [&](int64_t c) -> int4 {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + (int)(c - c0) * 1024, 0, 0);
+                return make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
+            };
+            int4 q0 = load(c0), q1 = load(c0 + 1), q2 = load(c0 + 2), q3 = load(c0 + 3);
+#define BPE_STAGE(QC, QN, CC)                                                                   \
+    {                                                                                           \
+        const int4 v_ = QC;                                                                     \
+        QC = load((CC) + 4);                                                                    \
+        const int32_t nx_ = (CC) + 1 < c1 ? bcast(QN.x, 0) : NONE;                              \
+        step_chunk<MERGE, MODE>(v_, nx_, (CC), c1, ids, ma, mb, mc, rc, lane, st, k);           \
+    }
+            for (int64_t c = c0; c < c1; c += 4) {
+                BPE_STAGE(q0, q1, c)
+                if (c + 1 >= c1) break;
+                BPE_STAGE(q1, q2, c + 1)
+                if (c + 2 >= c1) break;
+                BPE_STAGE(q2, q3, c + 2)
+                if (c + 3 >= c1) break;
+                BPE_STAGE(q3, q0, c + 3)
             }
-            // the post-merge token after this chunk is known now unless the merge can touch it
-            bool nxt_known = true;
-            if (MERGE) {
-                const int32_t nxt_pre = nxt == NONE ? rc.next_tok : nxt;
-                const int kl = w.len - 1;
-                if (!pre_started) {
-                    pre_started = true;
-                    const int32_t t0 = view_at(w, 0);
-                    pre_prev_match = pre_prev == ma && t0 == mb &&
-                                     (ma != mb || ((rc.carry_off - 1) & 1) == 0);
-                }
-                bool m[4];
-                int64_t last_off = 0;
-                const int32_t dn = __shfl_down(w.t[0], 1);
-                if (w.len == CHUNK) {
-                    const int32_t t4 = lane == 63 ? nxt_pre : dn;
-                    m[0] = w.t[0] == ma && w.t[1] == mb;
-                    m[1] = w.t[1] == ma && w.t[2] == mb;
-                    m[2] = w.t[2] == ma && w.t[3] == mb;
-                    m[3] = w.t[3] == ma && t4 == mb;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int k = 4 * lane + e;
-                        const int32_t partner = (k + 1 < w.len) ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
-                        m[e] = k < w.len && w.t[e] == ma && partner == mb;
-                    }
-                }
-                bool any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
-                const int32_t t_last = view_at(w, kl);
-                if (ma == mb && (any_m || t_last == ma)) {
-                    // X X merge: only even run offsets match (core.ts:285-290 == replaceAll)
-                    Nbr n;
-                    neighbours(w, pre_prev, nxt_pre, lane, n);
-                    int64_t off[4];
-                    last_off = run_offsets(w, n, lane, pre_prev_off, off);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) m[e] = m[e] && (off[e] & 1) == 0;
-                    any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
-                }
-                const bool m_last = ((__ballot(pick4(m, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
-                if (pre_prev_match || any_m) {
-                    const bool m_up = __shfl_up((int)m[3], 1) != 0;
-                    bool keep[4];
-                    keep[0] = 4 * lane + 0 < w.len && !(lane == 0 ? pre_prev_match : m_up);
-                    keep[1] = 4 * lane + 1 < w.len && !m[0];
-                    keep[2] = 4 * lane + 2 < w.len && !m[1];
-                    keep[3] = 4 * lane + 3 < w.len && !m[2];
-                    const int nk = (int)keep[0] + keep[1] + keep[2] + keep[3];
-                    const int incl = wave_incl_sum(nk, lane);
-                    const int total = bcast(incl, 63);
-                    // re-pack through the chunk itself (the LDS is all pair table): kept values
-                    // go to their packed slots, vacated slots become TOMB, then the wave reads the
-                    // chunk back.  Same-CU global stores are visible to the CU's later loads once
-                    // the workgroup-scope release (s_waitcnt vmcnt(0)) has completed them.
-                    int32_t *cp = ids + c * CHUNK;
-                    int pp = incl - nk;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int k = 4 * lane + e;
-                        if (keep[e]) cp[pp++] = m[e] ? mc : w.t[e];
-                        if (k >= total && k < w.len) cp[k] = TOMB;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    const int4 yv = v4[c * 64 + lane];
-                    const int32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
-                    n_match += __popcll(__ballot(m[0])) + __popcll(__ballot(m[1])) +
-                               __popcll(__ballot(m[2])) + __popcll(__ballot(m[3]));
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) w.t[e] = y[e];
-                    w.len = total;
-                }
-                pre_prev = t_last;
-                pre_prev_off = last_off;
-                pre_prev_match = m_last;
-                // the next chunk's first token survives unchanged unless it is a or b
-                nxt_known = nxt == NONE || (nxt != ma && nxt != mb);
-                if (w.len == 0) continue;
-            }
-            if (have_pend) {
-                count_view<MODE>(pend, view_at(w, 0), false, lane, s, k);
-                have_pend = false;
-            }
-            if (nxt_known) {
-                count_view<MODE>(w, nxt, nxt == NONE, lane, s, k);
-            } else {
-                pend = w;
-                have_pend = true;
-            }
+#undef BPE_STAGE
         }
-        if (have_pend) count_view<MODE>(pend, NONE, true, lane, s, k);
+        CountState &s = st.s;
+        if (st.have_pend) count_view<MODE>(st.pend, NONE, true, lane, s, k);
         if (lane == 0) {
-            RegionSum rs;
-            rs.n_live = s.n_live;
-            rs.first_tok = s.n_live ? s.first_tok : NONE;
-            rs.last_tok = s.n_live ? s.prev : NONE;
-            rs.pad = 0;
+            RegionSum rsum;
+            rsum.n_live = s.n_live;
+            rsum.first_tok = s.n_live ? s.first_tok : NONE;
+            rsum.last_tok = s.n_live ? s.prev : NONE;
+            rsum.pad = 0;
             if (s.n_live == 0) {
-                rs.lead_len = rs.trail_len = 0;
-                rs.uniform = 0;
+                rsum.lead_len = rsum.trail_len = 0;
+                rsum.uniform = 0;
             } else if (s.run_x != -2) {
-                rs.uniform = s.run_lead ? 1 : 0;
-                rs.trail_len = s.run_len;
-                rs.lead_len = s.run_lead ? s.run_len : s.lead_len;
+                rsum.uniform = s.run_lead ? 1 : 0;
+                rsum.trail_len = s.run_len;
+                rsum.lead_len = s.run_lead ? s.run_len : s.lead_len;
             } else {
-                rs.uniform = 0;
-                rs.trail_len = 0;
-                rs.lead_len = s.lead_len;
+                rsum.uniform = 0;
+                rsum.trail_len = 0;
+                rsum.lead_len = s.lead_len;
             }
-            sums[r] = rs;
-            if (MERGE && n_match) atomicAdd(replaced, n_match);
+            sums[r] = rsum;
+            if (MERGE && st.n_match) atomicAdd(replaced, st.n_match);
         }
     }
     if (MODE == MODE_TABLE) {

@@ -26,7 +26,8 @@ def index(a, b):
     """Table index of libbpe's pair table (include/bpe.h): hot bin, or cold sketch bucket."""
     if a < 256 and b < 256:
         return (a << 8) | b
-    return 65536 + ((((a << 16) | b) * 0x9E3779B1) & 0xFFFFFFFF) >> 18
+    h = ((a & 0xFFFFFF) * 0x9E3779 & 0xFFFFFFFF) + ((b & 0xFFFFFF) * 0x85EBCB & 0xFFFFFFFF)
+    return 65536 + ((h & 0xFFFFFFFF) >> 18)
 
 
 class OracleShard:
