@@ -245,12 +245,16 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
-    if (merge)
-        k_step<true, MODE_TABLE><<<c->G, WG, 0, s>>>(
+    if (merge && a == b)
+        k_step<MERGE_XX, MODE_TABLE><<<c->G, WG, 0, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
+            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+    else if (merge)
+        k_step<MERGE_XY, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     else
-        k_step<false, MODE_TABLE><<<c->G, WG, 0, s>>>(
+        k_step<NO_MERGE, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     HIP_TRY(hipGetLastError());
@@ -358,7 +362,7 @@ int exact_pass(bpe_ctx *c) {
     hipStream_t s = c->stream;
     k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
     HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
-    k_step<false, MODE_EXACT><<<c->G, WG, 0, s>>>(
+    k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
         c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
         c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,

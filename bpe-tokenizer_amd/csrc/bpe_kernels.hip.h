@@ -27,8 +27,11 @@ constexpr int32_t SEP = -1;                 // sample separator (live slot, neve
 constexpr int32_t TOMB = -2;                // dead slot in a chunk tail
 constexpr int32_t NONE = -3;                // "no token" (register sentinel only)
 constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x int4)
-constexpr int WAVES_PER_WG = 16;
-constexpr int WG = WAVES_PER_WG * 64;       // 1024 threads, one workgroup per CU (LDS-bound)
+#ifndef BPE_WAVES
+#define BPE_WAVES 16
+#endif
+constexpr int WAVES_PER_WG = BPE_WAVES;
+constexpr int WG = WAVES_PER_WG * 64;       // one workgroup per CU (LDS-bound)
 constexpr int MAX_WG = 256;                 // one per CU on MI355X
 constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
 constexpr int HOT = 256;                    // ids < HOT form the dense LDS histogram
@@ -612,7 +615,11 @@ struct StepState {
 
 // One chunk of the fused pass.  v = chunk c (pre-merge), nxt = lane-0 slot of chunk c+1
 // (pre-merge; NONE past the region).
-template <bool MERGE, int MODE>
+// What a k_step pass does before counting: nothing, a merge of two distinct ids, or an X X merge
+// (the only kind whose matches depend on run parity, so the only one carrying that code).
+enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
+
+template <int MERGE, int MODE>
 __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c, int64_t c1,
                                            int32_t *ids, int32_t ma, int32_t mb, int32_t mc,
                                            const RegionCarry &rc, int lane, StepState &st,
@@ -634,28 +641,30 @@ __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c,
             st.pre_started = true;
             const int32_t t0 = view_at(w, 0);
             st.pre_prev_match = st.pre_prev == ma && t0 == mb &&
-                                (ma != mb || ((rc.carry_off - 1) & 1) == 0);
+                                (MERGE == MERGE_XY || ((rc.carry_off - 1) & 1) == 0);
         }
         bool m[4];
         int64_t last_off = 0;
         const int32_t dn = from_next(w.t[0], nxt_pre);
+        int32_t t_last;
         if (w.len == CHUNK) {
-            const int32_t t4 = dn;
-            m[0] = w.t[0] == ma && w.t[1] == mb;
-            m[1] = w.t[1] == ma && w.t[2] == mb;
-            m[2] = w.t[2] == ma && w.t[3] == mb;
-            m[3] = w.t[3] == ma && t4 == mb;
+            m[0] = (w.t[0] == ma) & (w.t[1] == mb);
+            m[1] = (w.t[1] == ma) & (w.t[2] == mb);
+            m[2] = (w.t[2] == ma) & (w.t[3] == mb);
+            m[3] = (w.t[3] == ma) & (dn == mb);
+            t_last = bcast(w.t[3], 63);
         } else {
+            const int l4 = 4 * lane;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int q = 4 * lane + e;
-                const int32_t partner = (q + 1 < w.len) ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
-                m[e] = q < w.len && w.t[e] == ma && partner == mb;
+                const int32_t partner = l4 < kl - e ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
+                m[e] = (l4 < w.len - e) & (w.t[e] == ma) & (partner == mb);
             }
+            t_last = view_at(w, kl);
         }
-        bool any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
-        const int32_t t_last = view_at(w, kl);
-        if (ma == mb && (any_m || t_last == ma)) {
+        unsigned long long M0 = __ballot(m[0]), M1 = __ballot(m[1]), M2 = __ballot(m[2]),
+                           M3 = __ballot(m[3]);
+        if (MERGE == MERGE_XX && ((M0 | M1 | M2 | M3) != 0ull || t_last == ma)) {
             // X X merge: only even run offsets match (core.ts:285-290 == replaceAll)
             Nbr n;
             neighbours(w, st.pre_prev, nxt_pre, lane, n);
@@ -663,23 +672,28 @@ __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c,
             last_off = run_offsets(w, n, lane, st.pre_prev_off, off);
 #pragma unroll
             for (int e = 0; e < 4; ++e) m[e] = m[e] && (off[e] & 1) == 0;
-            any_m = __ballot(m[0] || m[1] || m[2] || m[3]) != 0ull;
+            M0 = __ballot(m[0]);
+            M1 = __ballot(m[1]);
+            M2 = __ballot(m[2]);
+            M3 = __ballot(m[3]);
         }
-        const bool m_last = ((__ballot(pick4(m, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
-        if (st.pre_prev_match || any_m) {
+        const int el = kl & 3;
+        const unsigned long long ML = el == 0 ? M0 : el == 1 ? M1 : el == 2 ? M2 : M3;
+        const bool m_last = ((ML >> (kl >> 2)) & 1ull) != 0;
+        if (st.pre_prev_match || (M0 | M1 | M2 | M3) != 0ull) {
             const bool m_up = from_prev((int)m[3], (int)st.pre_prev_match) != 0;
+            const int l4 = 4 * lane;
             bool keep[4];
-            keep[0] = 4 * lane + 0 < w.len && !m_up;
-            keep[1] = 4 * lane + 1 < w.len && !m[0];
-            keep[2] = 4 * lane + 2 < w.len && !m[1];
-            keep[3] = 4 * lane + 3 < w.len && !m[2];
+            keep[0] = (l4 < w.len) & !m_up;
+            keep[1] = (l4 < w.len - 1) & !m[0];
+            keep[2] = (l4 < w.len - 2) & !m[1];
+            keep[3] = (l4 < w.len - 3) & !m[2];
             int32_t y[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
             const int total = compact_chunk(y, keep, w.len, lane);
             reinterpret_cast<int4 *>(ids)[c * 64 + lane] = make_int4(y[0], y[1], y[2], y[3]);
-            st.n_match += __popcll(__ballot(m[0])) + __popcll(__ballot(m[1])) +
-                          __popcll(__ballot(m[2])) + __popcll(__ballot(m[3]));
+            st.n_match += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
 #pragma unroll
             for (int e = 0; e < 4; ++e) w.t[e] = y[e];
             w.len = total;
@@ -691,8 +705,10 @@ __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c,
         nxt_known = nxt == NONE || (nxt != ma && nxt != mb);
         if (w.len == 0) return;
     }
+    // A parked chunk (its right neighbour was unknown) is counted now, through the general path
+    // (rare: it keeps the inlined fast path single); then w is counted or parked in turn.
     if (st.have_pend) {
-        count_view<MODE>(st.pend, view_at(w, 0), false, lane, st.s, k);
+        st.s = count_view_general<MODE>(st.pend, view_at(w, 0), false, lane, st.s, k);
         st.have_pend = false;
     }
     if (nxt_known) {
@@ -711,7 +727,7 @@ __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c,
 // sparse table).  One wave streams one region through a 4-deep register ring (the loop is
 // unrolled by the ring depth so no register rotation waits on an in-flight load).
 // ---------------------------------------------------------------------------------------------
-template <bool MERGE, int MODE>
+template <int MERGE, int MODE>
 __global__ void __launch_bounds__(WG)
 k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
        const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
