@@ -206,7 +206,11 @@ __device__ __forceinline__ bool lds_needs_fix(int idx, uint32_t old) {
 __device__ __forceinline__ void lds_fix(const Sink &k, int idx, uint32_t old) {
     if (!lds_needs_fix(idx, old)) return;
     atomicSub(&k.hist[idx >> 1], 0x8000u << ((idx & 1) << 4));
-    atomicAdd(&k.spill[idx], 0x8000ull);
+    // (the constant is made opaque so it is materialised here, not held in registers across the
+    // streaming loop for this rare path)
+    uint32_t inc = 0x8000u;
+    asm volatile("" : "+v"(inc));
+    atomicAdd(&k.spill[idx], (unsigned long long)inc);
 }
 
 // One counted occurrence of (x, y).
@@ -438,10 +442,10 @@ __device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last
             if (MODE == MODE_TABLE) {
                 // four LDS atomics in flight, one overflow test; an invalid pair (SEP, dead
                 // slot) adds 0 to a lane-private word instead of branching
-                const int i0 = v0 ? table_index(t0, r0) : 8 * lane + 0;
-                const int i1 = v1 ? table_index(t1, r1) : 8 * lane + 2;
-                const int i2 = v2 ? table_index(t2, r2) : 8 * lane + 4;
-                const int i3 = v3 ? table_index(t3, r3) : 8 * lane + 6;
+                const int i0 = v0 ? table_index(t0, r0) : 2 * lane;   // dummy: a lane-private word, adds 0
+                const int i1 = v1 ? table_index(t1, r1) : 2 * lane;   // dummy: a lane-private word, adds 0
+                const int i2 = v2 ? table_index(t2, r2) : 2 * lane;   // dummy: a lane-private word, adds 0
+                const int i3 = v3 ? table_index(t3, r3) : 2 * lane;   // dummy: a lane-private word, adds 0
                 const uint32_t o0 = atomicAdd(&k.hist[i0 >> 1], (uint32_t)v0 << ((i0 & 1) << 4));
                 const uint32_t o1 = atomicAdd(&k.hist[i1 >> 1], (uint32_t)v1 << ((i1 & 1) << 4));
                 const uint32_t o2 = atomicAdd(&k.hist[i2 >> 1], (uint32_t)v2 << ((i2 & 1) << 4));
@@ -584,7 +588,7 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t x = __shfl_down(pk[e], dl);
-                nb[e] = lane + dl < 64 ? x : 0u;
+                nb[e] = lane < 64 - dl ? x : 0u;
             }
         }
         const uint32_t bit = (uint32_t)sh << 17;
@@ -597,7 +601,7 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        val[e] = 4 * lane + e < total ? (int32_t)(pk[e] & 0x1FFFFu) - 1 : TOMB;
+        val[e] = 4 * lane < total - e ? (int32_t)(pk[e] & 0x1FFFFu) - 1 : TOMB;
     return total;
 }
 
@@ -613,23 +617,26 @@ struct StepState {
     bool have_pend;
 };
 
-// One chunk of the fused pass.  v = chunk c (pre-merge), nxt = lane-0 slot of chunk c+1
-// (pre-merge; NONE past the region).
 // What a k_step pass does before counting: nothing, a merge of two distinct ids, or an X X merge
 // (the only kind whose matches depend on run parity, so the only one carrying that code).
 enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
 
+// One chunk of the fused pass.  v = chunk c of the region (pre-merge; c counts from the
+// region's first chunk, nc chunks in all, rs = the region's buffer descriptor), nxt = lane-0 slot
+// of chunk c+1 (pre-merge; NONE past the region).
 template <int MERGE, int MODE>
-__device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c, int64_t c1,
-                                           int32_t *ids, int32_t ma, int32_t mb, int32_t mc,
-                                           const RegionCarry &rc, int lane, StepState &st,
-                                           const Sink &k) {
+__device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int c, int nc,
+                                           const __amdgpu_buffer_rsrc_t rs, int32_t ma, int32_t mb,
+                                           int32_t mc, const RegionCarry &rc, int lane,
+                                           StepState &st, const Sink &k) {
     View w = make_view(v);
     if (w.len == 0) return;
     // first live pre-merge token after this chunk inside the region (NONE: none).  The chunks
     // after c are not rewritten yet, so these loads see pre-merge data.
     if (nxt == TOMB) {
-        for (int64_t q = c + 2; q < c1 && nxt == TOMB; ++q) nxt = ids[q * CHUNK];
+        for (int q = c + 2; q < nc && nxt == TOMB; ++q)
+            nxt = __builtin_amdgcn_readfirstlane(
+                (int)__builtin_amdgcn_raw_buffer_load_b32(rs, q * (CHUNK * 4), 0, 0));
         if (nxt == TOMB) nxt = NONE;
     }
     // the post-merge token after this chunk is known now unless the merge can touch it
@@ -692,7 +699,10 @@ __device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int64_t c,
 #pragma unroll
             for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
             const int total = compact_chunk(y, keep, w.len, lane);
-            reinterpret_cast<int4 *>(ids)[c * 64 + lane] = make_int4(y[0], y[1], y[2], y[3]);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
+                                   make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
+                rs, lane * 16 + c * (CHUNK * 4), 0, 0);
             st.n_match += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
 #pragma unroll
             for (int e = 0; e < 4; ++e) w.t[e] = y[e];
@@ -775,25 +785,26 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 ids + c0 * CHUNK, 0, (int)((c1 - c0) * CHUNK * 4), 0x00020000);
             const int lo = lane * 16;
-            auto load = [&](int64_t c) -> int4 {
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + (int)(c - c0) * 1024, 0, 0);
+            const int nc = (int)(c1 - c0);
+            auto load = [&](int c) -> int4 {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + c * (CHUNK * 4), 0, 0);
                 return make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
             };
-            int4 q0 = load(c0), q1 = load(c0 + 1), q2 = load(c0 + 2), q3 = load(c0 + 3);
+            int4 q0 = load(0), q1 = load(1), q2 = load(2), q3 = load(3);
 #define BPE_STAGE(QC, QN, CC)                                                                   \
     {                                                                                           \
         const int4 v_ = QC;                                                                     \
         QC = load((CC) + 4);                                                                    \
-        const int32_t nx_ = (CC) + 1 < c1 ? bcast(QN.x, 0) : NONE;                              \
-        step_chunk<MERGE, MODE>(v_, nx_, (CC), c1, ids, ma, mb, mc, rc, lane, st, k);           \
+        const int32_t nx_ = (CC) + 1 < nc ? bcast(QN.x, 0) : NONE;                              \
+        step_chunk<MERGE, MODE>(v_, nx_, (CC), nc, rs, ma, mb, mc, rc, lane, st, k);            \
     }
-            for (int64_t c = c0; c < c1; c += 4) {
+            for (int c = 0; c < nc; c += 4) {
                 BPE_STAGE(q0, q1, c)
-                if (c + 1 >= c1) break;
+                if (c + 1 >= nc) break;
                 BPE_STAGE(q1, q2, c + 1)
-                if (c + 2 >= c1) break;
+                if (c + 2 >= nc) break;
                 BPE_STAGE(q2, q3, c + 2)
-                if (c + 3 >= c1) break;
+                if (c + 3 >= nc) break;
                 BPE_STAGE(q3, q0, c + 3)
             }
 #undef BPE_STAGE
