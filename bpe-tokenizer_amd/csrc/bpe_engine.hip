@@ -96,10 +96,19 @@ struct bpe_ctx {
     int64_t cpr = 0;
     int R = 0, G = 0;
     int64_t last_replaced = 0;
-    // stats
+    // best hot key of d_hot computed by the last k_reduce_table (valid for best_ml)
+    bool best_ready = false;
+    int64_t best_ml = 0;
+    int64_t opt_max_length = 0;   // max_length of the last find (the reduce's filter)
+    // stats: kernel spans are timed with events read back lazily (no sync in the merge loop)
     bool stats_on = false;
     bpe_stats stats{};
-    hipEvent_t ev[6] = {};
+    struct Span {
+        hipEvent_t a, b;
+        int kind;   // 0 stream pass, 1 selection, 2 tie pass
+    };
+    std::vector<Span> spans;
+    std::vector<hipEvent_t> ev_pool;
 };
 
 namespace {
@@ -223,6 +232,50 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+hipEvent_t take_event(bpe_ctx *c) {
+    hipEvent_t e = nullptr;
+    if (!c->ev_pool.empty()) {
+        e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+    }
+    return e;
+}
+
+// Starts a timed span on the stream (nullptr when stats are off).
+hipEvent_t span_begin(bpe_ctx *c) {
+    if (!c->stats_on) return nullptr;
+    hipEvent_t e = take_event(c);
+    if (e) (void)hipEventRecord(e, c->stream);
+    return e;
+}
+
+// Reads every finished span into the stats and recycles the events.
+int flush_spans(bpe_ctx *c) {
+    if (c->spans.empty()) return BPE_OK;
+    HIP_TRY(hipEventSynchronize(c->spans.back().b));
+    for (auto &sp : c->spans) {
+        const double ms = ev_ms(sp.a, sp.b);
+        if (sp.kind == 0) c->stats.step_ms += ms;
+        else c->stats.select_ms += ms;
+        c->ev_pool.push_back(sp.a);
+        c->ev_pool.push_back(sp.b);
+    }
+    c->spans.clear();
+    return BPE_OK;
+}
+
+int span_end(bpe_ctx *c, hipEvent_t a, int kind) {
+    if (!a) return BPE_OK;
+    hipEvent_t b = take_event(c);
+    if (!b) return fail(BPE_ERR_HIP, "bpe native: event");
+    HIP_TRY(hipEventRecord(b, c->stream));
+    c->spans.push_back({a, b, kind});
+    if (c->spans.size() >= 1024) return flush_spans(c);
+    return BPE_OK;
+}
+
 // One streaming pass: (optionally apply the merge a,b -> cc, then) count every pair, stitch the
 // region boundaries and reduce the hot table.  Leaves counts + carries valid for the new corpus.
 // With a merge, *replaced receives the number of replacements.
@@ -241,10 +294,11 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         if ((rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS))) return rc;
         c->partials_wg = c->G;
     }
+    if (c->opt_max_length && (rc = sync_len16(c))) return rc;   // the reduce's max_length filter
     hipStream_t s = c->stream;
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[0], s));
+    hipEvent_t e_step = span_begin(c);
     if (merge && a == b)
         k_step<MERGE_XX, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
@@ -258,16 +312,17 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     HIP_TRY(hipGetLastError());
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[1], s));
+    if ((rc = span_end(c, e_step, 0))) return rc;
+    hipEvent_t e_red = span_begin(c);
     k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
                                                           c->cold, c->d_heavy);
-    k_reduce_table<<<HIST_WORDS / 256, 256, 0, s>>>(c->d_partials, c->G, c->d_spill, c->d_hot);
+    k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res);
     HIP_TRY(hipGetLastError());
+    if ((rc = span_end(c, e_red, 1))) return rc;
+    c->best_ready = true;
+    c->best_ml = c->opt_max_length;
     if (c->stats_on) {
-        HIP_TRY(hipEventRecord(c->ev[2], s));
-        HIP_TRY(hipEventSynchronize(c->ev[2]));
-        c->stats.step_ms += ev_ms(c->ev[0], c->ev[1]);
-        c->stats.select_ms += ev_ms(c->ev[1], c->ev[2]);
         c->stats.step_launches += 1;
         c->stats.step_slots += c->n_chunks * CHUNK;
         c->stats.step_live += c->n_live;
@@ -380,14 +435,24 @@ int exact_pass(bpe_ctx *c) {
 // then, when some bucket is heavy, the exact pass; then every pair sharing the best key.
 // Leaves the Result in h_res and the candidates in `cand`.
 int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_length,
-                      bool local, std::vector<int2> &cand) {
+                      bool local, std::vector<int2> &cand, hipEvent_t e_sel) {
     int rc;
     if ((rc = sync_len16(c))) return rc;
     hipStream_t s = c->stream;
-    k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand, c->d_heavy);
+    if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
+        // the reduce already left the best hot key in the Result: collect its pairs and the
+        // heavy sketch buckets with the whole chip
+        HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, 2 * sizeof(unsigned), s));
+        k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(table, c->d_len16, max_length, c->d_res,
+                                                        c->d_cand, c->d_heavy);
+    } else {
+        k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand, c->d_heavy);
+    }
+    c->best_ready = false;
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
+    if ((rc = span_end(c, e_sel, 1))) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     if ((rc = settle_with(c, c->h_res->replaced))) return rc;   // a pending apply's R came along
     if (c->h_res->n_heavy && local) {
@@ -433,16 +498,14 @@ int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long l
             A.cb[j] = cand[j0 + j].y;
         }
         HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
-        if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[3], s));
+        c->best_ready = false;   // the Result is reused
+        hipEvent_t e_tie = span_begin(c);
         if (c->n_live > 0) k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-        if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[4], s));
+        if ((rc = span_end(c, e_tie, 2))) return rc;
         HIP_TRY(hipStreamSynchronize(s));
-        if (c->stats_on) {
-            c->stats.select_ms += ev_ms(c->ev[3], c->ev[4]);
-            c->stats.tie_passes += 1;
-        }
+        if (c->stats_on) c->stats.tie_passes += 1;
         for (unsigned j = 0; j < nb; ++j) last[j0 + j] = c->h_res->last[j];
     }
     return BPE_OK;
@@ -456,16 +519,11 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     if (c->n_live < 2) return BPE_NO_MERGE;
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    hipStream_t s = c->stream;
-    if (c->stats_on) HIP_TRY(hipEventRecord(c->ev[5], s));
+    c->opt_max_length = max_length;
+    hipEvent_t e_sel = span_begin(c);
     std::vector<int2> cand;
-    if ((rc = select_from_table(c, c->d_hot, max_length, true, cand))) return rc;
+    if ((rc = select_from_table(c, c->d_hot, max_length, true, cand, e_sel))) return rc;
     if (c->stats_on) {
-        float ms = 0.f;
-        HIP_TRY(hipEventRecord(c->ev[2], s));
-        HIP_TRY(hipEventSynchronize(c->ev[2]));
-        ms = ev_ms(c->ev[5], c->ev[2]);
-        c->stats.select_ms += ms;
         c->stats.iterations += 1;
         c->stats.live_tokens += c->n_live;
     }
@@ -565,8 +623,6 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = set_device(c))) return bail(rc);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipStreamCreate failed"));
-    for (auto &e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) return bail(fail(BPE_ERR_HIP, "bpe native: event"));
     if ((rc = dev_alloc(&c->d_spill, TABLE_BINS))) return bail(rc);
     if (hipMemset(c->d_spill, 0, TABLE_BINS * sizeof(unsigned long long)) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipMemset failed"));
@@ -603,8 +659,9 @@ int bpe_destroy(bpe_ctx *c) {
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
-    for (auto &e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &sp : c->spans) c->ev_pool.insert(c->ev_pool.end(), {sp.a, sp.b});
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return BPE_OK;
@@ -946,12 +1003,16 @@ int bpe_stats_enable(bpe_ctx *c, int on) {
 
 int bpe_get_stats(bpe_ctx *c, bpe_stats *out) {
     if (!c || !out) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = flush_spans(c);
+    if (rc) return rc;
     *out = c->stats;
     return BPE_OK;
 }
 
 int bpe_reset_stats(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = flush_spans(c);
+    if (rc) return rc;
     memset(&c->stats, 0, sizeof c->stats);
     return BPE_OK;
 }

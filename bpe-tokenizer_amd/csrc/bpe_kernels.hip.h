@@ -926,23 +926,55 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     }
 }
 
-// Sums the per-workgroup 16-bit LDS partials and the spill table into the u64 table
-// (hot bins [0, 64K), sketch buckets [64K, TABLE_BINS)), and zeroes the spill for the next pass.
-__global__ void k_reduce_table(const uint32_t *__restrict__ partials, int G,
-                               unsigned long long *__restrict__ spill,
-                               unsigned long long *__restrict__ table) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= HIST_WORDS) return;
-    unsigned long long lo = 0, hi = 0;   // G <= 256 slabs of < 2^15 each
-    for (int g = 0; g < G; ++g) {
-        const uint32_t p = partials[(size_t)g * HIST_WORDS + w];
-        lo += p & 0xFFFFu;
-        hi += p >> 16;
+// Sums the per-workgroup 16-bit LDS partials and the spill table into the u64 table (hot bins
+// [0, 64K), sketch buckets [64K, TABLE_BINS)), zeroes the spill for the next pass, and leaves the
+// best hot key (max_length filter applied) in res->best.  A block owns 128 words (256 bins):
+// 32 lanes x 4 words, each of its 8 lane groups sums every 8th slab, so each thread keeps 32
+// independent uint4 loads in flight instead of walking all G slabs.
+constexpr int REDUCE_WORDS_PER_BLOCK = 128;
+static_assert(HIST_WORDS % REDUCE_WORDS_PER_BLOCK == 0, "reduce tiling");
+
+__device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len16,
+                                        int64_t max_length);
+
+__global__ void __launch_bounds__(256)
+k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ spill,
+               unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
+               int64_t max_length, Result *res) {
+    __shared__ uint32_t s_sum[8][32][8];
+    const int t = threadIdx.x;
+    const int wl = t & 31, grp = t >> 5;
+    const int w0 = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * wl;   // first of my 4 words
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                 // < 2^23 each: G <= 256 x 2^15
+    const uint4 *p4 = reinterpret_cast<const uint4 *>(partials + w0);
+    for (int g = grp; g < G; g += 8) {
+        const uint4 p = p4[(size_t)g * (HIST_WORDS / 4)];
+        acc[0] += p.x & 0xFFFFu;
+        acc[1] += p.x >> 16;
+        acc[2] += p.y & 0xFFFFu;
+        acc[3] += p.y >> 16;
+        acc[4] += p.z & 0xFFFFu;
+        acc[5] += p.z >> 16;
+        acc[6] += p.w & 0xFFFFu;
+        acc[7] += p.w >> 16;
     }
-    table[2 * w] = lo + spill[2 * w];
-    table[2 * w + 1] = hi + spill[2 * w + 1];
-    spill[2 * w] = 0;
-    spill[2 * w + 1] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_sum[grp][wl][i] = acc[i];
+    __syncthreads();
+    // thread t finalises bin 2*w0' + i for one (word-lane, i) pair: 256 threads, 256 bins
+    const int bl = t >> 3, bi = t & 7;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sum += s_sum[q][bl][bi];
+    const int bin = 2 * (blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * bl) + bi;
+    const unsigned long long v = (unsigned long long)sum + spill[bin];
+    table[bin] = v;
+    spill[bin] = 0;
+    unsigned long long k = 0;
+    if (bin < HOT_BINS && v && pair_ok(bin >> 8, bin & 255, len16, max_length))
+        k = pack_key(v, bin >> 8, bin & 255);
+    k = wave_max_u64(k);
+    if ((t & 63) == 0 && k) atomicMax(&res->best, k);
 }
 
 // Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there
@@ -1042,6 +1074,34 @@ __global__ void __launch_bounds__(1024) k_select(const unsigned long long *__res
         res->best = best;
         res->n_cand = s_n;
         res->n_heavy = s_heavy;
+    }
+}
+
+// Multi-workgroup selection once res->best holds the best hot key (k_reduce_table): every hot
+// pair sharing it (unordered: the tie rule does not depend on the order) and the heavy sketch
+// buckets (sum >= max(W_hot, 1)).  res->n_cand / n_heavy must be zero on entry.
+__global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *__restrict__ table,
+                                                      const int32_t *__restrict__ len16,
+                                                      int64_t max_length, Result *res, int2 *cand,
+                                                      uint32_t *__restrict__ heavy) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;   // grid covers TABLE_BINS exactly
+    const unsigned long long best = res->best;
+    if (idx < HOT_BINS) {
+        const int32_t a = idx >> 8, b = idx & 255;
+        if (best && pack_key(table[idx], a, b) == best && pair_ok(a, b, len16, max_length)) {
+            const unsigned i = atomicAdd(&res->n_cand, 1u);
+            if (i < CAND_CAP) cand[i] = make_int2(a, b);
+        }
+    } else {
+        const unsigned long long w_hot = best >> 17;
+        const unsigned long long T = w_hot ? w_hot : 1;
+        const int bk = idx - HOT_BINS;
+        const unsigned long long m = __ballot(table[idx] >= T);
+        if ((threadIdx.x & 31) == 0) {
+            const uint32_t word = (uint32_t)(m >> (threadIdx.x & 32));
+            heavy[bk >> 5] = word;
+            if (word) atomicAdd(&res->n_heavy, (unsigned)__popc(word));
+        }
     }
 }
 
