@@ -49,18 +49,17 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 // What one pass learned about its region of the (post-merge) corpus.  Live slots only.
 struct RegionSum {
     int64_t n_live;      // live slots (tokens + SEPs)
-    int64_t lead_len;    // length of the first run (deferred to k_runs)
-    int64_t trail_len;   // length of the last run (deferred to k_runs)
+    int64_t lead_len;    // length of the first run (the whole region when uniform)
     int32_t first_tok;   // first live slot value (NONE when the region is empty)
     int32_t last_tok;    // last live slot value
-    int32_t uniform;     // the region is one single run (lead == trail == whole region)
-    int32_t pad;
+    int32_t uniform;     // the region is one single run
+    int32_t trail_odd;   // the last run's length is odd (meaningful when not uniform)
 };
 
 // Boundary facts k_runs derives for the NEXT pass over the same corpus.
 struct RegionCarry {
-    int64_t carry_off;   // run offset of the region's first live token (0 unless its run began
-                         // in an earlier region)
+    int64_t carry_off;   // parity of the run offset of the region's first live token (0 unless
+                         // its run began in an earlier region)
     int32_t prev_tok;    // last live slot before the region (SEP at the corpus start)
     int32_t next_tok;    // first live slot after the region (SEP at the corpus end)
 };
@@ -314,19 +313,6 @@ __device__ __forceinline__ void run_starts(const Nbr &n, int lane, int rs[4]) {
     for (int e = 0; e < 4; ++e) rs[e] = rs[e] > excl ? rs[e] : excl;
 }
 
-__device__ __forceinline__ int first_start(const Nbr &n, int len) {
-    int f = len;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        unsigned long long m = __ballot(n.live[e] && !n.eqp[e]);
-        if (m) {
-            int k = 4 * __builtin_ctzll(m) + e;
-            f = k < f ? k : f;
-        }
-    }
-    return f;
-}
-
 // Exact run offsets of the live slots (needed where X X pairs are matched / located exactly).
 // prev_off = offset of the live token before the chunk (valid when slot 0 continues its run).
 // Returns the offset of the last live slot (the next chunk's prev_off).
@@ -351,200 +337,6 @@ __device__ __forceinline__ int64_t run_offsets(const View &w, const Nbr &n, int 
     }
     const int kl = w.len - 1;
     return bcast64(pick4(off, kl & 3), kl >> 2);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Count-side state of one region (wave-uniform).
-// ---------------------------------------------------------------------------------------------
-struct CountState {
-    int32_t prev;        // last live post-merge token counted so far (NONE at region start)
-    int32_t run_x;       // open run carried across chunks (-2: none)
-    int64_t run_len;
-    bool run_lead;       // the open run is the region's first run (deferred to k_runs)
-    bool started;
-    int64_t lead_len;
-    int64_t n_live;
-    int32_t first_tok;
-};
-
-// Counts the pairs of one post-merge chunk whose right side is inside the region: every pair
-// (k, next live) except X X pairs of the region's first and last run, which k_runs resolves.
-// nxt = first live token of the next non-empty chunk of the region, NONE for the region's last.
-template <int MODE>
-__device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
-                                                      CountState s, Sink k);
-
-template <int MODE>
-__device__ __forceinline__ void count_view(const View &w, int32_t nxt, bool last, int lane,
-                                           CountState &s, const Sink &k) {
-    if (!last && s.run_x == -2 && s.started) {
-        // Fast path: no run open across the chunk start.  Valid when no slot is the middle of a
-        // run of >= 3 and no X X pair ends the chunk: then every X X pair starts its run and
-        // counts (core.ts:285-290 never skips), so every valid pair (k, next live) counts.
-        const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
-        const int32_t p = from_prev(t3, s.prev);
-        const int kl = w.len - 1;
-        int32_t r0 = t1, r1 = t2, r2 = t3, r3 = from_next(t0, nxt);
-        if (MODE == MODE_TABLE && w.len == CHUNK) {
-            // Hottest path: a full chunk whose 256 pairs are all valid hot pairs (every id in
-            // [0, 256), so no SEP either) and no X X pair continues a run or ends the chunk.
-            const uint32_t u = (uint32_t)(t0 | t1 | t2 | t3 | r3);
-            const bool q0 = t0 == t1, q1 = t1 == t2, q2 = t2 == t3, q3 = t3 == r3;
-            const bool bad = u >= (uint32_t)HOT || (p == t0 && q0) || (q0 && q1) || (q1 && q2) ||
-                             (q2 && q3) || (lane == 63 && q3);
-            if (__ballot(bad) == 0ull) {
-                // bin b = x*256 + y: dword b/2 (byte (b*2) & ~3), half (y & 1)
-                const uint32_t b0 = ((uint32_t)t0 << 8) | (uint32_t)r0, b1 = ((uint32_t)t1 << 8) | (uint32_t)r1,
-                               b2 = ((uint32_t)t2 << 8) | (uint32_t)r2, b3 = ((uint32_t)t3 << 8) | (uint32_t)r3;
-                const uint32_t o0 = atomicAdd(&k.hist[b0 >> 1], 1u << ((b0 & 1) << 4));
-                const uint32_t o1 = atomicAdd(&k.hist[b1 >> 1], 1u << ((b1 & 1) << 4));
-                const uint32_t o2 = atomicAdd(&k.hist[b2 >> 1], 1u << ((b2 & 1) << 4));
-                const uint32_t o3 = atomicAdd(&k.hist[b3 >> 1], 1u << ((b3 & 1) << 4));
-                // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
-#ifdef BPE_EXP_NOCHECK
-                if (false) {
-#else
-                if (__ballot(((o0 | o1 | o2 | o3) & 0x40004000u) != 0u) != 0ull) {
-#endif
-                    const bool f0 = lds_needs_fix((int)b0, o0), f1 = lds_needs_fix((int)b1, o1),
-                               f2 = lds_needs_fix((int)b2, o2), f3 = lds_needs_fix((int)b3, o3);
-                    if (f0) lds_fix(k, (int)b0, o0);
-                    if (f1) lds_fix(k, (int)b1, o1);
-                    if (f2) lds_fix(k, (int)b2, o2);
-                    if (f3) lds_fix(k, (int)b3, o3);
-                }
-                s.n_live += CHUNK;
-                s.prev = bcast(t3, 63);
-                return;
-            }
-        }
-        bool end0 = false, end1 = false, end2 = false, end3 = lane == 63;
-        if (w.len != CHUNK) {
-            // left-packed partial chunk: the last live slot pairs with nxt, dead slots are TOMB
-            const bool ll = lane == (kl >> 2);
-            const int el = kl & 3;
-            end0 = ll && el == 0;
-            end1 = ll && el == 1;
-            end2 = ll && el == 2;
-            end3 = ll && el == 3;
-            r0 = end0 ? nxt : r0;
-            r1 = end1 ? nxt : r1;
-            r2 = end2 ? nxt : r2;
-            r3 = end3 ? nxt : r3;
-        }
-        const bool n0 = t0 >= 0 && t0 == r0, n1 = t1 >= 0 && t1 == r1, n2 = t2 >= 0 && t2 == r2,
-                   n3 = t3 >= 0 && t3 == r3;
-        const bool trip = (n0 && (t0 == p || end0)) || (n1 && (t1 == t0 || end1)) ||
-                          (n2 && (t2 == t1 || end2)) || (n3 && (t3 == t2 || end3));
-        if (__ballot(trip) == 0ull) {
-            const bool v0 = (t0 | r0) >= 0, v1 = (t1 | r1) >= 0, v2 = (t2 | r2) >= 0,
-                       v3 = (t3 | r3) >= 0;
-            if (MODE == MODE_TABLE) {
-                // four LDS atomics in flight, one overflow test; an invalid pair (SEP, dead
-                // slot) adds 0 to a lane-private word instead of branching
-                const int i0 = v0 ? table_index(t0, r0) : 2 * lane;   // dummy: a lane-private word, adds 0
-                const int i1 = v1 ? table_index(t1, r1) : 2 * lane;   // dummy: a lane-private word, adds 0
-                const int i2 = v2 ? table_index(t2, r2) : 2 * lane;   // dummy: a lane-private word, adds 0
-                const int i3 = v3 ? table_index(t3, r3) : 2 * lane;   // dummy: a lane-private word, adds 0
-                const uint32_t o0 = atomicAdd(&k.hist[i0 >> 1], (uint32_t)v0 << ((i0 & 1) << 4));
-                const uint32_t o1 = atomicAdd(&k.hist[i1 >> 1], (uint32_t)v1 << ((i1 & 1) << 4));
-                const uint32_t o2 = atomicAdd(&k.hist[i2 >> 1], (uint32_t)v2 << ((i2 & 1) << 4));
-                const uint32_t o3 = atomicAdd(&k.hist[i3 >> 1], (uint32_t)v3 << ((i3 & 1) << 4));
-                const bool f0 = v0 && lds_needs_fix(i0, o0), f1 = v1 && lds_needs_fix(i1, o1),
-                           f2 = v2 && lds_needs_fix(i2, o2), f3 = v3 && lds_needs_fix(i3, o3);
-                if (f0 || f1 || f2 || f3) {
-                    if (f0) lds_fix(k, i0, o0);
-                    if (f1) lds_fix(k, i1, o1);
-                    if (f2) lds_fix(k, i2, o2);
-                    if (f3) lds_fix(k, i3, o3);
-                }
-            } else {
-                if (v0) count_pair<MODE>(k, t0, r0);
-                if (v1) count_pair<MODE>(k, t1, r1);
-                if (v2) count_pair<MODE>(k, t2, r2);
-                if (v3) count_pair<MODE>(k, t3, r3);
-            }
-            s.n_live += w.len;
-            s.prev = w.len == CHUNK ? bcast(t3, 63) : view_at(w, kl);
-            return;
-        }
-    }
-    s = count_view_general<MODE>(w, nxt, last, lane, s, k);
-}
-
-// The general case: partial chunks, runs crossing chunk or region edges, SEPs.
-template <int MODE>
-__device__ __noinline__ CountState count_view_general(View w, int32_t nxt, bool last, int lane,
-                                                      CountState s, Sink k) {
-    if (!s.started) {
-        s.started = true;
-        s.first_tok = view_at(w, 0);
-        if (s.first_tok >= 0) {
-            // the first run is carried from "before" the chunk so that it is never counted here
-            s.prev = s.first_tok;
-            s.run_x = s.first_tok;
-            s.run_len = 0;
-            s.run_lead = true;
-        } else {
-            s.lead_len = 1;   // a SEP: a run of its own that never pairs
-        }
-    }
-    Nbr n;
-    neighbours(w, s.prev, nxt, lane, n);
-    s.n_live += w.len;
-    const int kl = w.len - 1;
-    bool slow = last || s.run_x != -2;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) slow |= n.eqn[e] && (n.eqp[e] || 4 * lane + e == kl);
-    bool counted[4];
-    if (__ballot(slow) == 0ull) {
-        // no run crosses the chunk and every run is <= 2 long: every valid pair counts
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            counted[e] = n.live[e] && w.t[e] >= 0 && n.partner[e] >= 0;
-    } else {
-        int rs[4];
-        run_starts(n, lane, rs);
-        const int rs_l = bcast(pick4(rs, kl & 3), kl >> 2);
-        const bool eqn_l = ((__ballot(pick4(n.eqn, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
-        const bool end_open = last || eqn_l;   // the last run continues past the chunk / is deferred
-        const int f = first_start(n, w.len);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            bool ok = n.live[e] && w.t[e] >= 0 && n.partner[e] >= 0;
-            if (ok && n.eqn[e]) {
-                const int k = 4 * lane + e;
-                if (rs[e] < 0) ok = false;                          // carried run
-                else if (end_open && rs[e] == rs_l) ok = false;     // open / deferred last run
-                else ok = ((k - rs[e]) & 1) == 0;
-            }
-            counted[e] = ok;
-        }
-        if (s.run_x != -2) {
-            int64_t L = -1;
-            if (f < w.len) L = s.run_len + f;
-            else if (!end_open) L = s.run_len + w.len;
-            else s.run_len += w.len;
-            if (L >= 0) {
-                if (s.run_lead) s.lead_len = L;
-                else if (lane == 0 && L >= 2)
-                    add_pairs_global<MODE>(k, s.run_x, s.run_x, (unsigned long long)(L >> 1));
-                s.run_x = -2;
-                s.run_len = 0;
-                s.run_lead = false;
-            }
-        }
-        if (s.run_x == -2 && end_open) {
-            s.run_x = view_at(w, kl);
-            s.run_len = w.len - rs_l;
-            s.run_lead = false;
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-        if (counted[e]) count_pair<MODE>(k, w.t[e], n.partner[e]);
-    s.prev = view_at(w, kl);
-    return s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -605,138 +397,257 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
     return total;
 }
 
-// Per-region state of the fused pass.
-struct StepState {
-    int32_t pre_prev;          // last pre-merge live token before the current chunk
-    int64_t pre_prev_off;      // its run offset
-    bool pre_prev_match;       // it is an `a` matched with the current chunk's first token
-    bool pre_started;
+// ---------------------------------------------------------------------------------------------
+// K1 (fused with K4): the streaming pass.
+//
+// One wave streams one region chunk by chunk through a 4-deep register ring.  With a merge the
+// pass is a two-stage pipeline inside the wave:
+//   stage 1  apply   chunk j-1 (pre-merge) once chunk j has arrived: its right-hand neighbour
+//                    (the first live token of chunk j) is then known, so every match, including
+//                    one straddling the chunk edge, is decided from registers;
+//   stage 2  count   the post-merge chunk before that, once the post-merge first token of its
+//                    successor is known.
+// Without a merge only stage 2 runs.  Empty chunks are skipped, so "the next chunk" is always
+// the next non-empty one and nothing is ever re-read.
+//
+// X X pairs follow the reference's skip rule (core.ts:285-290): an X X pair counts iff its left
+// slot sits at an even offset of its maximal run of X.  The wave carries the offset parity of the
+// last token from chunk to chunk, and measures the region's first run from the region start as if
+// nothing preceded it; k_runs adds what that assumption missed for runs that cross regions.
+// A chunk with no slot in the middle of a run of three or more (the common case) needs no parity
+// at all: then every valid pair counts.
+// ---------------------------------------------------------------------------------------------
+
+// Right-hand partner of each slot of a left-packed chunk: the next slot, or `nxt` (the first live
+// token after the chunk) for the last live slot.  Dead slots get junk and are never valid.
+__device__ __forceinline__ void right_of(const int32_t (&t)[4], int32_t nxt, int32_t (&r)[4]) {
+    r[0] = t[1];
+    r[1] = t[2];
+    r[2] = t[3];
+    r[3] = from_next(t[0], nxt);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = r[e] == TOMB ? nxt : r[e];
+}
+
+// Exact run-offset parity of every live slot (SEPs are runs of their own).  prev = the live token
+// before slot 0 (NONE: none), prev_par = the parity of its offset.
+__device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32_t prev,
+                                           int prev_par, int lane, int (&par)[4]) {
+    const int32_t l0 = from_prev(t[3], prev);
+    int lmax = -1;
+    int rs[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k = 4 * lane + e;
+        const int32_t left = e == 0 ? l0 : t[e - 1];
+        if (k < len && !(t[e] >= 0 && t[e] == left)) lmax = k;
+        rs[e] = lmax;
+    }
+    int incl = lmax;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl = o > incl ? o : incl;
+    }
+    int excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = -1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k = 4 * lane + e;
+        const int s = rs[e] > excl ? rs[e] : excl;
+        par[e] = s >= 0 ? ((k - s) & 1) : ((prev_par + 1 + k) & 1);
+    }
+}
+
+// Adds the counted pairs (t[e], r[e]) of one chunk to the sink.
+template <int MODE>
+__device__ __forceinline__ void count_pairs(const int32_t (&t)[4], const int32_t (&r)[4],
+                                            const bool (&cnt)[4], int lane, const Sink &k) {
+    if (MODE == MODE_TABLE) {
+        // t | r is < HOT (unsigned) exactly when the pair is valid and hot
+        bool cold = false;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cold |= cnt[e] && (uint32_t)(t[e] | r[e]) >= (uint32_t)HOT;
+        uint32_t i[4], o[4];
+        if (__ballot(cold) == 0ull) {
+            // hot pairs only: bin x*256 + y.  An uncounted slot adds 0 to a lane-private word.
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                i[e] = cnt[e] ? (((uint32_t)t[e] << 8) | (uint32_t)r[e]) : 2u * (uint32_t)lane;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = atomicAdd(&k.hist[i[e] >> 1], (uint32_t)cnt[e] << ((i[e] & 1) << 4));
+            // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
+            if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (cnt[e]) lds_fix(k, (int)i[e], o[e]);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                i[e] = cnt[e] ? (uint32_t)table_index(t[e], r[e]) : 2u * (uint32_t)lane;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = atomicAdd(&k.hist[i[e] >> 1], (uint32_t)cnt[e] << ((i[e] & 1) << 4));
+            bool f = false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f |= cnt[e] && lds_needs_fix((int)i[e], o[e]);
+            if (__ballot(f) != 0ull) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (cnt[e]) lds_fix(k, (int)i[e], o[e]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (cnt[e]) count_pair<MODE>(k, t[e], r[e]);
+    }
+}
+
+// Count-side state of one region (wave-uniform).
+struct Tally {
+    int64_t n_live;      // live slots counted so far
+    int64_t lead_len;    // length of the region's first run (once it has ended)
+    int32_t prev;        // last live token counted (NONE before the first)
+    int32_t par;         // run-offset parity of prev (the first run counts from the region start)
+    int32_t first_tok;   // the region's first live token
+    bool in_lead;        // every live token so far belongs to the region's first run
+};
+
+// Counts the pairs of one post-merge chunk (len > 0) whose right side lies inside the region:
+// nxt = the first live token of the next non-empty chunk, NONE past the region's end.
+template <int MODE>
+__device__ __forceinline__ void count_chunk(const int32_t (&t)[4], int len, int32_t nxt, int lane,
+                                            Tally &s, const Sink &k) {
+    int32_t r[4];
+    right_of(t, nxt, r);
+    const int32_t l0 = from_prev(t[3], s.prev);
+    bool eqL[4], eqR[4];
+    bool trip = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int32_t left = e == 0 ? l0 : t[e - 1];
+        eqL[e] = t[e] >= 0 && t[e] == left;
+        eqR[e] = t[e] >= 0 && t[e] == r[e];
+        trip |= eqL[e] && eqR[e];
+    }
+    const int kl = len - 1;
+    bool cnt[4];
+    int par_last;
+    if (__ballot(trip) == 0ull && !s.in_lead) {
+        // no slot inside a run of >= 3: every X X pair starts its run, so every valid pair counts
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt[e] = (t[e] | r[e]) >= 0;
+        const bool eql = ((__ballot(pick4(eqL, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
+        par_last = eql ? (kl >= 1 ? 1 : (s.par ^ 1)) : 0;
+    } else {
+        int par[4];
+        run_parity(t, len, s.prev, s.par, lane, par);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt[e] = (t[e] | r[e]) >= 0 && !(eqR[e] && par[e]);
+        par_last = bcast(pick4(par, kl & 3), kl >> 2);
+        if (s.in_lead) {
+            // the first run ends at the first run start at region position >= 1
+            int f = len;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int kk = 4 * lane + e;
+                const unsigned long long m =
+                    __ballot(kk < len && !eqL[e] && (s.n_live + kk) > 0);
+                if (m) {
+                    const int q = 4 * __builtin_ctzll(m) + e;
+                    f = q < f ? q : f;
+                }
+            }
+            if (f < len) {
+                s.lead_len = s.n_live + f;
+                s.in_lead = false;
+            }
+        }
+    }
+    if (s.n_live == 0) s.first_tok = bcast(t[0], 0);
+    count_pairs<MODE>(t, r, cnt, lane, k);
+    s.prev = bcast(pick4(t, kl & 3), kl >> 2);
+    s.par = par_last;
+    s.n_live += len;
+}
+
+// Apply-side state of one region (wave-uniform).
+struct Apply {
+    int32_t prev;                // last pre-merge live token before the chunk
+    int32_t par;                 // its run-offset parity (X X merges only)
+    bool match;                  // it is an `a` matched with the chunk's first live token
+    bool started;
     unsigned long long n_match;
-    CountState s;
-    View pend;                 // post-merge chunk waiting for its right neighbour
-    bool have_pend;
 };
 
 // What a k_step pass does before counting: nothing, a merge of two distinct ids, or an X X merge
 // (the only kind whose matches depend on run parity, so the only one carrying that code).
 enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
 
-// One chunk of the fused pass.  v = chunk c of the region (pre-merge; c counts from the
-// region's first chunk, nc chunks in all, rs = the region's buffer descriptor), nxt = lane-0 slot
-// of chunk c+1 (pre-merge; NONE past the region).
-template <int MERGE, int MODE>
-__device__ __forceinline__ void step_chunk(const int4 v, int32_t nxt, int c, int nc,
-                                           const __amdgpu_buffer_rsrc_t rs, int32_t ma, int32_t mb,
-                                           int32_t mc, const RegionCarry &rc, int lane,
-                                           StepState &st, const Sink &k) {
-    View w = make_view(v);
-    if (w.len == 0) return;
-    // first live pre-merge token after this chunk inside the region (NONE: none).  The chunks
-    // after c are not rewritten yet, so these loads see pre-merge data.
-    if (nxt == TOMB) {
-        for (int q = c + 2; q < nc && nxt == TOMB; ++q)
-            nxt = __builtin_amdgcn_readfirstlane(
-                (int)__builtin_amdgcn_raw_buffer_load_b32(rs, q * (CHUNK * 4), 0, 0));
-        if (nxt == TOMB) nxt = NONE;
+// Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region:
+// nxt = the first pre-merge live token after it (the next region's first for the last chunk).
+// A touched chunk is re-packed and written back; w becomes the post-merge chunk (possibly empty).
+template <int MERGE>
+__device__ __forceinline__ void apply_chunk(View &w, int32_t nxt, int32_t ma, int32_t mb,
+                                            int32_t mc, const __amdgpu_buffer_rsrc_t rs, int c,
+                                            int lane, Apply &ap) {
+    int32_t r[4];
+    right_of(w.t, nxt, r);
+    if (!ap.started) {
+        ap.started = true;
+        ap.match = ap.prev == ma && bcast(w.t[0], 0) == mb && (MERGE == MERGE_XY || ap.par == 0);
     }
-    // the post-merge token after this chunk is known now unless the merge can touch it
-    bool nxt_known = true;
-    if (MERGE) {
-        const int32_t nxt_pre = nxt == NONE ? rc.next_tok : nxt;
-        const int kl = w.len - 1;
-        if (!st.pre_started) {
-            st.pre_started = true;
-            const int32_t t0 = view_at(w, 0);
-            st.pre_prev_match = st.pre_prev == ma && t0 == mb &&
-                                (MERGE == MERGE_XY || ((rc.carry_off - 1) & 1) == 0);
-        }
-        bool m[4];
-        int64_t last_off = 0;
-        const int32_t dn = from_next(w.t[0], nxt_pre);
-        int32_t t_last;
-        if (w.len == CHUNK) {
-            m[0] = (w.t[0] == ma) & (w.t[1] == mb);
-            m[1] = (w.t[1] == ma) & (w.t[2] == mb);
-            m[2] = (w.t[2] == ma) & (w.t[3] == mb);
-            m[3] = (w.t[3] == ma) & (dn == mb);
-            t_last = bcast(w.t[3], 63);
-        } else {
-            const int l4 = 4 * lane;
+    bool m[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int32_t partner = l4 < kl - e ? (e < 3 ? w.t[e + 1] : dn) : nxt_pre;
-                m[e] = (l4 < w.len - e) & (w.t[e] == ma) & (partner == mb);
-            }
-            t_last = view_at(w, kl);
-        }
-        unsigned long long M0 = __ballot(m[0]), M1 = __ballot(m[1]), M2 = __ballot(m[2]),
-                           M3 = __ballot(m[3]);
-        if (MERGE == MERGE_XX && ((M0 | M1 | M2 | M3) != 0ull || t_last == ma)) {
-            // X X merge: only even run offsets match (core.ts:285-290 == replaceAll)
-            Nbr n;
-            neighbours(w, st.pre_prev, nxt_pre, lane, n);
-            int64_t off[4];
-            last_off = run_offsets(w, n, lane, st.pre_prev_off, off);
+    for (int e = 0; e < 4; ++e) m[e] = (w.t[e] == ma) & (r[e] == mb);
+    const int kl = w.len - 1;
+    const int32_t t_last = bcast(pick4(w.t, kl & 3), kl >> 2);
+    int par_last = 0;
+    if (MERGE == MERGE_XX) {
+        // only even run offsets match (core.ts:285-290 == replaceAll's leftmost rule); the
+        // parity is carried only while the chunk ends in `a`
+        if (__ballot(m[0] | m[1] | m[2] | m[3]) != 0ull || t_last == ma) {
+            int par[4];
+            run_parity(w.t, w.len, ap.prev, ap.par, lane, par);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) m[e] = m[e] && (off[e] & 1) == 0;
-            M0 = __ballot(m[0]);
-            M1 = __ballot(m[1]);
-            M2 = __ballot(m[2]);
-            M3 = __ballot(m[3]);
+            for (int e = 0; e < 4; ++e) m[e] = m[e] && par[e] == 0;
+            par_last = bcast(pick4(par, kl & 3), kl >> 2);
         }
-        const int el = kl & 3;
-        const unsigned long long ML = el == 0 ? M0 : el == 1 ? M1 : el == 2 ? M2 : M3;
-        const bool m_last = ((ML >> (kl >> 2)) & 1ull) != 0;
-        if (st.pre_prev_match || (M0 | M1 | M2 | M3) != 0ull) {
-            const bool m_up = from_prev((int)m[3], (int)st.pre_prev_match) != 0;
-            const int l4 = 4 * lane;
-            bool keep[4];
-            keep[0] = (l4 < w.len) & !m_up;
-            keep[1] = (l4 < w.len - 1) & !m[0];
-            keep[2] = (l4 < w.len - 2) & !m[1];
-            keep[3] = (l4 < w.len - 3) & !m[2];
-            int32_t y[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
-            const int total = compact_chunk(y, keep, w.len, lane);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
-                                   make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
-                rs, lane * 16 + c * (CHUNK * 4), 0, 0);
-            st.n_match += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w.t[e] = y[e];
-            w.len = total;
-        }
-        st.pre_prev = t_last;
-        st.pre_prev_off = last_off;
-        st.pre_prev_match = m_last;
-        // the next chunk's first token survives unchanged unless it is a or b
-        nxt_known = nxt == NONE || (nxt != ma && nxt != mb);
-        if (w.len == 0) return;
     }
-    // A parked chunk (its right neighbour was unknown) is counted now, through the general path
-    // (rare: it keeps the inlined fast path single); then w is counted or parked in turn.
-    if (st.have_pend) {
-        st.s = count_view_general<MODE>(st.pend, view_at(w, 0), false, lane, st.s, k);
-        st.have_pend = false;
+    const unsigned long long M0 = __ballot(m[0]), M1 = __ballot(m[1]), M2 = __ballot(m[2]),
+                             M3 = __ballot(m[3]);
+    const int el = kl & 3;
+    const unsigned long long ML = el == 0 ? M0 : el == 1 ? M1 : el == 2 ? M2 : M3;
+    const bool m_last = ((ML >> (kl >> 2)) & 1ull) != 0;
+    if (ap.match || (M0 | M1 | M2 | M3) != 0ull) {
+        const bool up = from_prev((int)m[3], (int)ap.match) != 0;
+        const int l4 = 4 * lane;
+        bool keep[4];
+        keep[0] = (l4 < w.len) & !up;
+        keep[1] = (l4 < w.len - 1) & !m[0];
+        keep[2] = (l4 < w.len - 2) & !m[1];
+        keep[3] = (l4 < w.len - 3) & !m[2];
+        int32_t y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
+        const int total = compact_chunk(y, keep, w.len, lane);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
+                               make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
+            rs, lane * 16 + c * (CHUNK * 4), 0, 0);
+        ap.n_match += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w.t[e] = y[e];
+        w.len = total;
     }
-    if (nxt_known) {
-        count_view<MODE>(w, nxt, nxt == NONE, lane, st.s, k);
-    } else {
-        st.pend = w;
-        st.have_pend = true;
-    }
+    ap.prev = t_last;
+    ap.par = par_last;
+    ap.match = m_last;
 }
 
-// ---------------------------------------------------------------------------------------------
-// K1 (fused with K4): one streaming pass over the corpus.  With MERGE, first applies the pending
-// merge (a, b) -> c to every chunk (matches found on the pre-merge stream with the exact X X
-// parity; touched chunks are re-packed and written back), then counts every pair of the
-// post-merge stream (hot pairs and sketch buckets in LDS; MODE_EXACT: heavy cold pairs in the
-// sparse table).  One wave streams one region through a 4-deep register ring (the loop is
-// unrolled by the ring depth so no register rotation waits on an in-flight load).
-// ---------------------------------------------------------------------------------------------
 template <int MERGE, int MODE>
 __global__ void __launch_bounds__(WG)
 k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
@@ -764,73 +675,86 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
         const int64_t c0 = (int64_t)r * cpr;
         const int64_t c1 = min(c0 + cpr, n_chunks);
         const RegionCarry rc = carry[r];
-        StepState st;
-        st.pre_prev = rc.prev_tok;
-        st.pre_prev_off = rc.carry_off - 1;
-        st.pre_prev_match = false;
-        st.pre_started = false;
-        st.n_match = 0;
-        st.s.prev = NONE;
-        st.s.run_x = -2;
-        st.s.run_len = 0;
-        st.s.run_lead = false;
-        st.s.started = false;
-        st.s.lead_len = 0;
-        st.s.n_live = 0;
-        st.s.first_tok = NONE;
-        st.have_pend = false;
+        Tally s;
+        s.n_live = 0;
+        s.lead_len = 0;
+        s.prev = NONE;
+        s.par = 0;
+        s.first_tok = NONE;
+        s.in_lead = true;
+        Apply ap;
+        ap.prev = rc.prev_tok;
+        ap.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
+        ap.match = false;
+        ap.started = false;
+        ap.n_match = 0;
+        View P, H;           // P: post-merge chunk awaiting its count; H: pre-merge chunk awaiting
+        P.len = H.len = 0;   //    its apply (merge passes only)
+        int hc = 0;
+        // the region through a range-checked buffer descriptor (loads past its end return 0 and
+        // are never consumed)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            ids + c0 * CHUNK, 0, (int)(c1 > c0 ? (c1 - c0) * CHUNK * 4 : 0), 0x00020000);
+        // stage 2 input: the next non-empty post-merge chunk in stream order
+        auto feed = [&](const View &q) {
+            if (P.len) count_chunk<MODE>(P.t, P.len, bcast(q.t[0], 0), lane, s, k);
+            P = q;
+        };
+        auto stage = [&](const int4 v, int c) {
+            const View q = make_view(v);
+            if (q.len == 0) return;
+            if (MERGE) {
+                if (H.len) {
+                    apply_chunk<MERGE>(H, bcast(q.t[0], 0), ma, mb, mc, rs, hc, lane, ap);
+                    if (H.len) feed(H);
+                }
+                H = q;
+                hc = c;
+            } else {
+                feed(q);
+            }
+        };
         if (c0 < c1) {
-            // the region through a range-checked buffer descriptor: loads past its end return 0
-            // and are never consumed
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                ids + c0 * CHUNK, 0, (int)((c1 - c0) * CHUNK * 4), 0x00020000);
             const int lo = lane * 16;
             const int nc = (int)(c1 - c0);
             auto load = [&](int c) -> int4 {
                 const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + c * (CHUNK * 4), 0, 0);
                 return make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
             };
+            // 4-deep ring, unrolled by its depth so no register rotation waits on a load
             int4 q0 = load(0), q1 = load(1), q2 = load(2), q3 = load(3);
-#define BPE_STAGE(QC, QN, CC)                                                                   \
+#define BPE_STAGE(QC, CC)                                                                       \
     {                                                                                           \
         const int4 v_ = QC;                                                                     \
         QC = load((CC) + 4);                                                                    \
-        const int32_t nx_ = (CC) + 1 < nc ? bcast(QN.x, 0) : NONE;                              \
-        step_chunk<MERGE, MODE>(v_, nx_, (CC), nc, rs, ma, mb, mc, rc, lane, st, k);            \
+        stage(v_, (CC));                                                                        \
     }
             for (int c = 0; c < nc; c += 4) {
-                BPE_STAGE(q0, q1, c)
+                BPE_STAGE(q0, c)
                 if (c + 1 >= nc) break;
-                BPE_STAGE(q1, q2, c + 1)
+                BPE_STAGE(q1, c + 1)
                 if (c + 2 >= nc) break;
-                BPE_STAGE(q2, q3, c + 2)
+                BPE_STAGE(q2, c + 2)
                 if (c + 3 >= nc) break;
-                BPE_STAGE(q3, q0, c + 3)
+                BPE_STAGE(q3, c + 3)
             }
 #undef BPE_STAGE
         }
-        CountState &s = st.s;
-        if (st.have_pend) count_view<MODE>(st.pend, NONE, true, lane, s, k);
+        if (MERGE && H.len) {
+            apply_chunk<MERGE>(H, rc.next_tok, ma, mb, mc, rs, hc, lane, ap);
+            if (H.len) feed(H);
+        }
+        if (P.len) count_chunk<MODE>(P.t, P.len, NONE, lane, s, k);
         if (lane == 0) {
-            RegionSum rsum;
-            rsum.n_live = s.n_live;
-            rsum.first_tok = s.n_live ? s.first_tok : NONE;
-            rsum.last_tok = s.n_live ? s.prev : NONE;
-            rsum.pad = 0;
-            if (s.n_live == 0) {
-                rsum.lead_len = rsum.trail_len = 0;
-                rsum.uniform = 0;
-            } else if (s.run_x != -2) {
-                rsum.uniform = s.run_lead ? 1 : 0;
-                rsum.trail_len = s.run_len;
-                rsum.lead_len = s.run_lead ? s.run_len : s.lead_len;
-            } else {
-                rsum.uniform = 0;
-                rsum.trail_len = 0;
-                rsum.lead_len = s.lead_len;
-            }
-            sums[r] = rsum;
-            if (MERGE && st.n_match) atomicAdd(replaced, st.n_match);
+            RegionSum o;
+            o.n_live = s.n_live;
+            o.first_tok = s.n_live ? s.first_tok : NONE;
+            o.last_tok = s.n_live ? s.prev : NONE;
+            o.uniform = s.n_live && s.in_lead ? 1 : 0;
+            o.lead_len = s.in_lead ? s.n_live : s.lead_len;
+            o.trail_odd = s.par ^ 1;   // trail run length = offset of the last token + 1
+            sums[r] = o;
+            if (MERGE && ap.n_match) atomicAdd(replaced, ap.n_match);
         }
     }
     if (MODE == MODE_TABLE) {
@@ -851,9 +775,13 @@ __device__ __forceinline__ int next_nonempty(const RegionSum *s, int q, int R) {
     return q;
 }
 
-// Stitches the regions: counts the pair straddling every boundary, floor(L/2) X X pairs of every
-// run that was deferred (a region's first and last run, possibly spanning regions), and derives
-// the RegionCarry the next pass over this corpus needs.
+// Stitches the regions after a pass.  The waves counted every pair inside their region, with the
+// X X pairs of each region's first run counted from the region start; here, per region:
+//  - the pair straddling its left boundary (unless both sides belong to one run);
+//  - for the run that starts in the region and continues into later regions (segments of lengths
+//    L_1..L_n, the waves having counted sum floor(L_i / 2)): floor(sum L_i / 2) - sum floor(L_i / 2)
+//    = floor(#odd segments / 2) more X X pairs;
+//  - the RegionCarry the next pass needs (neighbour tokens, run-offset parity of the first token).
 template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
                        unsigned long long *__restrict__ spill, ColdTable ct,
@@ -879,51 +807,41 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     const int32_t x0 = me.first_tok;
     const bool linked = p >= 0 && x0 >= 0 && s[p].last_tok == x0;
     if (linked) {
-        int64_t off = 0;
+        // parity of the number of x0 tokens of the run before this region
+        int64_t par = 0;
         for (int q = p; q >= 0;) {
             if (s[q].uniform) {
-                off += s[q].n_live;
+                par ^= s[q].n_live & 1;
                 const int q2 = prev_nonempty(s, q - 1);
                 if (q2 >= 0 && s[q2].last_tok == x0) q = q2;
                 else break;
             } else {
-                off += s[q].trail_len;
+                par ^= s[q].trail_odd;
                 break;
             }
         }
-        rc.carry_off = off;
+        rc.carry_off = par;
     } else if (p >= 0 && x0 >= 0 && s[p].last_tok >= 0) {
         add_pairs_global<MODE>(k, s[p].last_tok, x0, 1);            // the boundary pair
     }
     carry[r] = rc;
-    // runs that START in this region: the first run (if not continuing one) and the last run
-    int32_t wx = NONE;
-    int64_t L = 0;
-    if (me.uniform) {
-        if (!linked && x0 >= 0) {
-            wx = x0;
-            L = me.n_live;
-        }
-    } else {
-        if (!linked && x0 >= 0 && me.lead_len >= 2)
-            add_pairs_global<MODE>(k, x0, x0, (unsigned long long)(me.lead_len >> 1));
-        if (me.last_tok >= 0 && me.trail_len > 0) {
-            wx = me.last_tok;
-            L = me.trail_len;
+    // the run that starts in this region and reaches its end
+    if (me.uniform && linked) return;
+    const int32_t x = me.uniform ? x0 : me.last_tok;
+    if (x < 0) return;
+    int64_t odd = me.uniform ? (me.n_live & 1) : me.trail_odd;
+    int segs = 1;
+    for (int q = nx; q < R && s[q].first_tok == x;) {
+        ++segs;
+        if (s[q].uniform) {
+            odd += s[q].n_live & 1;
+            q = next_nonempty(s, q + 1, R);
+        } else {
+            odd += s[q].lead_len & 1;
+            break;
         }
     }
-    if (wx >= 0) {
-        for (int q = nx; q < R && s[q].first_tok == wx;) {
-            if (s[q].uniform) {
-                L += s[q].n_live;
-                q = next_nonempty(s, q + 1, R);
-            } else {
-                L += s[q].lead_len;
-                break;
-            }
-        }
-        if (L >= 2) add_pairs_global<MODE>(k, wx, wx, (unsigned long long)(L >> 1));
-    }
+    if (segs > 1 && odd >= 2) add_pairs_global<MODE>(k, x, x, (unsigned long long)(odd >> 1));
 }
 
 // Sums the per-workgroup 16-bit LDS partials and the spill table into the u64 table (hot bins

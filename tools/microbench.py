@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Kernel-level timing of the engine on the C3 corpus: plain count passes (K1 alone) and merge
-passes (fused K4+K1), from the engine's own HIP events.  Usage: python tools/microbench.py [MiB]"""
+passes (fused K4+K1), from the engine's own HIP events, optionally after PRE untimed merges
+(the steady state of a long run).  Usage: python tools/microbench.py [MiB] [alphabet] [steps] [PRE]"""
 import importlib
 import json
 import os
@@ -16,12 +17,15 @@ def main():
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     A = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    pre = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     data = pkg.synth_latin1(mib << 20, seed=12345, A=A, base=0 if A == 256 else 0x20)
     e = pkg.Engine(0)
     t0 = time.perf_counter()
     cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
     ingest = time.perf_counter() - t0
     del data
+    if pre:
+        nt += len(e.merge_until(0, 2, pre))
     e.stats_enable(True)
     e.recount()
     e.reset_stats()
@@ -39,7 +43,7 @@ def main():
     st = e.stats()
     live = rc['step_live'] / rc['step_launches']
     out = {
-        'corpus_mib': mib, 'ingest_s': ingest,
+        'corpus_mib': mib, 'pre_merges': pre, 'ingest_s': ingest,
         'recount_ms': rc['step_ms'] / rc['step_launches'],
         'recount_GBps_alg': 4 * live / (rc['step_ms'] / rc['step_launches'] * 1e-3) / 1e9,
         'merge_pass_ms': st['step_ms'] / max(1, st['step_launches']),
