@@ -190,34 +190,67 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
     else if (exact_wanted<MODE>(k, x, y)) cold_add(k.ct, pair_key(x, y), (uint32_t)n);
 }
 
-// 16-bit LDS counters, two per dword.  A counter reaching 0x8000 spills 0x8000 to the global u64
-// table: exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom
-// absorbs every add that lands before its subtraction (a CU issues far fewer in flight), so no
-// field ever carries into its neighbour.
-__device__ __forceinline__ uint32_t lds_inc(uint32_t *hist, int idx) {
-    return atomicAdd(&hist[idx >> 1], 1u << ((idx & 1) << 4));
+// The LDS table: 16-bit counters, two per dword.
+//  - hot pair (x, y), both < 256: dword (y << 7) | (x >> 1), half x & 1, i.e. byte address
+//    ((x << 1) & 0x1FC) | (y << 9) and increment 1 << ((x << 4) & 16): five VALU operations, the
+//    half chosen by a bit the shift amount already carries;
+//  - sketch bucket b of a cold pair: dword HOT_BINS / 2 + (b >> 1), half b & 1.
+// A counter reaching 0x8000 spills 0x8000 to the global u64 table (indexed by table_index):
+// exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom absorbs
+// every add that lands before its subtraction (a CU issues far fewer in flight), so no field
+// ever carries into its neighbour.
+constexpr uint32_t HOT_BYTES = HOT_BINS * 2;   // 128 KiB
+
+__device__ __forceinline__ uint32_t hot_addr(int32_t x, int32_t y) {
+    return (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
 }
 
-__device__ __forceinline__ bool lds_needs_fix(int idx, uint32_t old) {
-    return ((old >> ((idx & 1) << 4)) & 0xFFFFu) == 0x7FFFu;
+// 1 << ((x & 1) * 16): the shift operand's low five bits of x << 4 are exactly that
+__device__ __forceinline__ uint32_t hot_inc(int32_t x) {
+    return 1u << (((uint32_t)x << 4) & 31u);
 }
 
-__device__ __forceinline__ void lds_fix(const Sink &k, int idx, uint32_t old) {
-    if (!lds_needs_fix(idx, old)) return;
-    atomicSub(&k.hist[idx >> 1], 0x8000u << ((idx & 1) << 4));
+__device__ __forceinline__ uint32_t sketch_hash(int32_t x, int32_t y) {
+    return (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) + (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
+}
+
+// bucket h >> 18: dword HOT_BINS / 2 + (h >> 19), half (h >> 18) & 1
+__device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | ((h >> 17) & 0x7FFCu); }
+__device__ __forceinline__ uint32_t cold_inc(uint32_t h) { return 1u << ((h >> 14) & 16u); }
+
+__device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
+    return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + addr);
+}
+
+// After an add of inc (1 << sh) at addr returned old: spill if this add reached 0x8000.
+__device__ __forceinline__ void lds_fix(const Sink &k, uint32_t addr, uint32_t inc, uint32_t bin,
+                                        uint32_t old) {
+    const uint32_t sh = inc == 1u ? 0u : 16u;
+    if (((old >> sh) & 0xFFFFu) != 0x7FFFu) return;
+    atomicSub(lds_word(k, addr), 0x8000u << sh);
     // (the constant is made opaque so it is materialised here, not held in registers across the
     // streaming loop for this rare path)
-    uint32_t inc = 0x8000u;
-    asm volatile("" : "+v"(inc));
-    atomicAdd(&k.spill[idx], (unsigned long long)inc);
+    uint32_t big = 0x8000u;
+    asm volatile("" : "+v"(big));
+    atomicAdd(&k.spill[bin], (unsigned long long)big);
 }
 
-// One counted occurrence of (x, y).
+// One counted occurrence of (x, y) (outside the streaming fast paths).
 template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
     if (MODE == MODE_TABLE) {
-        const int idx = table_index(x, y);
-        lds_fix(k, idx, lds_inc(k.hist, idx));
+        uint32_t addr, inc, bin;
+        if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) {
+            addr = hot_addr(x, y);
+            inc = hot_inc(x);
+            bin = ((uint32_t)x << 8) | (uint32_t)y;
+        } else {
+            const uint32_t h = sketch_hash(x, y);
+            addr = cold_addr(h);
+            inc = cold_inc(h);
+            bin = HOT_BINS + (h >> SKETCH_SHIFT);
+        }
+        lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
     } else if (exact_wanted<MODE>(k, x, y)) {
         cold_add(k.ct, pair_key(x, y), 1u);
     }
@@ -400,39 +433,75 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
 // ---------------------------------------------------------------------------------------------
 // K1 (fused with K4): the streaming pass.
 //
-// One wave streams one region chunk by chunk through a 4-deep register ring.  With a merge the
-// pass is a two-stage pipeline inside the wave:
-//   stage 1  apply   chunk j-1 (pre-merge) once chunk j has arrived: its right-hand neighbour
-//                    (the first live token of chunk j) is then known, so every match, including
-//                    one straddling the chunk edge, is decided from registers;
-//   stage 2  count   the post-merge chunk before that, once the post-merge first token of its
-//                    successor is known.
-// Without a merge only stage 2 runs.  Empty chunks are skipped, so "the next chunk" is always
-// the next non-empty one and nothing is ever re-read.
+// One wave streams one region chunk by chunk through a 6-slot register ring (the loop is unrolled
+// by 6, so every slot is a fixed set of registers and nothing is ever copied):
+//   - the current chunk j is applied in place (merge passes), its right-hand neighbour being the
+//     first live token of chunk j+1, already in the ring;
+//   - the post-merge chunk before it (the ring slot of j-1) is counted, its right-hand neighbour
+//     being the first post-merge token of chunk j;
+//   - that slot is then refilled with chunk j+5.
+// Empty chunks (rare: every token deleted) hand the pending chunk on to the next slot.
+//
+// Per-slot tests are vector compares whose results are wave masks (SGPR pairs); everything
+// derived from them is scalar work.  Only the pair-table address arithmetic and the compares are
+// vector instructions on the common path.
 //
 // X X pairs follow the reference's skip rule (core.ts:285-290): an X X pair counts iff its left
 // slot sits at an even offset of its maximal run of X.  The wave carries the offset parity of the
 // last token from chunk to chunk, and measures the region's first run from the region start as if
-// nothing preceded it; k_runs adds what that assumption missed for runs that cross regions.
-// A chunk with no slot in the middle of a run of three or more (the common case) needs no parity
-// at all: then every valid pair counts.
+// nothing preceded it; k_runs adds what that assumption missed for runs that cross regions.  A
+// chunk with no slot in the middle of a run of three or more (the common case) needs no parity:
+// then every valid pair counts.
 // ---------------------------------------------------------------------------------------------
 
-// Right-hand partner of each slot of a left-packed chunk: the next slot, or `nxt` (the first live
-// token after the chunk) for the last live slot.  Dead slots get junk and are never valid.
-__device__ __forceinline__ void right_of(const int32_t (&t)[4], int32_t nxt, int32_t (&r)[4]) {
-    r[0] = t[1];
-    r[1] = t[2];
-    r[2] = t[3];
-    r[3] = from_next(t[0], nxt);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] = r[e] == TOMB ? nxt : r[e];
+// Registers of one ring slot: the lane's four slots + wave-uniform facts.
+struct Chunk {
+    int32_t t[4];
+    int len;         // live slots (left-packed)
+    int32_t first;   // slot 0 (TOMB when empty)
+    int32_t last;    // last live slot (NONE when empty)
+};
+
+// Slot k (wave-uniform) broadcast from its lane.
+__device__ __forceinline__ int32_t slot_at(const int32_t (&t)[4], int k) {
+    const int l = k >> 2;
+    switch (k & 3) {
+    case 0: return bcast(t[0], l);
+    case 1: return bcast(t[1], l);
+    case 2: return bcast(t[2], l);
+    default: return bcast(t[3], l);
+    }
 }
 
-// Exact run-offset parity of every live slot (SEPs are runs of their own).  prev = the live token
-// before slot 0 (NONE: none), prev_par = the parity of its offset.
+// Lanes whose plane-e slot 4*lane + e lies below n.
+__device__ __forceinline__ unsigned long long lanes_below(int n, int e) {
+    const int m = (n - e + 3) >> 2;
+    return m >= 64 ? ~0ull : m <= 0 ? 0ull : ((1ull << m) - 1ull);
+}
+
+__device__ __forceinline__ bool lane_in(unsigned long long m) {
+    return __builtin_amdgcn_inverse_ballot_w64(m);
+}
+
+// Wave-uniform facts of a freshly loaded chunk.
+__device__ __forceinline__ void finish_load(Chunk &c) {
+    c.first = bcast(c.t[0], 0);
+    const int32_t l3 = bcast(c.t[3], 63);
+    if (l3 != TOMB) {
+        c.len = CHUNK;
+        c.last = l3;
+    } else {
+        c.len = __popcll(__ballot(c.t[0] != TOMB)) + __popcll(__ballot(c.t[1] != TOMB)) +
+                __popcll(__ballot(c.t[2] != TOMB)) + __popcll(__ballot(c.t[3] != TOMB));
+        c.last = c.len ? slot_at(c.t, c.len - 1) : NONE;
+    }
+}
+
+// Exact run-offset parity of every live slot (SEPs are runs of their own), and the run starts.
+// prev = the live token before slot 0 (NONE: none), prev_par = the parity of its offset.
 __device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32_t prev,
-                                           int prev_par, int lane, int (&par)[4]) {
+                                           int prev_par, int lane, int (&par)[4],
+                                           bool (&start)[4]) {
     const int32_t l0 = from_prev(t[3], prev);
     int lmax = -1;
     int rs[4];
@@ -440,7 +509,8 @@ __device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32
     for (int e = 0; e < 4; ++e) {
         const int k = 4 * lane + e;
         const int32_t left = e == 0 ? l0 : t[e - 1];
-        if (k < len && !(t[e] >= 0 && t[e] == left)) lmax = k;
+        start[e] = k < len && !(t[e] >= 0 && t[e] == left);
+        if (start[e]) lmax = k;
         rs[e] = lmax;
     }
     int incl = lmax;
@@ -459,53 +529,6 @@ __device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32
     }
 }
 
-// Adds the counted pairs (t[e], r[e]) of one chunk to the sink.
-template <int MODE>
-__device__ __forceinline__ void count_pairs(const int32_t (&t)[4], const int32_t (&r)[4],
-                                            const bool (&cnt)[4], int lane, const Sink &k) {
-    if (MODE == MODE_TABLE) {
-        // t | r is < HOT (unsigned) exactly when the pair is valid and hot
-        bool cold = false;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cold |= cnt[e] && (uint32_t)(t[e] | r[e]) >= (uint32_t)HOT;
-        uint32_t i[4], o[4];
-        if (__ballot(cold) == 0ull) {
-            // hot pairs only: bin x*256 + y.  An uncounted slot adds 0 to a lane-private word.
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                i[e] = cnt[e] ? (((uint32_t)t[e] << 8) | (uint32_t)r[e]) : 2u * (uint32_t)lane;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                o[e] = atomicAdd(&k.hist[i[e] >> 1], (uint32_t)cnt[e] << ((i[e] & 1) << 4));
-            // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
-            if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (cnt[e]) lds_fix(k, (int)i[e], o[e]);
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                i[e] = cnt[e] ? (uint32_t)table_index(t[e], r[e]) : 2u * (uint32_t)lane;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                o[e] = atomicAdd(&k.hist[i[e] >> 1], (uint32_t)cnt[e] << ((i[e] & 1) << 4));
-            bool f = false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) f |= cnt[e] && lds_needs_fix((int)i[e], o[e]);
-            if (__ballot(f) != 0ull) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (cnt[e]) lds_fix(k, (int)i[e], o[e]);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (cnt[e]) count_pair<MODE>(k, t[e], r[e]);
-    }
-}
-
 // Count-side state of one region (wave-uniform).
 struct Tally {
     int64_t n_live;      // live slots counted so far
@@ -516,60 +539,179 @@ struct Tally {
     bool in_lead;        // every live token so far belongs to the region's first run
 };
 
-// Counts the pairs of one post-merge chunk (len > 0) whose right side lies inside the region:
-// nxt = the first live token of the next non-empty chunk, NONE past the region's end.
-template <int MODE>
-__device__ __forceinline__ void count_chunk(const int32_t (&t)[4], int len, int32_t nxt, int lane,
-                                            Tally &s, const Sink &k) {
-    int32_t r[4];
-    right_of(t, nxt, r);
-    const int32_t l0 = from_prev(t[3], s.prev);
-    bool eqL[4], eqR[4];
-    bool trip = false;
+// Hot pairs (t[e], r[e]) of lanes in `m` (all lanes when m is ~0): LDS adds with the overflow
+// screen; returns the OR of the returned words (the caller screens) in acc.
+template <bool MASKED>
+__device__ __forceinline__ void add_hot(const int32_t (&x)[4], const int32_t (&y)[4],
+                                        const unsigned long long (&m)[4], uint32_t (&o)[4],
+                                        uint32_t &acc, const Sink &k) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        const int32_t left = e == 0 ? l0 : t[e - 1];
-        eqL[e] = t[e] >= 0 && t[e] == left;
-        eqR[e] = t[e] >= 0 && t[e] == r[e];
-        trip |= eqL[e] && eqR[e];
-    }
-    const int kl = len - 1;
-    bool cnt[4];
-    int par_last;
-    if (__ballot(trip) == 0ull && !s.in_lead) {
-        // no slot inside a run of >= 3: every X X pair starts its run, so every valid pair counts
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cnt[e] = (t[e] | r[e]) >= 0;
-        const bool eql = ((__ballot(pick4(eqL, kl & 3)) >> (kl >> 2)) & 1ull) != 0;
-        par_last = eql ? (kl >= 1 ? 1 : (s.par ^ 1)) : 0;
-    } else {
-        int par[4];
-        run_parity(t, len, s.prev, s.par, lane, par);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cnt[e] = (t[e] | r[e]) >= 0 && !(eqR[e] && par[e]);
-        par_last = bcast(pick4(par, kl & 3), kl >> 2);
-        if (s.in_lead) {
-            // the first run ends at the first run start at region position >= 1
-            int f = len;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int kk = 4 * lane + e;
-                const unsigned long long m =
-                    __ballot(kk < len && !eqL[e] && (s.n_live + kk) > 0);
-                if (m) {
-                    const int q = 4 * __builtin_ctzll(m) + e;
-                    f = q < f ? q : f;
-                }
-            }
-            if (f < len) {
-                s.lead_len = s.n_live + f;
-                s.in_lead = false;
-            }
+        if (!MASKED || lane_in(m[e])) {
+            o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
+            acc |= o[e];
         }
     }
-    if (s.n_live == 0) s.first_tok = bcast(t[0], 0);
-    count_pairs<MODE>(t, r, cnt, lane, k);
-    s.prev = bcast(pick4(t, kl & 3), kl >> 2);
+}
+
+// Cold pairs of lanes in `m`: sketch buckets.
+__device__ __forceinline__ void add_cold(const int32_t (&x)[4], const int32_t (&y)[4],
+                                         const unsigned long long (&m)[4], uint32_t (&o)[4],
+                                         uint32_t &acc, const Sink &k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (lane_in(m[e])) {
+            const uint32_t h = sketch_hash(x[e], y[e]);
+            o[e] = atomicAdd(lds_word(k, cold_addr(h)), cold_inc(h));
+            acc |= o[e];
+        }
+    }
+}
+
+// Exact spill check after a screen hit (rare).
+__device__ __forceinline__ void fix_all(const int32_t (&x)[4], const int32_t (&y)[4],
+                                        const unsigned long long (&H)[4],
+                                        const unsigned long long (&Cd)[4], const uint32_t (&oh)[4],
+                                        const uint32_t (&oc)[4], const Sink &k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (lane_in(H[e]))
+            lds_fix(k, hot_addr(x[e], y[e]), hot_inc(x[e]), ((uint32_t)x[e] << 8) | (uint32_t)y[e],
+                    oh[e]);
+        if (lane_in(Cd[e])) {
+            const uint32_t h = sketch_hash(x[e], y[e]);
+            lds_fix(k, cold_addr(h), cold_inc(h), HOT_BINS + (h >> SKETCH_SHIFT), oc[e]);
+        }
+    }
+}
+
+// Counts the pairs of one post-merge chunk (len > 0) whose right side lies inside the region:
+// nxt = the first live token of the next non-empty chunk, NONE past the region's end.
+//
+// Three paths, cheapest first:
+//  1. a full chunk of hot tokens with no slot inside a run of >= 3: four unmasked LDS adds;
+//  2. any chunk with no such slot whose last token differs from nxt: masked adds, hot and cold;
+//     a partial chunk's last pair (last, nxt) is moved to lane 63's slot 3 (dead in a partial
+//     chunk), so no lane-dependent fix-up is needed;
+//  3. everything else (runs of >= 3, the region's first run, a partial chunk ending in an X X
+//     pair): exact run parity.
+template <int MODE>
+__device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
+                                            const Sink &k) {
+    const int len = w.len;
+    const bool full = len == CHUNK;
+    const int32_t r3 = from_next(w.t[0], nxt);
+    const int32_t r[4] = {w.t[1], w.t[2], w.t[3], r3};
+    // E[e]: slot e equals its right-hand neighbour (junk on dead slots: masked where it matters)
+    unsigned long long E[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == r[e]);
+    const unsigned long long b0 = s.prev == w.first ? 1ull : 0ull;
+    uint32_t oh[4], oc[4];
+    uint32_t acc = 0;
+    if (MODE == MODE_TABLE && full && !s.in_lead) {
+        // path 1
+        const uint32_t mx = max(max((uint32_t)w.t[0], (uint32_t)w.t[1]),
+                                max(max((uint32_t)w.t[2], (uint32_t)w.t[3]), (uint32_t)r3));
+        const unsigned long long Em1 = (E[3] << 1) | b0;
+        const unsigned long long trip = (E[0] & (Em1 | E[1])) | (E[2] & (E[1] | E[3]));
+        if ((__ballot(mx >= (uint32_t)HOT) | trip) == 0ull) {
+            const unsigned long long all[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+            add_hot<false>(w.t, r, all, oh, acc, k);
+            if (__ballot((acc & 0x40004000u) != 0u) != 0ull) {
+                const unsigned long long none[4] = {0, 0, 0, 0};
+                fix_all(w.t, r, all, none, oh, oc, k);
+            }
+            if (s.n_live == 0) s.first_tok = w.first;
+            s.par = (w.last == nxt) ? (int)((E[2] >> 63) & 1ull) : 0;
+            s.prev = w.last;
+            s.n_live += len;
+            return;
+        }
+    }
+    if ((full || w.last != nxt) && !s.in_lead) {
+        // path 2: valid pairs have t | r >= 0; hot ones t | r < HOT (unsigned)
+        int32_t x[4] = {w.t[0], w.t[1], w.t[2], w.t[3]};
+        if (!full) x[3] = lane_in(1ull << 63) ? w.last : x[3];
+        uint32_t u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = (uint32_t)(x[e] | r[e]);
+        unsigned long long H[4], Cd[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) H[e] = __ballot(u[e] < (uint32_t)HOT);
+        const int32_t umax = max(max((int32_t)u[0], (int32_t)u[1]), max((int32_t)u[2], (int32_t)u[3]));
+        const bool any_cold = __ballot(umax >= HOT) != 0ull;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cd[e] = any_cold ? __ballot((int32_t)u[e] >= HOT) : 0ull;
+        // an X X pair needs both slots live: valid pairs only (lane 63's moved pair is no X X
+        // pair of the chunk: last != nxt on this path)
+        unsigned long long V[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) V[e] = E[e] & (H[e] | Cd[e]);
+        if (!full) V[3] &= ~(1ull << 63);
+        const unsigned long long Em1 = (V[3] << 1) | b0;
+        const unsigned long long trip = (V[0] & (Em1 | V[1])) | (V[2] & (V[1] | V[3]));
+        if (trip == 0ull) {
+            if (MODE == MODE_TABLE) {
+                add_hot<true>(x, r, H, oh, acc, k);
+                if (any_cold) add_cold(x, r, Cd, oc, acc, k);
+                if (__ballot((acc & 0x40004000u) != 0u) != 0ull) fix_all(x, r, H, Cd, oh, oc, k);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (lane_in(Cd[e])) count_pair<MODE>(k, x[e], r[e]);
+            }
+            if (s.n_live == 0) s.first_tok = w.first;
+            // the parity of the last token only matters when the next chunk continues its run
+            s.par = (full && w.last == nxt) ? (int)((V[2] >> 63) & 1ull) : 0;
+            s.prev = w.last;
+            s.n_live += len;
+            return;
+        }
+    }
+    // path 3: exact
+    const int kl = len - 1, ll = kl >> 2, el = kl & 3;
+    int32_t rr[4] = {r[0], r[1], r[2], r[3]};
+    if (!full) {
+        const bool me = lane_in(1ull << ll);
+        switch (el) {
+        case 0: rr[0] = me ? nxt : rr[0]; break;
+        case 1: rr[1] = me ? nxt : rr[1]; break;
+        case 2: rr[2] = me ? nxt : rr[2]; break;
+        default: rr[3] = me ? nxt : rr[3]; break;
+        }
+    }
+    int par[4];
+    bool start[4];
+    run_parity(w.t, len, s.prev, s.par, lane, par, start);
+    bool cnt[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const bool valid = (w.t[e] | rr[e]) >= 0 && 4 * lane + e < len;
+        cnt[e] = valid && !(w.t[e] == rr[e] && par[e]);
+    }
+    const int par_last = bcast(pick4(par, el), ll);
+    if (s.in_lead) {
+        // the first run ends at the first run start at region position >= 1
+        int f = len;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const unsigned long long m = __ballot(start[e] && (s.n_live + 4 * lane + e) > 0);
+            if (m) {
+                const int q = 4 * __builtin_ctzll(m) + e;
+                f = q < f ? q : f;
+            }
+        }
+        if (f < len) {
+            s.lead_len = s.n_live + f;
+            s.in_lead = false;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (cnt[e]) count_pair<MODE>(k, w.t[e], rr[e]);
+    if (s.n_live == 0) s.first_tok = w.first;
+    s.prev = w.last;
     s.par = par_last;
     s.n_live += len;
 }
@@ -587,43 +729,58 @@ struct Apply {
 // (the only kind whose matches depend on run parity, so the only one carrying that code).
 enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
 
-// Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region:
-// nxt = the first pre-merge live token after it (the next region's first for the last chunk).
-// A touched chunk is re-packed and written back; w becomes the post-merge chunk (possibly empty).
+// Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
+// in place: nxt = the first pre-merge live token after it (the next region's first for the last
+// chunk).  A touched chunk is re-packed and written back.  The common case (no match) is eight
+// compares and a handful of mask operations.
 template <int MERGE>
-__device__ __forceinline__ void apply_chunk(View &w, int32_t nxt, int32_t ma, int32_t mb,
+__device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, int32_t mb,
                                             int32_t mc, const __amdgpu_buffer_rsrc_t rs, int c,
                                             int lane, Apply &ap) {
-    int32_t r[4];
-    right_of(w.t, nxt, r);
     if (!ap.started) {
         ap.started = true;
-        ap.match = ap.prev == ma && bcast(w.t[0], 0) == mb && (MERGE == MERGE_XY || ap.par == 0);
+        ap.match = ap.prev == ma && w.first == mb && (MERGE == MERGE_XY || ap.par == 0);
     }
-    bool m[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = (w.t[e] == ma) & (r[e] == mb);
-    const int kl = w.len - 1;
-    const int32_t t_last = bcast(pick4(w.t, kl & 3), kl >> 2);
+    // M[e]: slot e is `a` and its in-register right-hand neighbour is `b`
+    const unsigned long long A0 = __ballot(w.t[0] == ma), A1 = __ballot(w.t[1] == ma),
+                             A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
+    const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
+                             B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
+    unsigned long long M[4] = {A0 & B1, A1 & B2, A2 & B3,
+                               A3 & ((B0 >> 1) | (nxt == mb ? (1ull << 63) : 0ull))};
+    // the last live slot's neighbour is nxt (for a full chunk that bit is already in M[3])
+    bool m_last = w.last == ma && nxt == mb;
     int par_last = 0;
     if (MERGE == MERGE_XX) {
         // only even run offsets match (core.ts:285-290 == replaceAll's leftmost rule); the
         // parity is carried only while the chunk ends in `a`
-        if (__ballot(m[0] | m[1] | m[2] | m[3]) != 0ull || t_last == ma) {
+        if ((M[0] | M[1] | M[2] | M[3]) != 0ull || w.last == ma) {
+            const int kl = w.len - 1;
             int par[4];
-            run_parity(w.t, w.len, ap.prev, ap.par, lane, par);
+            bool start[4];
+            run_parity(w.t, w.len, ap.prev, ap.par, lane, par, start);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) m[e] = m[e] && par[e] == 0;
+            for (int e = 0; e < 4; ++e) M[e] &= __ballot(par[e] == 0);
             par_last = bcast(pick4(par, kl & 3), kl >> 2);
+            m_last = m_last && par_last == 0;
         }
     }
-    const unsigned long long M0 = __ballot(m[0]), M1 = __ballot(m[1]), M2 = __ballot(m[2]),
-                             M3 = __ballot(m[3]);
-    const int el = kl & 3;
-    const unsigned long long ML = el == 0 ? M0 : el == 1 ? M1 : el == 2 ? M2 : M3;
-    const bool m_last = ((ML >> (kl >> 2)) & 1ull) != 0;
-    if (ap.match || (M0 | M1 | M2 | M3) != 0ull) {
-        const bool up = from_prev((int)m[3], (int)ap.match) != 0;
+    const int32_t t_last = w.last;
+    if (ap.match || m_last || (M[0] | M[1] | M[2] | M[3]) != 0ull) {
+        const int kl = w.len - 1;
+        if (m_last) {
+            const unsigned long long bit = 1ull << (kl >> 2);
+            switch (kl & 3) {
+            case 0: M[0] |= bit; break;
+            case 1: M[1] |= bit; break;
+            case 2: M[2] |= bit; break;
+            default: M[3] |= bit; break;
+            }
+        }
+        bool m[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = lane_in(M[e]);
+        const bool up = lane_in((M[3] << 1) | (ap.match ? 1ull : 0ull));
         const int l4 = 4 * lane;
         bool keep[4];
         keep[0] = (l4 < w.len) & !up;
@@ -638,10 +795,12 @@ __device__ __forceinline__ void apply_chunk(View &w, int32_t nxt, int32_t ma, in
             __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
                                make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
             rs, lane * 16 + c * (CHUNK * 4), 0, 0);
-        ap.n_match += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+        ap.n_match += __popcll(M[0]) + __popcll(M[1]) + __popcll(M[2]) + __popcll(M[3]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) w.t[e] = y[e];
         w.len = total;
+        w.first = total ? bcast(y[0], 0) : TOMB;
+        w.last = total ? slot_at(w.t, total - 1) : NONE;
     }
     ap.prev = t_last;
     ap.par = par_last;
@@ -674,6 +833,7 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     if (r < R) {
         const int64_t c0 = (int64_t)r * cpr;
         const int64_t c1 = min(c0 + cpr, n_chunks);
+        const int nc = (int)(c1 > c0 ? c1 - c0 : 0);
         const RegionCarry rc = carry[r];
         Tally s;
         s.n_live = 0;
@@ -688,63 +848,75 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
         ap.match = false;
         ap.started = false;
         ap.n_match = 0;
-        View P, H;           // P: post-merge chunk awaiting its count; H: pre-merge chunk awaiting
-        P.len = H.len = 0;   //    its apply (merge passes only)
-        int hc = 0;
         // the region through a range-checked buffer descriptor (loads past its end return 0 and
         // are never consumed)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            ids + c0 * CHUNK, 0, (int)(c1 > c0 ? (c1 - c0) * CHUNK * 4 : 0), 0x00020000);
-        // stage 2 input: the next non-empty post-merge chunk in stream order
-        auto feed = [&](const View &q) {
-            if (P.len) count_chunk<MODE>(P.t, P.len, bcast(q.t[0], 0), lane, s, k);
-            P = q;
+            ids + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
+        const int lo = lane * 16;
+        auto load = [&](Chunk &q, int c) {
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + c * (CHUNK * 4), 0, 0);
+            q.t[0] = (int)x[0];
+            q.t[1] = (int)x[1];
+            q.t[2] = (int)x[2];
+            q.t[3] = (int)x[3];
         };
-        auto stage = [&](const int4 v, int c) {
-            const View q = make_view(v);
-            if (q.len == 0) return;
-            if (MERGE) {
-                if (H.len) {
-                    apply_chunk<MERGE>(H, bcast(q.t[0], 0), ma, mb, mc, rs, hc, lane, ap);
-                    if (H.len) feed(H);
-                }
-                H = q;
-                hc = c;
+        // first pre-merge live token after chunk c (whose successor's slot 0 is f1)
+        auto next_pre = [&](int c, int32_t f1) -> int32_t {
+            if (c + 1 >= nc) return rc.next_tok;
+            int32_t v = f1;
+            for (int q = c + 2; q < nc && v == TOMB; ++q)
+                v = __builtin_amdgcn_readfirstlane(
+                    (int)__builtin_amdgcn_raw_buffer_load_b32(rs, q * (CHUNK * 4), 0, 0));
+            return v == TOMB ? rc.next_tok : v;
+        };
+        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, int c) {
+            finish_load(cur);
+            if (MERGE && cur.len)
+                apply_chunk<MERGE>(cur, next_pre(c, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs, c,
+                                   lane, ap);
+            if (cur.len) {
+                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k);
             } else {
-                feed(q);
+                cur = prv;   // rare: hand the pending chunk on
             }
+            load(prv, c + 5);
+            prv.len = 0;
         };
-        if (c0 < c1) {
-            const int lo = lane * 16;
-            const int nc = (int)(c1 - c0);
-            auto load = [&](int c) -> int4 {
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + c * (CHUNK * 4), 0, 0);
-                return make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
-            };
-            // 4-deep ring, unrolled by its depth so no register rotation waits on a load
-            int4 q0 = load(0), q1 = load(1), q2 = load(2), q3 = load(3);
-#define BPE_STAGE(QC, CC)                                                                       \
-    {                                                                                           \
-        const int4 v_ = QC;                                                                     \
-        QC = load((CC) + 4);                                                                    \
-        stage(v_, (CC));                                                                        \
-    }
-            for (int c = 0; c < nc; c += 4) {
-                BPE_STAGE(q0, c)
-                if (c + 1 >= nc) break;
-                BPE_STAGE(q1, c + 1)
-                if (c + 2 >= nc) break;
-                BPE_STAGE(q2, c + 2)
-                if (c + 3 >= nc) break;
-                BPE_STAGE(q3, c + 3)
+        if (nc > 0) {
+            Chunk S0, S1, S2, S3, S4, S5;
+            load(S0, 0);
+            load(S1, 1);
+            load(S2, 2);
+            load(S3, 3);
+            load(S4, 4);
+            S5.len = 0;
+            int c = 0;
+            for (;;) {
+                stage(S0, S1, S5, c);
+                if (++c >= nc) break;
+                stage(S1, S2, S0, c);
+                if (++c >= nc) break;
+                stage(S2, S3, S1, c);
+                if (++c >= nc) break;
+                stage(S3, S4, S2, c);
+                if (++c >= nc) break;
+                stage(S4, S5, S3, c);
+                if (++c >= nc) break;
+                stage(S5, S0, S4, c);
+                if (++c >= nc) break;
             }
-#undef BPE_STAGE
+            // the pending chunk sits in the slot of the last stage
+            Chunk F;
+            switch ((nc - 1) % 6) {
+            case 0: F = S0; break;
+            case 1: F = S1; break;
+            case 2: F = S2; break;
+            case 3: F = S3; break;
+            case 4: F = S4; break;
+            default: F = S5; break;
+            }
+            if (F.len) count_chunk<MODE>(F, NONE, lane, s, k);
         }
-        if (MERGE && H.len) {
-            apply_chunk<MERGE>(H, rc.next_tok, ma, mb, mc, rs, hc, lane, ap);
-            if (H.len) feed(H);
-        }
-        if (P.len) count_chunk<MODE>(P.t, P.len, NONE, lane, s, k);
         if (lane == 0) {
             RegionSum o;
             o.n_live = s.n_live;
@@ -884,7 +1056,10 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) sum += s_sum[q][bl][bi];
-    const int bin = 2 * (blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * bl) + bi;
+    // hot dword w holds pairs ((w & 127) * 2 + half, w >> 7); sketch dwords hold buckets in order
+    const int wi = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * bl + (bi >> 1);
+    const int hf = bi & 1;
+    const int bin = wi < HOT_BINS / 2 ? (((((wi & 127) << 1) | hf) << 8) | (wi >> 7)) : 2 * wi + hf;
     const unsigned long long v = (unsigned long long)sum + spill[bin];
     table[bin] = v;
     spill[bin] = 0;
