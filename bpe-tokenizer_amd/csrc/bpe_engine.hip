@@ -159,6 +159,10 @@ int seal_packed(bpe_ctx *c) {
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + c->live_slots), TOMB,
                                   end - c->live_slots, c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + end), SEP, CHUNK, c->stream));
+    if (end > c->live_slots) {
+        k_seal<<<1, 1, 0, c->stream>>>(c->d_ids, c->live_slots);
+        HIP_TRY(hipGetLastError());
+    }
     c->packed = true;
     c->counts_valid = c->carry_valid = false;
     geometry(c);
@@ -841,7 +845,7 @@ int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *samp
     sample_off[0] = 0;
     for (int64_t i = 0; i < slots; ++i) {
         const int32_t v = buf[i];
-        if (v == TOMB) continue;
+        if (v < SEP) continue;   // dead slot (TOMB or a tail tag)
         if (v == SEP) {
             if (sidx >= c->n_samples) return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
             sample_off[++sidx] = o;

@@ -26,6 +26,10 @@ namespace bpe {
 constexpr int32_t SEP = -1;                 // sample separator (live slot, never in a pair)
 constexpr int32_t TOMB = -2;                // dead slot in a chunk tail
 constexpr int32_t NONE = -3;                // "no token" (register sentinel only)
+// Tail tags of a partial chunk (every stored value < SEP is a dead slot): slot 255 holds
+// LEN_TAG - len; slot 254, when dead, holds LAST_TAG - (the last live token), else TOMB.
+constexpr int32_t LEN_TAG = -16;
+constexpr int32_t LAST_TAG = -1000;
 constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x int4)
 #ifndef BPE_WAVES
 #define BPE_WAVES 16
@@ -37,7 +41,6 @@ constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
 constexpr int HOT = 256;                    // ids < HOT form the dense LDS histogram
 constexpr int HOT_BINS = HOT * HOT;
 constexpr int SKETCH_BINS = 16384;          // count sketch of the cold pairs (an id >= HOT)
-constexpr int SKETCH_SHIFT = 18;            // bucket = (key * golden) >> SKETCH_SHIFT
 constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, then the sketch
 constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword: 160 KiB, all of it
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
@@ -159,7 +162,7 @@ __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
     // (HIP's __umul24 returns int: the sum must be shifted as unsigned)
     const uint32_t h = (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) +
                        (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
-    const uint32_t cold = HOT_BINS + (h >> SKETCH_SHIFT);
+    const uint32_t cold = HOT_BINS + (((h >> 19) << 1) | ((uint32_t)x & 1u));
     return ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT ? (int)hot : (int)cold;
 }
 
@@ -194,7 +197,9 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
 //  - hot pair (x, y), both < 256: dword (y << 7) | (x >> 1), half x & 1, i.e. byte address
 //    ((x << 1) & 0x1FC) | (y << 9) and increment 1 << ((x << 4) & 16): five VALU operations, the
 //    half chosen by a bit the shift amount already carries;
-//  - sketch bucket b of a cold pair: dword HOT_BINS / 2 + (b >> 1), half b & 1.
+//  - sketch bucket b of a cold pair: dword HOT_BINS / 2 + (b >> 1), half b & 1, with
+//    b = ((hash >> 19) << 1) | (x & 1): the dword from the hash, the half from x, so both
+//    classes share the increment.
 // A counter reaching 0x8000 spills 0x8000 to the global u64 table (indexed by table_index):
 // exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom absorbs
 // every add that lands before its subtraction (a CU issues far fewer in flight), so no field
@@ -214,9 +219,12 @@ __device__ __forceinline__ uint32_t sketch_hash(int32_t x, int32_t y) {
     return (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) + (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
 }
 
-// bucket h >> 18: dword HOT_BINS / 2 + (h >> 19), half (h >> 18) & 1
+// sketch dword HOT_BINS / 2 + (h >> 19)
 __device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | ((h >> 17) & 0x7FFCu); }
-__device__ __forceinline__ uint32_t cold_inc(uint32_t h) { return 1u << ((h >> 14) & 16u); }
+
+__device__ __forceinline__ uint32_t sketch_bucket(int32_t x, int32_t y) {
+    return ((sketch_hash(x, y) >> 19) << 1) | ((uint32_t)x & 1u);
+}
 
 __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
     return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + addr);
@@ -245,10 +253,9 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) 
             inc = hot_inc(x);
             bin = ((uint32_t)x << 8) | (uint32_t)y;
         } else {
-            const uint32_t h = sketch_hash(x, y);
-            addr = cold_addr(h);
-            inc = cold_inc(h);
-            bin = HOT_BINS + (h >> SKETCH_SHIFT);
+            addr = cold_addr(sketch_hash(x, y));
+            inc = hot_inc(x);
+            bin = HOT_BINS + sketch_bucket(x, y);
         }
         lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
     } else if (exact_wanted<MODE>(k, x, y)) {
@@ -271,19 +278,24 @@ __device__ __forceinline__ View make_view(const int4 v) {
     w.t[2] = v.z;
     w.t[3] = v.w;
     // chunks are left-packed, so len = number of non-TOMB slots (256 iff the last slot is live)
-    if (__builtin_amdgcn_readlane(v.w, 63) != TOMB) {
+    if (__builtin_amdgcn_readlane(v.w, 63) >= SEP) {
         w.len = CHUNK;
     } else {
-        w.len = __popcll(__ballot(v.x != TOMB)) + __popcll(__ballot(v.y != TOMB)) +
-                __popcll(__ballot(v.z != TOMB)) + __popcll(__ballot(v.w != TOMB));
+        w.len = LEN_TAG - __builtin_amdgcn_readlane(v.w, 63);
     }
     return w;
 }
 
 template <typename T>
 __device__ __forceinline__ T pick4(const T (&a)[4], int e) {
-    return e == 0 ? a[0] : e == 1 ? a[1] : e == 2 ? a[2] : a[3];
+    const T a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+    return e == 0 ? a0 : e == 1 ? a1 : e == 2 ? a2 : a3;
 }
+
+// c ? a : b on values (a conditional over two lvalues compiles to a select of their addresses,
+// which pins arrays and structs in registers to scratch)
+template <typename T>
+__device__ __forceinline__ T sel(bool c, T a, T b) { return c ? a : b; }
 
 // Broadcast of lane `src` (wave-uniform) through v_readlane.
 __device__ __forceinline__ int32_t bcast(int32_t v, int src) {
@@ -317,9 +329,9 @@ __device__ __forceinline__ void neighbours(const View &w, int32_t prev, int32_t 
     for (int e = 0; e < 4; ++e) {
         const int k = 4 * lane + e;
         n.live[e] = k < w.len;
-        const int32_t right = e < 3 ? w.t[e + 1] : dn;
+        const int32_t right = sel(e < 3, w.t[e < 3 ? e + 1 : 0], dn);
         n.partner[e] = (k + 1 < w.len) ? right : nxt;
-        const int32_t left = e == 0 ? pm : w.t[e - 1];
+        const int32_t left = sel(e == 0, pm, w.t[e > 0 ? e - 1 : 0]);
         n.eqp[e] = n.live[e] && w.t[e] >= 0 && w.t[e] == left;
         n.eqn[e] = n.live[e] && w.t[e] >= 0 && w.t[e] == n.partner[e];
     }
@@ -343,7 +355,7 @@ __device__ __forceinline__ void run_starts(const Nbr &n, int lane, int rs[4]) {
     int excl = __shfl_up(incl, 1);
     if (lane == 0) excl = -1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) rs[e] = rs[e] > excl ? rs[e] : excl;
+    for (int e = 0; e < 4; ++e) rs[e] = max(rs[e], excl);
 }
 
 // Exact run offsets of the live slots (needed where X X pairs are matched / located exactly).
@@ -413,7 +425,7 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t x = __shfl_down(pk[e], dl);
-                nb[e] = lane < 64 - dl ? x : 0u;
+                nb[e] = sel(lane < 64 - dl, x, 0u);
             }
         }
         const uint32_t bit = (uint32_t)sh << 17;
@@ -421,12 +433,12 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
         for (int e = 0; e < 4; ++e) {
             const bool mv = (nb[e] & KEPT) && (nb[e] & bit);
             const bool stay = (pk[e] & KEPT) && !(pk[e] & bit);
-            pk[e] = mv ? nb[e] : stay ? pk[e] : 0u;
+            pk[e] = sel(mv, nb[e], sel(stay, pk[e], 0u));
         }
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        val[e] = 4 * lane < total - e ? (int32_t)(pk[e] & 0x1FFFFu) - 1 : TOMB;
+        val[e] = sel(4 * lane < total - e, (int32_t)(pk[e] & 0x1FFFFu) - 1, TOMB);
     return total;
 }
 
@@ -458,7 +470,7 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
 struct Chunk {
     int32_t t[4];
     int len;         // live slots (left-packed)
-    int32_t first;   // slot 0 (TOMB when empty)
+    int32_t first;   // slot 0 (dead when empty)
     int32_t last;    // last live slot (NONE when empty)
 };
 
@@ -473,27 +485,21 @@ __device__ __forceinline__ int32_t slot_at(const int32_t (&t)[4], int k) {
     }
 }
 
-// Lanes whose plane-e slot 4*lane + e lies below n.
-__device__ __forceinline__ unsigned long long lanes_below(int n, int e) {
-    const int m = (n - e + 3) >> 2;
-    return m >= 64 ? ~0ull : m <= 0 ? 0ull : ((1ull << m) - 1ull);
-}
-
 __device__ __forceinline__ bool lane_in(unsigned long long m) {
     return __builtin_amdgcn_inverse_ballot_w64(m);
 }
 
-// Wave-uniform facts of a freshly loaded chunk.
+// Wave-uniform facts of a freshly loaded chunk, from its tail (see LEN_TAG / LAST_TAG).
 __device__ __forceinline__ void finish_load(Chunk &c) {
     c.first = bcast(c.t[0], 0);
     const int32_t l3 = bcast(c.t[3], 63);
-    if (l3 != TOMB) {
+    if (l3 >= SEP) {
         c.len = CHUNK;
         c.last = l3;
     } else {
-        c.len = __popcll(__ballot(c.t[0] != TOMB)) + __popcll(__ballot(c.t[1] != TOMB)) +
-                __popcll(__ballot(c.t[2] != TOMB)) + __popcll(__ballot(c.t[3] != TOMB));
-        c.last = c.len ? slot_at(c.t, c.len - 1) : NONE;
+        c.len = LEN_TAG - l3;
+        const int32_t l2 = bcast(c.t[2], 63);
+        c.last = c.len == CHUNK - 1 ? l2 : c.len ? LAST_TAG - l2 : NONE;
     }
 }
 
@@ -508,7 +514,7 @@ __device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int k = 4 * lane + e;
-        const int32_t left = e == 0 ? l0 : t[e - 1];
+        const int32_t left = sel(e == 0, l0, t[e > 0 ? e - 1 : 0]);
         start[e] = k < len && !(t[e] >= 0 && t[e] == left);
         if (start[e]) lmax = k;
         rs[e] = lmax;
@@ -524,63 +530,59 @@ __device__ __forceinline__ void run_parity(const int32_t (&t)[4], int len, int32
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int k = 4 * lane + e;
-        const int s = rs[e] > excl ? rs[e] : excl;
+        const int s = max(rs[e], excl);
         par[e] = s >= 0 ? ((k - s) & 1) : ((prev_par + 1 + k) & 1);
     }
 }
 
 // Count-side state of one region (wave-uniform).
 struct Tally {
-    int64_t n_live;      // live slots counted so far
-    int64_t lead_len;    // length of the region's first run (once it has ended)
+    int32_t n_live;      // live slots counted so far
+    int32_t lead_len;    // length of the region's first run (once it has ended)
     int32_t prev;        // last live token counted (NONE before the first)
     int32_t par;         // run-offset parity of prev (the first run counts from the region start)
     int32_t first_tok;   // the region's first live token
-    bool in_lead;        // every live token so far belongs to the region's first run
+    int32_t in_lead;     // every live token so far belongs to the region's first run
 };
 
-// Hot pairs (t[e], r[e]) of lanes in `m` (all lanes when m is ~0): LDS adds with the overflow
-// screen; returns the OR of the returned words (the caller screens) in acc.
-template <bool MASKED>
-__device__ __forceinline__ void add_hot(const int32_t (&x)[4], const int32_t (&y)[4],
-                                        const unsigned long long (&m)[4], uint32_t (&o)[4],
-                                        uint32_t &acc, const Sink &k) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        if (!MASKED || lane_in(m[e])) {
-            o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
-            acc |= o[e];
-        }
-    }
+// LDS adds of one chunk's pairs (x[e], y[e]), then the overflow screen.  Per pair: the hot
+// address (three operations), the increment (two, shared by both classes: a sketch bucket's
+// half is also x & 1), and, when the chunk has cold pairs, the sketch address (four) and a
+// select.  Pairs that do not count add 0; their address stays inside the table.
+template <bool COLD>
+__device__ __forceinline__ uint32_t pair_addr(int32_t x, int32_t y) {
+    uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | (((uint32_t)y << 9) & 0x1FE00u);
+    if (COLD) a = ((uint32_t)(x | y) < (uint32_t)HOT) ? a : cold_addr(sketch_hash(x, y));
+    return a;
 }
 
-// Cold pairs of lanes in `m`: sketch buckets.
-__device__ __forceinline__ void add_cold(const int32_t (&x)[4], const int32_t (&y)[4],
-                                         const unsigned long long (&m)[4], uint32_t (&o)[4],
-                                         uint32_t &acc, const Sink &k) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        if (lane_in(m[e])) {
-            const uint32_t h = sketch_hash(x[e], y[e]);
-            o[e] = atomicAdd(lds_word(k, cold_addr(h)), cold_inc(h));
-            acc |= o[e];
-        }
-    }
+template <bool COLD>
+__device__ __forceinline__ uint32_t pair_inc(int32_t x, int32_t y) {
+    const uint32_t u = (uint32_t)(x | y);
+    return (COLD ? (int32_t)u >= 0 : u < (uint32_t)HOT) ? hot_inc(x) : 0u;
 }
 
-// Exact spill check after a screen hit (rare).
-__device__ __forceinline__ void fix_all(const int32_t (&x)[4], const int32_t (&y)[4],
-                                        const unsigned long long (&H)[4],
-                                        const unsigned long long (&Cd)[4], const uint32_t (&oh)[4],
-                                        const uint32_t (&oc)[4], const Sink &k) {
+template <bool COLD>
+__device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
+                                          const Sink &k) {
+    uint32_t o[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        if (lane_in(H[e]))
-            lds_fix(k, hot_addr(x[e], y[e]), hot_inc(x[e]), ((uint32_t)x[e] << 8) | (uint32_t)y[e],
-                    oh[e]);
-        if (lane_in(Cd[e])) {
-            const uint32_t h = sketch_hash(x[e], y[e]);
-            lds_fix(k, cold_addr(h), cold_inc(h), HOT_BINS + (h >> SKETCH_SHIFT), oc[e]);
+    for (int e = 0; e < 4; ++e)
+        o[e] = atomicAdd(lds_word(k, pair_addr<COLD>(x[e], y[e])), pair_inc<COLD>(x[e], y[e]));
+    // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
+    if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            // recomputed here (rare) rather than kept live across the adds
+            int32_t xx = x[e], yy = y[e];
+            asm volatile("" : "+v"(xx), "+v"(yy));
+            const uint32_t inc = pair_inc<COLD>(xx, yy);
+            if (inc) {
+                const bool hot = (uint32_t)(xx | yy) < (uint32_t)HOT;
+                const uint32_t bin = hot ? (((uint32_t)xx << 8) | (uint32_t)yy)
+                                         : HOT_BINS + sketch_bucket(xx, yy);
+                lds_fix(k, pair_addr<COLD>(xx, yy), inc, bin, o[e]);
+            }
         }
     }
 }
@@ -588,39 +590,38 @@ __device__ __forceinline__ void fix_all(const int32_t (&x)[4], const int32_t (&y
 // Counts the pairs of one post-merge chunk (len > 0) whose right side lies inside the region:
 // nxt = the first live token of the next non-empty chunk, NONE past the region's end.
 //
-// Three paths, cheapest first:
-//  1. a full chunk of hot tokens with no slot inside a run of >= 3: four unmasked LDS adds;
-//  2. any chunk with no such slot whose last token differs from nxt: masked adds, hot and cold;
-//     a partial chunk's last pair (last, nxt) is moved to lane 63's slot 3 (dead in a partial
-//     chunk), so no lane-dependent fix-up is needed;
-//  3. everything else (runs of >= 3, the region's first run, a partial chunk ending in an X X
-//     pair): exact run parity.
+// Fast path: no slot inside a run of >= 3 and, for a partial chunk, a last token that differs
+// from nxt.  A partial chunk's last pair (last, nxt) is moved to lane 63's slot 3 (dead in a
+// partial chunk), so no lane-dependent fix-up is needed.  Everything else (runs of >= 3, the
+// region's first run, a partial chunk ending in an X X pair) takes the exact path.
 template <int MODE>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k) {
     const int len = w.len;
     const bool full = len == CHUNK;
     const int32_t r3 = from_next(w.t[0], nxt);
-    const int32_t r[4] = {w.t[1], w.t[2], w.t[3], r3};
-    // E[e]: slot e equals its right-hand neighbour (junk on dead slots: masked where it matters)
-    unsigned long long E[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == r[e]);
-    const unsigned long long b0 = s.prev == w.first ? 1ull : 0ull;
-    uint32_t oh[4], oc[4];
-    uint32_t acc = 0;
     if (MODE == MODE_TABLE && full && !s.in_lead) {
-        // path 1
+        // a full chunk of hot tokens (no SEP, no dead slot) with no slot inside a run of >= 3:
+        // four unmasked adds
         const uint32_t mx = max(max((uint32_t)w.t[0], (uint32_t)w.t[1]),
                                 max(max((uint32_t)w.t[2], (uint32_t)w.t[3]), (uint32_t)r3));
-        const unsigned long long Em1 = (E[3] << 1) | b0;
+        const int32_t y[4] = {w.t[1], w.t[2], w.t[3], r3};
+        unsigned long long E[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == y[e]);
+        const unsigned long long Em1 = (E[3] << 1) | (s.prev == w.first ? 1ull : 0ull);
         const unsigned long long trip = (E[0] & (Em1 | E[1])) | (E[2] & (E[1] | E[3]));
         if ((__ballot(mx >= (uint32_t)HOT) | trip) == 0ull) {
-            const unsigned long long all[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-            add_hot<false>(w.t, r, all, oh, acc, k);
-            if (__ballot((acc & 0x40004000u) != 0u) != 0ull) {
-                const unsigned long long none[4] = {0, 0, 0, 0};
-                fix_all(w.t, r, all, none, oh, oc, k);
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = atomicAdd(lds_word(k, hot_addr(w.t[e], y[e])), hot_inc(w.t[e]));
+            if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    int32_t xx = w.t[e], yy = y[e];
+                    asm volatile("" : "+v"(xx), "+v"(yy));
+                    lds_fix(k, hot_addr(xx, yy), hot_inc(xx), ((uint32_t)xx << 8) | (uint32_t)yy, o[e]);
+                }
             }
             if (s.n_live == 0) s.first_tok = w.first;
             s.par = (w.last == nxt) ? (int)((E[2] >> 63) & 1ull) : 0;
@@ -629,56 +630,54 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             return;
         }
     }
-    if ((full || w.last != nxt) && !s.in_lead) {
-        // path 2: valid pairs have t | r >= 0; hot ones t | r < HOT (unsigned)
-        int32_t x[4] = {w.t[0], w.t[1], w.t[2], w.t[3]};
-        if (!full) x[3] = lane_in(1ull << 63) ? w.last : x[3];
-        uint32_t u[4];
+    if (!s.in_lead && (full || w.last != nxt)) {
+        // (values, not lvalues, in the conditional: a select of two lvalues becomes a select of
+        // their addresses, which pins the chunk registers to scratch)
+        const int32_t t3 = w.t[3], last = w.last;
+        const int32_t x3 = (!full && lane_in(1ull << 63)) ? last : t3;
+        const int32_t x[4] = {w.t[0], w.t[1], w.t[2], x3};
+        const int32_t y[4] = {w.t[1], w.t[2], w.t[3], r3};
+        // E[e]: slot e equals its right-hand neighbour; both live and not SEP
+        unsigned long long E[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = (uint32_t)(x[e] | r[e]);
-        unsigned long long H[4], Cd[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) H[e] = __ballot(u[e] < (uint32_t)HOT);
-        const int32_t umax = max(max((int32_t)u[0], (int32_t)u[1]), max((int32_t)u[2], (int32_t)u[3]));
-        const bool any_cold = __ballot(umax >= HOT) != 0ull;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Cd[e] = any_cold ? __ballot((int32_t)u[e] >= HOT) : 0ull;
-        // an X X pair needs both slots live: valid pairs only (lane 63's moved pair is no X X
-        // pair of the chunk: last != nxt on this path)
-        unsigned long long V[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) V[e] = E[e] & (H[e] | Cd[e]);
-        if (!full) V[3] &= ~(1ull << 63);
-        const unsigned long long Em1 = (V[3] << 1) | b0;
-        const unsigned long long trip = (V[0] & (Em1 | V[1])) | (V[2] & (V[1] | V[3]));
+        for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == y[e] && w.t[e] >= 0);
+        const unsigned long long Em1 = (E[3] << 1) | (s.prev == w.first ? 1ull : 0ull);
+        const unsigned long long trip = (E[0] & (Em1 | E[1])) | (E[2] & (E[1] | E[3]));
         if (trip == 0ull) {
+            // every X X pair starts its run, so every valid pair counts
             if (MODE == MODE_TABLE) {
-                add_hot<true>(x, r, H, oh, acc, k);
-                if (any_cold) add_cold(x, r, Cd, oc, acc, k);
-                if (__ballot((acc & 0x40004000u) != 0u) != 0ull) fix_all(x, r, H, Cd, oh, oc, k);
+                // any valid cold pair?  (t | r >= HOT as a signed value)
+                const int32_t smx = max(max((int32_t)((uint32_t)x[0] | (uint32_t)y[0]), (int32_t)((uint32_t)x[1] | (uint32_t)y[1])),
+                                        max((int32_t)((uint32_t)x[2] | (uint32_t)y[2]), (int32_t)((uint32_t)x[3] | (uint32_t)y[3])));
+                if (__ballot(smx >= HOT) == 0ull) add_pairs<false>(x, y, k);
+                else add_pairs<true>(x, y, k);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if (lane_in(Cd[e])) count_pair<MODE>(k, x[e], r[e]);
+                    if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
             }
             if (s.n_live == 0) s.first_tok = w.first;
             // the parity of the last token only matters when the next chunk continues its run
-            s.par = (full && w.last == nxt) ? (int)((V[2] >> 63) & 1ull) : 0;
+            s.par = (full && w.last == nxt) ? (int)((E[2] >> 63) & 1ull) : 0;
             s.prev = w.last;
             s.n_live += len;
             return;
         }
     }
-    // path 3: exact
+    // exact path
+#ifdef BPE_PROBE_COMMON
+    s.in_lead = 0;   // (static instruction-count probe only: drop the exact path)
+    return;
+#endif
     const int kl = len - 1, ll = kl >> 2, el = kl & 3;
-    int32_t rr[4] = {r[0], r[1], r[2], r[3]};
+    int32_t rr[4] = {w.t[1], w.t[2], w.t[3], r3};
     if (!full) {
         const bool me = lane_in(1ull << ll);
         switch (el) {
-        case 0: rr[0] = me ? nxt : rr[0]; break;
-        case 1: rr[1] = me ? nxt : rr[1]; break;
-        case 2: rr[2] = me ? nxt : rr[2]; break;
-        default: rr[3] = me ? nxt : rr[3]; break;
+        case 0: rr[0] = sel(me, nxt, rr[0]); break;
+        case 1: rr[1] = sel(me, nxt, rr[1]); break;
+        case 2: rr[2] = sel(me, nxt, rr[2]); break;
+        default: rr[3] = sel(me, nxt, rr[3]); break;
         }
     }
     int par[4];
@@ -704,7 +703,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
         }
         if (f < len) {
             s.lead_len = s.n_live + f;
-            s.in_lead = false;
+            s.in_lead = 0;
         }
     }
 #pragma unroll
@@ -718,16 +717,24 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
 
 // Apply-side state of one region (wave-uniform).
 struct Apply {
-    int32_t prev;                // last pre-merge live token before the chunk
-    int32_t par;                 // its run-offset parity (X X merges only)
-    bool match;                  // it is an `a` matched with the chunk's first live token
-    bool started;
-    unsigned long long n_match;
+    int32_t prev;        // last pre-merge live token before the chunk
+    int32_t par;         // its run-offset parity (X X merges only)
+    int32_t match;       // it is an `a` matched with the chunk's first live token
+    uint32_t n_match;
 };
 
 // What a k_step pass does before counting: nothing, a merge of two distinct ids, or an X X merge
 // (the only kind whose matches depend on run parity, so the only one carrying that code).
 enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
+
+// Writes the tail tags of a re-packed chunk (slots 254 and 255 live on lane 63).
+__device__ __forceinline__ void tag_tail(int32_t (&y)[4], int total, int32_t last) {
+    if (total < CHUNK) {
+        const bool l63 = lane_in(1ull << 63);
+        y[3] = sel(l63, LEN_TAG - total, y[3]);
+        if (total < CHUNK - 1) y[2] = sel(l63, total ? LAST_TAG - last : TOMB, y[2]);
+    }
+}
 
 // Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
 // in place: nxt = the first pre-merge live token after it (the next region's first for the last
@@ -737,19 +744,14 @@ template <int MERGE>
 __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, int32_t mb,
                                             int32_t mc, const __amdgpu_buffer_rsrc_t rs, int c,
                                             int lane, Apply &ap) {
-    if (!ap.started) {
-        ap.started = true;
-        ap.match = ap.prev == ma && w.first == mb && (MERGE == MERGE_XY || ap.par == 0);
-    }
     // M[e]: slot e is `a` and its in-register right-hand neighbour is `b`
     const unsigned long long A0 = __ballot(w.t[0] == ma), A1 = __ballot(w.t[1] == ma),
                              A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
     const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
                              B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
-    unsigned long long M[4] = {A0 & B1, A1 & B2, A2 & B3,
-                               A3 & ((B0 >> 1) | (nxt == mb ? (1ull << 63) : 0ull))};
-    // the last live slot's neighbour is nxt (for a full chunk that bit is already in M[3])
-    bool m_last = w.last == ma && nxt == mb;
+    unsigned long long M[4] = {A0 & B1, A1 & B2, A2 & B3, A3 & (B0 >> 1)};
+    // the last live slot's neighbour is nxt
+    int m_last = (w.last == ma) & (nxt == mb);
     int par_last = 0;
     if (MERGE == MERGE_XX) {
         // only even run offsets match (core.ts:285-290 == replaceAll's leftmost rule); the
@@ -762,11 +764,14 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
 #pragma unroll
             for (int e = 0; e < 4; ++e) M[e] &= __ballot(par[e] == 0);
             par_last = bcast(pick4(par, kl & 3), kl >> 2);
-            m_last = m_last && par_last == 0;
+            m_last &= par_last == 0;
         }
     }
     const int32_t t_last = w.last;
-    if (ap.match || m_last || (M[0] | M[1] | M[2] | M[3]) != 0ull) {
+    if ((ap.match | m_last) || (M[0] | M[1] | M[2] | M[3]) != 0ull) {
+#ifdef BPE_PROBE_COMMON
+        if (lane < 0) {   // (static instruction-count probe only: drop the rewrite)
+#endif
         const int kl = w.len - 1;
         if (m_last) {
             const unsigned long long bit = 1ull << (kl >> 2);
@@ -789,18 +794,23 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
         keep[3] = (l4 < w.len - 3) & !m[2];
         int32_t y[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = m[e] ? mc : w.t[e];
+        for (int e = 0; e < 4; ++e) y[e] = sel(m[e], mc, w.t[e]);
         const int total = compact_chunk(y, keep, w.len, lane);
+        const int32_t last = total ? slot_at(y, total - 1) : NONE;
+        w.first = total ? bcast(y[0], 0) : TOMB;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w.t[e] = y[e];
+        tag_tail(y, total, last);
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
                                make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
-            rs, lane * 16 + c * (CHUNK * 4), 0, 0);
-        ap.n_match += __popcll(M[0]) + __popcll(M[1]) + __popcll(M[2]) + __popcll(M[3]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w.t[e] = y[e];
+            rs, lane * 16, c * (CHUNK * 4), 0);
+        ap.n_match += (uint32_t)(__popcll(M[0]) + __popcll(M[1]) + __popcll(M[2]) + __popcll(M[3]));
         w.len = total;
-        w.first = total ? bcast(y[0], 0) : TOMB;
-        w.last = total ? slot_at(w.t, total - 1) : NONE;
+        w.last = last;
+#ifdef BPE_PROBE_COMMON
+        }
+#endif
     }
     ap.prev = t_last;
     ap.par = par_last;
@@ -841,12 +851,11 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
         s.prev = NONE;
         s.par = 0;
         s.first_tok = NONE;
-        s.in_lead = true;
+        s.in_lead = 1;
         Apply ap;
         ap.prev = rc.prev_tok;
         ap.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
-        ap.match = false;
-        ap.started = false;
+        ap.match = 0;
         ap.n_match = 0;
         // the region through a range-checked buffer descriptor (loads past its end return 0 and
         // are never consumed)
@@ -854,26 +863,34 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             ids + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
         const int lo = lane * 16;
         auto load = [&](Chunk &q, int c) {
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + c * (CHUNK * 4), 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
             q.t[0] = (int)x[0];
             q.t[1] = (int)x[1];
             q.t[2] = (int)x[2];
             q.t[3] = (int)x[3];
         };
-        // first pre-merge live token after chunk c (whose successor's slot 0 is f1)
-        auto next_pre = [&](int c, int32_t f1) -> int32_t {
-            if (c + 1 >= nc) return rc.next_tok;
-            int32_t v = f1;
-            for (int q = c + 2; q < nc && v == TOMB; ++q)
+        // first pre-merge live token at or after chunk c (whose slot 0 is f0)
+        auto live_from = [&](int c, int32_t f0) -> int32_t {
+            if (c >= nc) return rc.next_tok;
+            int32_t v = f0;
+            for (int q = c + 1; q < nc && v < SEP; ++q)
                 v = __builtin_amdgcn_readfirstlane(
-                    (int)__builtin_amdgcn_raw_buffer_load_b32(rs, q * (CHUNK * 4), 0, 0));
-            return v == TOMB ? rc.next_tok : v;
+                    (int)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, q * (CHUNK * 4), 0));
+            return v < SEP ? rc.next_tok : v;
         };
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, int c) {
-            finish_load(cur);
+            if (c < nc) {
+                finish_load(cur);
+            } else {
+                // past the region: an empty chunk hands the pending one on (every field stored on
+                // both sides, so the stores merge as values, not as a select of addresses)
+                cur.first = TOMB;
+                cur.len = 0;
+                cur.last = NONE;
+            }
             if (MERGE && cur.len)
-                apply_chunk<MERGE>(cur, next_pre(c, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs, c,
-                                   lane, ap);
+                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs,
+                                   c, lane, ap);
             if (cur.len) {
                 if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k);
             } else {
@@ -890,32 +907,22 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             load(S3, 3);
             load(S4, 4);
             S5.len = 0;
-            int c = 0;
-            for (;;) {
+            if (MERGE) {
+                // does the token before the region match the region's first live token?
+                const int32_t f = live_from(0, bcast(S0.t[0], 0));
+                ap.match = ap.prev == ma && f == mb && (MERGE == MERGE_XY || ap.par == 0);
+            }
+            // whole rounds of six stages; stages past the region see empty chunks, so the pending
+            // chunk always ends in S5
+            for (int c = 0; c < nc; c += 6) {
                 stage(S0, S1, S5, c);
-                if (++c >= nc) break;
-                stage(S1, S2, S0, c);
-                if (++c >= nc) break;
-                stage(S2, S3, S1, c);
-                if (++c >= nc) break;
-                stage(S3, S4, S2, c);
-                if (++c >= nc) break;
-                stage(S4, S5, S3, c);
-                if (++c >= nc) break;
-                stage(S5, S0, S4, c);
-                if (++c >= nc) break;
+                stage(S1, S2, S0, c + 1);
+                stage(S2, S3, S1, c + 2);
+                stage(S3, S4, S2, c + 3);
+                stage(S4, S5, S3, c + 4);
+                stage(S5, S0, S4, c + 5);
             }
-            // the pending chunk sits in the slot of the last stage
-            Chunk F;
-            switch ((nc - 1) % 6) {
-            case 0: F = S0; break;
-            case 1: F = S1; break;
-            case 2: F = S2; break;
-            case 3: F = S3; break;
-            case 4: F = S4; break;
-            default: F = S5; break;
-            }
-            if (F.len) count_chunk<MODE>(F, NONE, lane, s, k);
+            if (S5.len) count_chunk<MODE>(S5, NONE, lane, s, k);
         }
         if (lane == 0) {
             RegionSum o;
@@ -926,7 +933,7 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             o.lead_len = s.in_lead ? s.n_live : s.lead_len;
             o.trail_odd = s.par ^ 1;   // trail run length = offset of the last token + 1
             sums[r] = o;
-            if (MERGE && ap.n_match) atomicAdd(replaced, ap.n_match);
+            if (MERGE && ap.n_match) atomicAdd(replaced, (unsigned long long)ap.n_match);
         }
     }
     if (MODE == MODE_TABLE) {
@@ -1309,8 +1316,8 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         View w = make_view(v4[c * 64 + lane]);
         if (w.len == 0) continue;
         int32_t nxt = TOMB;
-        for (int64_t q = c + 1; q < c1 && nxt == TOMB; ++q) nxt = A.ids[q * CHUNK];
-        if (nxt == TOMB) nxt = rc.next_tok;
+        for (int64_t q = c + 1; q < c1 && nxt < SEP; ++q) nxt = A.ids[q * CHUNK];
+        if (nxt < SEP) nxt = rc.next_tok;
         Nbr n;
         neighbours(w, prev, nxt, lane, n);
         int64_t off[4];
@@ -1322,7 +1329,7 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
             for (int j = 0; j < A.n_cand; ++j) {
                 if (x == A.ca[j] && y == A.cb[j] && (x != y || (off[e] & 1) == 0)) {
                     const unsigned long long pos = (unsigned long long)(c * CHUNK + 4 * lane + e) + 1;
-                    last[j] = pos > last[j] ? pos : last[j];
+                    last[j] = max(pos, last[j]);
                 }
             }
         }
@@ -1386,6 +1393,15 @@ __global__ void __launch_bounds__(256) k_compact(const int32_t *__restrict__ ids
             if (4 * lane + e < w.len) out[o + 4 * lane + e] = w.t[e];
         o += w.len;
     }
+}
+
+// Tail tags of the last chunk after a dense write of live_slots slots (TOMB already filled).
+__global__ void k_seal(int32_t *__restrict__ ids, int64_t live_slots) {
+    const int len = (int)(live_slots % CHUNK);
+    if (len == 0) return;
+    int32_t *p = ids + (live_slots / CHUNK) * CHUNK;
+    p[CHUNK - 1] = LEN_TAG - len;
+    if (len < CHUNK - 1) p[CHUNK - 2] = LAST_TAG - p[len - 1];
 }
 
 // ---------------------------------------------------------------------------------------------
