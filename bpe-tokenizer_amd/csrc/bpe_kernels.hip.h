@@ -594,75 +594,75 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
 // from nxt.  A partial chunk's last pair (last, nxt) is moved to lane 63's slot 3 (dead in a
 // partial chunk), so no lane-dependent fix-up is needed.  Everything else (runs of >= 3, the
 // region's first run, a partial chunk ending in an X X pair) takes the exact path.
+//
+// Per-slot conditions are wave masks combined with 64-bit bitwise operations and uniform
+// conditions are integers: no short-circuit operators on the common path (they become control
+// flow whose booleans round-trip through vector registers).
 template <int MODE>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k) {
     const int len = w.len;
-    const bool full = len == CHUNK;
-    const int32_t r3 = from_next(w.t[0], nxt);
-    if (MODE == MODE_TABLE && full && !s.in_lead) {
-        // a full chunk of hot tokens (no SEP, no dead slot) with no slot inside a run of >= 3:
-        // four unmasked adds
-        const uint32_t mx = max(max((uint32_t)w.t[0], (uint32_t)w.t[1]),
-                                max(max((uint32_t)w.t[2], (uint32_t)w.t[3]), (uint32_t)r3));
-        const int32_t y[4] = {w.t[1], w.t[2], w.t[3], r3};
-        unsigned long long E[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == y[e]);
-        const unsigned long long Em1 = (E[3] << 1) | (s.prev == w.first ? 1ull : 0ull);
-        const unsigned long long trip = (E[0] & (Em1 | E[1])) | (E[2] & (E[1] | E[3]));
-        if ((__ballot(mx >= (uint32_t)HOT) | trip) == 0ull) {
-            uint32_t o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = atomicAdd(lds_word(k, hot_addr(w.t[e], y[e])), hot_inc(w.t[e]));
-            if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    int32_t xx = w.t[e], yy = y[e];
-                    asm volatile("" : "+v"(xx), "+v"(yy));
-                    lds_fix(k, hot_addr(xx, yy), hot_inc(xx), ((uint32_t)xx << 8) | (uint32_t)yy, o[e]);
-                }
-            }
-            if (s.n_live == 0) s.first_tok = w.first;
-            s.par = (w.last == nxt) ? (int)((E[2] >> 63) & 1ull) : 0;
-            s.prev = w.last;
-            s.n_live += len;
-            return;
-        }
+    const int full = len == CHUNK;
+    const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
+    const int32_t r3 = from_next(t0, nxt);
+    const int32_t l0 = from_prev(t3, s.prev);
+    // E*: slot equals its right-hand neighbour (Em1: slot 0 equals the token before it)
+    unsigned long long Em1 = __ballot(t0 == l0), E0 = __ballot(t0 == t1), E1 = __ballot(t1 == t2),
+                       E2 = __ballot(t2 == t3), E3 = __ballot(t3 == r3);
+    if (!full) {
+        // dead slots equal each other: keep live non-SEP slots only
+        const unsigned long long P0 = __ballot(t0 >= 0), P1 = __ballot(t1 >= 0),
+                                 P2 = __ballot(t2 >= 0), P3 = __ballot(t3 >= 0);
+        Em1 &= P0;
+        E0 &= P0;
+        E1 &= P1;
+        E2 &= P2;
+        E3 &= P3;
     }
-    if (!s.in_lead && (full || w.last != nxt)) {
-        // (values, not lvalues, in the conditional: a select of two lvalues becomes a select of
-        // their addresses, which pins the chunk registers to scratch)
-        const int32_t t3 = w.t[3], last = w.last;
-        const int32_t x3 = (!full && lane_in(1ull << 63)) ? last : t3;
-        const int32_t x[4] = {w.t[0], w.t[1], w.t[2], x3};
-        const int32_t y[4] = {w.t[1], w.t[2], w.t[3], r3};
-        // E[e]: slot e equals its right-hand neighbour; both live and not SEP
-        unsigned long long E[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) E[e] = __ballot(w.t[e] == y[e] && w.t[e] >= 0);
-        const unsigned long long Em1 = (E[3] << 1) | (s.prev == w.first ? 1ull : 0ull);
-        const unsigned long long trip = (E[0] & (Em1 | E[1])) | (E[2] & (E[1] | E[3]));
-        if (trip == 0ull) {
-            // every X X pair starts its run, so every valid pair counts
-            if (MODE == MODE_TABLE) {
-                // any valid cold pair?  (t | r >= HOT as a signed value)
-                const int32_t smx = max(max((int32_t)((uint32_t)x[0] | (uint32_t)y[0]), (int32_t)((uint32_t)x[1] | (uint32_t)y[1])),
-                                        max((int32_t)((uint32_t)x[2] | (uint32_t)y[2]), (int32_t)((uint32_t)x[3] | (uint32_t)y[3])));
-                if (__ballot(smx >= HOT) == 0ull) add_pairs<false>(x, y, k);
-                else add_pairs<true>(x, y, k);
-            } else {
+    const unsigned long long trip = (E0 & (Em1 | E1)) | (E2 & (E1 | E3));
+    const int fast = (trip == 0ull) & (s.in_lead == 0) & (full | (w.last != nxt));
+    if (fast) {
+        // every X X pair starts its run, so every valid pair counts
+        if (MODE == MODE_TABLE) {
+            const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1), max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
+            if (full & (__ballot(mx >= (uint32_t)HOT) == 0ull)) {
+                // hot tokens only, no SEP: unmasked adds
+                const int32_t x[4] = {t0, t1, t2, t3}, y[4] = {t1, t2, t3, r3};
+                uint32_t o[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
+                    o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
+                if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        int32_t xx = x[e], yy = y[e];
+                        asm volatile("" : "+v"(xx), "+v"(yy));
+                        lds_fix(k, hot_addr(xx, yy), hot_inc(xx), ((uint32_t)xx << 8) | (uint32_t)yy, o[e]);
+                    }
+                }
+            } else {
+                const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
+                const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
+                // any valid cold pair?  (x | y >= HOT as a signed value)
+                const int32_t smx = max(max((int32_t)(x[0] | y[0]), (int32_t)(x[1] | y[1])),
+                                        max((int32_t)(x[2] | y[2]), (int32_t)(x[3] | y[3])));
+                if (__ballot(smx >= HOT) == 0ull) add_pairs<false>(x, y, k);
+                else add_pairs<true>(x, y, k);
             }
-            if (s.n_live == 0) s.first_tok = w.first;
-            // the parity of the last token only matters when the next chunk continues its run
-            s.par = (full && w.last == nxt) ? (int)((E[2] >> 63) & 1ull) : 0;
-            s.prev = w.last;
-            s.n_live += len;
-            return;
+        } else {
+            const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
+            const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
         }
+        // the parity of the last token only matters when the next chunk continues its run
+        // (a full chunk's last slot: E2's lane-63 bit says it continues its left neighbour)
+        s.first_tok = s.n_live ? s.first_tok : w.first;
+        s.par = (int)((E2 >> 63) & (unsigned long long)(full & (w.last == nxt)));
+        s.prev = w.last;
+        s.n_live += len;
+        return;
     }
     // exact path
 #ifdef BPE_PROBE_COMMON
@@ -670,7 +670,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     return;
 #endif
     const int kl = len - 1, ll = kl >> 2, el = kl & 3;
-    int32_t rr[4] = {w.t[1], w.t[2], w.t[3], r3};
+    int32_t rr[4] = {t1, t2, t3, r3};
     if (!full) {
         const bool me = lane_in(1ull << ll);
         switch (el) {
@@ -686,8 +686,8 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     bool cnt[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        const bool valid = (w.t[e] | rr[e]) >= 0 && 4 * lane + e < len;
-        cnt[e] = valid && !(w.t[e] == rr[e] && par[e]);
+        const bool valid = ((w.t[e] | rr[e]) >= 0) & (4 * lane + e < len);
+        cnt[e] = valid & !((w.t[e] == rr[e]) & (par[e] != 0));
     }
     const int par_last = bcast(pick4(par, el), ll);
     if (s.in_lead) {
@@ -695,7 +695,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
         int f = len;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const unsigned long long m = __ballot(start[e] && (s.n_live + 4 * lane + e) > 0);
+            const unsigned long long m = __ballot(start[e] & ((s.n_live + 4 * lane + e) > 0));
             if (m) {
                 const int q = 4 * __builtin_ctzll(m) + e;
                 f = q < f ? q : f;
@@ -709,7 +709,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
 #pragma unroll
     for (int e = 0; e < 4; ++e)
         if (cnt[e]) count_pair<MODE>(k, w.t[e], rr[e]);
-    if (s.n_live == 0) s.first_tok = w.first;
+    s.first_tok = s.n_live ? s.first_tok : w.first;
     s.prev = w.last;
     s.par = par_last;
     s.n_live += len;
@@ -749,26 +749,28 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
                              A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
     const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
                              B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
-    unsigned long long M[4] = {A0 & B1, A1 & B2, A2 & B3, A3 & (B0 >> 1)};
+    unsigned long long M0 = A0 & B1, M1 = A1 & B2, M2 = A2 & B3, M3 = A3 & (B0 >> 1);
     // the last live slot's neighbour is nxt
-    int m_last = (w.last == ma) & (nxt == mb);
+    int m_last = ((uint32_t)(w.last ^ ma) | (uint32_t)(nxt ^ mb)) == 0u;
     int par_last = 0;
     if (MERGE == MERGE_XX) {
         // only even run offsets match (core.ts:285-290 == replaceAll's leftmost rule); the
         // parity is carried only while the chunk ends in `a`
-        if ((M[0] | M[1] | M[2] | M[3]) != 0ull || w.last == ma) {
+        if (((M0 | M1 | M2 | M3) != 0ull) | (w.last == ma)) {
             const int kl = w.len - 1;
             int par[4];
             bool start[4];
             run_parity(w.t, w.len, ap.prev, ap.par, lane, par, start);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) M[e] &= __ballot(par[e] == 0);
+            M0 &= __ballot(par[0] == 0);
+            M1 &= __ballot(par[1] == 0);
+            M2 &= __ballot(par[2] == 0);
+            M3 &= __ballot(par[3] == 0);
             par_last = bcast(pick4(par, kl & 3), kl >> 2);
             m_last &= par_last == 0;
         }
     }
     const int32_t t_last = w.last;
-    if ((ap.match | m_last) || (M[0] | M[1] | M[2] | M[3]) != 0ull) {
+    if (((M0 | M1 | M2 | M3) != 0ull) | ((ap.match | m_last) != 0)) {
 #ifdef BPE_PROBE_COMMON
         if (lane < 0) {   // (static instruction-count probe only: drop the rewrite)
 #endif
@@ -776,16 +778,14 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
         if (m_last) {
             const unsigned long long bit = 1ull << (kl >> 2);
             switch (kl & 3) {
-            case 0: M[0] |= bit; break;
-            case 1: M[1] |= bit; break;
-            case 2: M[2] |= bit; break;
-            default: M[3] |= bit; break;
+            case 0: M0 |= bit; break;
+            case 1: M1 |= bit; break;
+            case 2: M2 |= bit; break;
+            default: M3 |= bit; break;
             }
         }
-        bool m[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) m[e] = lane_in(M[e]);
-        const bool up = lane_in((M[3] << 1) | (ap.match ? 1ull : 0ull));
+        const bool m[4] = {lane_in(M0), lane_in(M1), lane_in(M2), lane_in(M3)};
+        const bool up = lane_in((M3 << 1) | (unsigned long long)(ap.match != 0));
         const int l4 = 4 * lane;
         bool keep[4];
         keep[0] = (l4 < w.len) & !up;
@@ -805,7 +805,7 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
             __builtin_bit_cast(__attribute__((__vector_size__(4 * sizeof(unsigned)))) unsigned,
                                make_uint4((unsigned)y[0], (unsigned)y[1], (unsigned)y[2], (unsigned)y[3])),
             rs, lane * 16, c * (CHUNK * 4), 0);
-        ap.n_match += (uint32_t)(__popcll(M[0]) + __popcll(M[1]) + __popcll(M[2]) + __popcll(M[3]));
+        ap.n_match += (uint32_t)(__popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3));
         w.len = total;
         w.last = last;
 #ifdef BPE_PROBE_COMMON
@@ -871,12 +871,18 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
         };
         // first pre-merge live token at or after chunk c (whose slot 0 is f0)
         auto live_from = [&](int c, int32_t f0) -> int32_t {
-            if (c >= nc) return rc.next_tok;
-            int32_t v = f0;
-            for (int q = c + 1; q < nc && v < SEP; ++q)
-                v = __builtin_amdgcn_readfirstlane(
-                    (int)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, q * (CHUNK * 4), 0));
-            return v < SEP ? rc.next_tok : v;
+            int32_t v = c < nc ? f0 : rc.next_tok;
+            if (__builtin_expect(v < SEP, 0)) {
+                // rare: empty chunks; scan their slot 0s
+                int q = c + 1;
+                for (; q < nc; ++q) {
+                    v = __builtin_amdgcn_readfirstlane(
+                        (int)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, q * (CHUNK * 4), 0));
+                    if (v >= SEP) break;
+                }
+                if (q >= nc) v = rc.next_tok;
+            }
+            return v;
         };
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, int c) {
             if (c < nc) {
