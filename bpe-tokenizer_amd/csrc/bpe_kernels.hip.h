@@ -551,9 +551,12 @@ struct Tally {
 // select.  Pairs that do not count add 0; their address stays inside the table.
 template <bool COLD>
 __device__ __forceinline__ uint32_t pair_addr(int32_t x, int32_t y) {
-    uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | (((uint32_t)y << 9) & 0x1FE00u);
-    if (COLD) a = ((uint32_t)(x | y) < (uint32_t)HOT) ? a : cold_addr(sketch_hash(x, y));
-    return a;
+    const uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | (((uint32_t)y << 9) & 0x1FE00u);
+    if (!COLD) return a;
+    // both addresses computed, then selected: the lanes of a plane mix both classes, so a
+    // branch would run both sides anyway and add exec-mask bookkeeping
+    const uint32_t c = cold_addr(sketch_hash(x, y));
+    return sel((uint32_t)(x | y) < (uint32_t)HOT, a, c);
 }
 
 template <bool COLD>
@@ -916,7 +919,9 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             if (MERGE) {
                 // does the token before the region match the region's first live token?
                 const int32_t f = live_from(0, bcast(S0.t[0], 0));
-                ap.match = ap.prev == ma && f == mb && (MERGE == MERGE_XY || ap.par == 0);
+                // (integer arithmetic: a short-circuit && here makes the flag a vector value)
+                ap.match = (((uint32_t)(ap.prev ^ ma) | (uint32_t)(f ^ mb)) == 0u) &
+                           ((MERGE == MERGE_XY) | (ap.par == 0));
             }
             // whole rounds of six stages; stages past the region see empty chunks, so the pending
             // chunk always ends in S5
