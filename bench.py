@@ -124,6 +124,13 @@ def main():
     st = trainer.engine.stats()
 
     if rank == 0:
+        # HBM bytes per launch of the same kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
+        # this same command (tools/gpu_round.sh -> tools/pmc_summary.py; counters cannot be read
+        # from inside the timed run)
+        traffic = {}
+        tpath = os.path.join(ROOT, 'profiles', 'current_pmc.json')
+        if os.path.exists(tpath):
+            traffic = json.load(open(tpath))
         k1_ms = st['step_ms'] / max(1, st['step_launches'])
         live_per_launch = st['step_live'] / max(1, st['step_launches'])
         slots_per_launch = st['step_slots'] / max(1, st['step_launches'])
@@ -156,10 +163,13 @@ def main():
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
-                'traffic': None,
+                'traffic': traffic.get('traffic_bytes_per_launch'),
                 'kernel_avg_ms': k1_ms,
                 'alg_bytes_per_launch': ALG_BYTES_PER_PAIR_SCAN * live_per_launch,
                 'slots_streamed_per_launch': slots_per_launch,
+                'traffic_fetch_bytes': traffic.get('fetch_bytes_per_launch'),
+                'traffic_write_bytes': traffic.get('write_bytes_per_launch'),
+                'traffic_source': traffic.get('source'),
             },
             'breakdown_ms_per_step': {
                 'stream_pass': st['step_ms'] / max(1, args.steps),

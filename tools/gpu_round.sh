@@ -22,16 +22,17 @@ if has bench; then
   timeout -k 10 600 python3 bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
   cat "$OUT/bench.jsonl"
 fi
-BENCH="bench.py --steps 40 --warmup 5 --no-cpu-baseline"
+BENCH="bench.py"   # the driver's default bench command, profiled as is
 if has prof; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
       -- python3 $BENCH > "$OUT/trace.log" 2>&1
   find "$OUT/trace" -name '*kernel_stats.csv' -exec cat {} \;
 fi
 if has pmc; then
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
       -- python3 $BENCH > "$OUT/fetch.log" 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
       -- python3 $BENCH > "$OUT/write.log" 2>&1
   echo pmc done
 fi
+python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" > /dev/null && echo summary written
