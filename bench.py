@@ -5,7 +5,9 @@ the argmax with the reference's tie-break, and the in-place rewrite.
 
 Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted on): a 1 GiB
 synthetic latin1 corpus (xorshift32 seed 12345, 256-char alphabet, 1 MiB samples; SURVEY.md
-§8(d)) per GPU, mergeUntil({min_weight: 2}).  Steps W+1..W+K of the merge sequence are timed.
+§8(d)) per GPU, mergeUntil({min_weight: 2}) for 8000 merges: by default W = 5 untimed warmup
+merges, then the remaining K = 7995 merges of the config are timed (every pass, tie pass and
+exact pass of the run is inside the timed region).
 With N > 1 GPUs each rank holds its own contiguous 1 GiB shard of one corpus stream (weak
 scaling); the per-iteration pair-count exchange is an RCCL all-reduce (bpe-tokenizer_amd/sharded.py).
 
@@ -62,7 +64,7 @@ def cpu_baseline(sample_mib, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--steps', type=int, default=7995)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--corpus-mib', type=int, default=1024, help='corpus MiB per GPU')
     ap.add_argument('--alphabet', type=int, default=256)

@@ -72,7 +72,7 @@ struct bpe_ctx {
     std::vector<int64_t> h_count;      // occurrences per token in the corpus (exact)
     int32_t *d_len16 = nullptr;
     int64_t cap_vocab = 0;
-    bool len16_dirty = true;
+    int64_t len16_lo = 0;      // h_len16[len16_lo:] is not yet on the device
     // pass state
     uint32_t *d_partials = nullptr;
     int partials_wg = 0;         // workgroups the partial slab can hold
@@ -169,11 +169,13 @@ int seal_packed(bpe_ctx *c) {
     return BPE_OK;
 }
 
+void mark_len16(bpe_ctx *c, int64_t i) { c->len16_lo = std::min(c->len16_lo, i); }
+
 int ensure_vocab(bpe_ctx *c, int64_t n) {
     if ((int64_t)c->h_len16.size() < n) {
+        mark_len16(c, (int64_t)c->h_len16.size());
         c->h_len16.resize(n, 1);
         c->h_count.resize(n, 0);
-        c->len16_dirty = true;
     }
     if (n > c->cap_vocab) {
         int64_t cap = std::max<int64_t>(n, std::max<int64_t>(1024, c->cap_vocab * 2));
@@ -181,16 +183,19 @@ int ensure_vocab(bpe_ctx *c, int64_t n) {
         int rc = dev_alloc(&c->d_len16, cap);
         if (rc) return rc;
         c->cap_vocab = cap;
-        c->len16_dirty = true;
+        c->len16_lo = 0;   // a fresh device buffer
     }
     return BPE_OK;
 }
 
-int sync_len16(bpe_ctx *c) {
-    if (!c->len16_dirty || c->h_len16.empty()) return BPE_OK;
-    HIP_TRY(hipMemcpyAsync(c->d_len16, c->h_len16.data(), c->h_len16.size() * sizeof(int32_t),
-                           hipMemcpyHostToDevice, c->stream));
-    c->len16_dirty = false;
+// The UTF-16 length table is read on the device only by the max_length filter (core.ts:270-273),
+// so it is brought up to date lazily and incrementally (a merge adds one entry).
+int sync_len16(bpe_ctx *c, int64_t max_length) {
+    const int64_t n = (int64_t)c->h_len16.size();
+    if (!max_length || c->len16_lo >= n) return BPE_OK;
+    HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
+                           (n - c->len16_lo) * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    c->len16_lo = n;
     return BPE_OK;
 }
 
@@ -298,7 +303,7 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         if ((rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS))) return rc;
         c->partials_wg = c->G;
     }
-    if (c->opt_max_length && (rc = sync_len16(c))) return rc;   // the reduce's max_length filter
+    if ((rc = sync_len16(c, c->opt_max_length))) return rc;   // the reduce's max_length filter
     hipStream_t s = c->stream;
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
@@ -441,7 +446,7 @@ int exact_pass(bpe_ctx *c) {
 int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_length,
                       bool local, std::vector<int2> &cand, hipEvent_t e_sel) {
     int rc;
-    if ((rc = sync_len16(c))) return rc;
+    if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
     if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
         // the reduce already left the best hot key in the Result: collect its pairs and the
@@ -569,7 +574,7 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
     if ((rc = ensure_vocab(c, (int64_t)cc + 1))) return rc;
     c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                   // core.ts:318
-    c->len16_dirty = true;
+    mark_len16(c, cc);
     if (replaced) *replaced = 0;
     if ((rc = settle(c))) return rc;
     if ((rc = maybe_compact(c))) return rc;
@@ -680,7 +685,7 @@ int bpe_set_token_len16(bpe_ctx *c, int32_t id, int32_t len16) {
     if ((rc = ensure_vocab(c, (int64_t)id + 1))) return rc;
     if (c->h_len16[id] != len16) {
         c->h_len16[id] = len16;
-        c->len16_dirty = true;
+        mark_len16(c, id);
     }
     return BPE_OK;
 }
@@ -783,7 +788,7 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
         c->h_count[id] += (int64_t)st[256 + ch];
         if (id >= *n_tokens_io) {
             c->h_len16[id] = 1;
-            c->len16_dirty = true;
+            mark_len16(c, id);
         }
     }
     *n_tokens_io = next;
@@ -920,7 +925,7 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     int rc = set_device(c);
     if (rc) return rc;
     if ((rc = settle(c))) return rc;
-    if ((rc = sync_len16(c))) return rc;
+    if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
     const auto *t = (const unsigned long long *)table;
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
@@ -956,7 +961,7 @@ int bpe_select_counts(bpe_ctx *c, const uint64_t *table, const uint32_t *cold_ke
     int rc = set_device(c);
     if (rc) return rc;
     if (min_weight == 0) min_weight = 2;                               // core.ts:256
-    if ((rc = sync_len16(c))) return rc;
+    if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     const auto *h = (const unsigned long long *)hot;

@@ -489,6 +489,12 @@ __device__ __forceinline__ bool lane_in(unsigned long long m) {
     return __builtin_amdgcn_inverse_ballot_w64(m);
 }
 
+// Lanes whose plane-e slot 4*lane + e lies below n.
+__device__ __forceinline__ unsigned long long lanes_upto(int n, int e) {
+    const int m = (n - e + 3) >> 2;
+    return m >= 64 ? ~0ull : m <= 0 ? 0ull : ((1ull << m) - 1ull);
+}
+
 // Wave-uniform facts of a freshly loaded chunk, from its tail (see LEN_TAG / LAST_TAG).
 __device__ __forceinline__ void finish_load(Chunk &c) {
     c.first = bcast(c.t[0], 0);
@@ -1299,7 +1305,10 @@ __global__ void k_cold_clear(ColdTable ct) {
 
 // ---------------------------------------------------------------------------------------------
 // K3 tie pass (rule R3): last counted occurrence (slot + 1) of up to MAX_CAND tied pairs on the
-// current corpus, with exact X X parity (carry from k_runs).
+// current corpus, with exact X X parity (carry from k_runs).  Same streaming structure as k_step:
+// a 6-slot register ring, each chunk checked once the next chunk's first token (its last slot's
+// right-hand neighbour) has arrived.  Per chunk and candidate: four compares of a packed
+// (token, right neighbour) word; the positions are worked out only in chunks that match.
 // ---------------------------------------------------------------------------------------------
 struct TieArgs {
     const int32_t *ids;
@@ -1311,45 +1320,154 @@ struct TieArgs {
     Result *res;
 };
 
+// (low 16 bits of x) << 16 | (low 16 bits of y): one v_perm.  Dead slots and SEPs have low halves
+// >= 0xFF01, which no token id (< 55296) has.
+__device__ __forceinline__ uint32_t pack_pair(int32_t x, int32_t y) {
+    return __builtin_amdgcn_perm((uint32_t)x, (uint32_t)y, 0x05040100u);
+}
+
+struct TieState {
+    int32_t prev;     // last live token before the chunk
+    int32_t par;      // its run-offset parity (valid when it is an X X candidate's token)
+    int32_t any_xx;   // some candidate is an X X pair
+    int32_t pos[MAX_CAND];   // region slot + 1 of the last counted occurrence (0: none)
+};
+
+// Checks one chunk (w.len > 0) at chunk index c of the region; nxt = the first live token after it.
+__device__ __forceinline__ void tie_chunk(const Chunk &w, int32_t nxt, int c, int lane,
+                                          const TieArgs &A, TieState &ts) {
+    const int32_t r3 = from_next(w.t[0], nxt);
+    const uint32_t k0 = pack_pair(w.t[0], w.t[1]), k1 = pack_pair(w.t[1], w.t[2]),
+                   k2 = pack_pair(w.t[2], w.t[3]), k3 = pack_pair(w.t[3], r3);
+    const int kl = w.len - 1;
+    int par[4] = {0, 0, 0, 0};
+    int have_par = 0;
+    for (int j = 0; j < A.n_cand; ++j) {
+        const int32_t a = A.ca[j], b = A.cb[j];
+        const uint32_t key = ((uint32_t)a << 16) | (uint32_t)b;
+        unsigned long long M0 = __ballot(k0 == key), M1 = __ballot(k1 == key),
+                           M2 = __ballot(k2 == key), M3 = __ballot(k3 == key);
+        int m_last = (w.last == a) & (nxt == b);
+        if (((M0 | M1 | M2 | M3) != 0ull) | m_last) {
+            // rare: keep pairs whose right-hand slot is live (slot < kl), add the last slot's pair
+            if (w.len < CHUNK) {
+                const int lim = kl;   // slots [0, kl) pair with a live in-register neighbour
+                M0 &= lanes_upto(lim, 0);
+                M1 &= lanes_upto(lim, 1);
+                M2 &= lanes_upto(lim, 2);
+                M3 &= lanes_upto(lim, 3);
+                if (m_last) {
+                    const unsigned long long bit = 1ull << (kl >> 2);
+                    switch (kl & 3) {
+                    case 0: M0 |= bit; break;
+                    case 1: M1 |= bit; break;
+                    case 2: M2 |= bit; break;
+                    default: M3 |= bit; break;
+                    }
+                }
+            }
+            if (a == b) {
+                // X X: only even run offsets count (core.ts:285-290)
+                if (!have_par) {
+                    bool start[4];
+                    run_parity(w.t, w.len, ts.prev, ts.par, lane, par, start);
+                    have_par = 1;
+                }
+                M0 &= __ballot(par[0] == 0);
+                M1 &= __ballot(par[1] == 0);
+                M2 &= __ballot(par[2] == 0);
+                M3 &= __ballot(par[3] == 0);
+            }
+            // highest matching slot of the chunk
+            int best = -1;
+            if (M0) best = max(best, 4 * (63 - __builtin_clzll(M0)) + 0);
+            if (M1) best = max(best, 4 * (63 - __builtin_clzll(M1)) + 1);
+            if (M2) best = max(best, 4 * (63 - __builtin_clzll(M2)) + 2);
+            if (M3) best = max(best, 4 * (63 - __builtin_clzll(M3)) + 3);
+            if (best >= 0) ts.pos[j] = c * CHUNK + best + 1;
+        }
+    }
+    // the parity of the last token matters only while it continues an X X candidate's run
+    int par_last = 0;
+    if (ts.any_xx) {
+        int need = 0;
+        for (int j = 0; j < A.n_cand; ++j) need |= (A.ca[j] == A.cb[j]) & (A.ca[j] == w.last);
+        if (need) {
+            if (!have_par) {
+                bool start[4];
+                run_parity(w.t, w.len, ts.prev, ts.par, lane, par, start);
+            }
+            par_last = bcast(pick4(par, kl & 3), kl >> 2);
+        }
+    }
+    ts.prev = w.last;
+    ts.par = par_last;
+}
+
 __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (r >= A.R) return;
     const int64_t c0 = (int64_t)r * A.cpr;
     const int64_t c1 = min(c0 + A.cpr, A.n_chunks);
-    const int4 *v4 = reinterpret_cast<const int4 *>(A.ids);
+    const int nc = (int)(c1 > c0 ? c1 - c0 : 0);
+    if (nc == 0) return;
     const RegionCarry rc = A.carry[r];
-    int32_t prev = rc.prev_tok;
-    int64_t prev_off = rc.carry_off - 1;
-    unsigned long long last[MAX_CAND];
-    for (int j = 0; j < MAX_CAND; ++j) last[j] = 0;
-    for (int64_t c = c0; c < c1; ++c) {
-        View w = make_view(v4[c * 64 + lane]);
-        if (w.len == 0) continue;
-        int32_t nxt = TOMB;
-        for (int64_t q = c + 1; q < c1 && nxt < SEP; ++q) nxt = A.ids[q * CHUNK];
-        if (nxt < SEP) nxt = rc.next_tok;
-        Nbr n;
-        neighbours(w, prev, nxt, lane, n);
-        int64_t off[4];
-        const int64_t lo = run_offsets(w, n, lane, prev_off, off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int32_t x = w.t[e], y = n.partner[e];
-            if (!n.live[e] || x < 0 || y < 0) continue;
-            for (int j = 0; j < A.n_cand; ++j) {
-                if (x == A.ca[j] && y == A.cb[j] && (x != y || (off[e] & 1) == 0)) {
-                    const unsigned long long pos = (unsigned long long)(c * CHUNK + 4 * lane + e) + 1;
-                    last[j] = max(pos, last[j]);
-                }
-            }
-        }
-        prev = view_at(w, w.len - 1);
-        prev_off = lo;
+    TieState ts;
+    ts.prev = rc.prev_tok;
+    ts.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
+    ts.any_xx = 0;
+    for (int j = 0; j < MAX_CAND; ++j) {
+        ts.pos[j] = 0;
+        if (j < A.n_cand) ts.any_xx |= A.ca[j] == A.cb[j];
     }
-    for (int j = 0; j < A.n_cand; ++j) {
-        unsigned long long v = wave_max_u64(last[j]);
-        if (lane == 0 && v) atomicMax(&A.res->last[j], v);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t *>(A.ids) + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
+    const int lo = lane * 16;
+    auto load = [&](Chunk &q, int c) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
+        q.t[0] = (int)x[0];
+        q.t[1] = (int)x[1];
+        q.t[2] = (int)x[2];
+        q.t[3] = (int)x[3];
+    };
+    int pc = 0;   // chunk index of the pending chunk
+    auto stage = [&](Chunk &cur, Chunk &prv, int c) {
+        if (c < nc) {
+            finish_load(cur);
+        } else {
+            cur.first = TOMB;
+            cur.len = 0;
+            cur.last = NONE;
+        }
+        if (cur.len) {
+            if (prv.len) tie_chunk(prv, cur.first, pc, lane, A, ts);
+            pc = c;
+        } else {
+            cur = prv;   // rare: hand the pending chunk on
+        }
+        load(prv, c + 5);
+        prv.len = 0;
+    };
+    Chunk S0, S1, S2, S3, S4, S5;
+    load(S0, 0);
+    load(S1, 1);
+    load(S2, 2);
+    load(S3, 3);
+    load(S4, 4);
+    S5.len = 0;
+    for (int c = 0; c < nc; c += 6) {
+        stage(S0, S5, c);
+        stage(S1, S0, c + 1);
+        stage(S2, S1, c + 2);
+        stage(S3, S2, c + 3);
+        stage(S4, S3, c + 4);
+        stage(S5, S4, c + 5);
+    }
+    if (S5.len) tie_chunk(S5, rc.next_tok, pc, lane, A, ts);
+    if (lane == 0) {
+        for (int j = 0; j < A.n_cand; ++j)
+            if (ts.pos[j]) atomicMax(&A.res->last[j], (unsigned long long)(c0 * CHUNK + ts.pos[j]));
     }
 }
 

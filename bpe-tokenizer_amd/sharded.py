@@ -86,7 +86,7 @@ class GpuShard:
         return self.engine.tie_positions(cands)
 
     def apply(self, a, b, c):
-        return self.engine.apply_merge(a, b, c)
+        return self.engine.apply_merge(a, b, c, sync=False)
 
 
 def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
@@ -198,7 +198,7 @@ class ShardedTrainer:
         if self.world == 1:
             self.engine.apply_merge(a, b, self.n_tokens, sync=False)
         else:
-            self.shard.apply(a, b, self.n_tokens)
+            self.shard.apply(a, b, self.n_tokens)   # (no host sync: the count settles lazily)
         self.n_tokens += 1
         self.live -= w
         self.merges.append(m)

@@ -28,11 +28,14 @@ if has prof; then
       -- python3 $BENCH > "$OUT/trace.log" 2>&1
   find "$OUT/trace" -name '*kernel_stats.csv' -exec cat {} \;
 fi
+# counters per launch of the same kernel on a shorter run of the same bench (each counted dispatch
+# is serialised, so the full 8000-merge run would take minutes per pass)
+PMC_BENCH="bench.py --steps 500 --warmup 5 --no-cpu-baseline"
 if has pmc; then
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
-      -- python3 $BENCH > "$OUT/fetch.log" 2>&1
+      -- python3 $PMC_BENCH > "$OUT/fetch.log" 2>&1
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
-      -- python3 $BENCH > "$OUT/write.log" 2>&1
+      -- python3 $PMC_BENCH > "$OUT/write.log" 2>&1
   echo pmc done
 fi
 python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" > /dev/null && echo summary written
