@@ -96,14 +96,8 @@ def main():
                                                seed=12345, alphabet=args.alphabet, base=base,
                                                dist=dist)
 
-    def step():
-        m = trainer.step(max_length=0, min_weight=2)
-        if m is None:
-            raise SystemExit('corpus exhausted before the timed steps finished')
-        return m
-
-    for _ in range(args.warmup):
-        step()
+    if len(trainer.run(args.warmup, max_length=0, min_weight=2)) != args.warmup:
+        raise SystemExit('corpus exhausted during warmup')
     trainer.engine.reset_stats()
     trainer.engine.stats_enable(True)
     live0 = trainer.live_tokens_global()
@@ -111,14 +105,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scans = 0
-    for _ in range(args.steps):
-        scans += trainer.live_tokens_global()
-        step()
+    merges = trainer.run(args.steps, max_length=0, min_weight=2)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if len(merges) != args.steps:
+        raise SystemExit('corpus exhausted before the timed steps finished')
+    # pair-scans: every iteration scans the live corpus it starts from
+    scans = 0
+    live = live0
+    for m in merges:
+        scans += live
+        live -= m[2]
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device='cuda')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -257,7 +257,8 @@ class Engine:
 
     def heavy_counts(self, table_ptr, keys_ptr, counts_ptr, cap, max_length=0):
         """Exact shard counts of the cold pairs whose GLOBAL sketch bucket could still win.
-        Returns the entry count (> cap means nothing was written: grow and retry)."""
+        Returns the entry count (> cap means nothing was written: grow and retry; -1 means no
+        bucket qualified, which every rank decides alike)."""
         n = ctypes.c_int64()
         rc = lib().bpe_heavy_counts(self._ctx, table_ptr, int(max_length or 0), keys_ptr,
                                     counts_ptr, cap, ctypes.byref(n))

@@ -13,6 +13,7 @@
 #include "bpe_tools.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -40,6 +41,9 @@ int fail(int code, const std::string &msg) {
 inline void dfree(void *p) {
     if (p) (void)hipFree(p);
 }
+
+// mergeUntil iterations the device runs per host round trip (each ends in one sync)
+constexpr int64_t LOOP_BATCH = 64;
 
 static_assert(TABLE_BINS == BPE_TABLE_BINS && HOT_BINS == BPE_HOT_BINS, "include/bpe.h table layout");
 
@@ -109,6 +113,9 @@ struct bpe_ctx {
     };
     std::vector<Span> spans;
     std::vector<hipEvent_t> ev_pool;
+    // device-resident mergeUntil loop: control block + merge log (pinned host mirrors)
+    LoopCtl *d_ctl = nullptr, *h_ctl = nullptr;
+    long long *d_log = nullptr, *h_log = nullptr;
 };
 
 namespace {
@@ -171,12 +178,8 @@ int seal_packed(bpe_ctx *c) {
 
 void mark_len16(bpe_ctx *c, int64_t i) { c->len16_lo = std::min(c->len16_lo, i); }
 
-int ensure_vocab(bpe_ctx *c, int64_t n) {
-    if ((int64_t)c->h_len16.size() < n) {
-        mark_len16(c, (int64_t)c->h_len16.size());
-        c->h_len16.resize(n, 1);
-        c->h_count.resize(n, 0);
-    }
+// Room for ids [0, n) in the device length table (the host tables are not extended).
+int ensure_len16_cap(bpe_ctx *c, int64_t n) {
     if (n > c->cap_vocab) {
         int64_t cap = std::max<int64_t>(n, std::max<int64_t>(1024, c->cap_vocab * 2));
         dfree(c->d_len16);
@@ -188,11 +191,21 @@ int ensure_vocab(bpe_ctx *c, int64_t n) {
     return BPE_OK;
 }
 
+int ensure_vocab(bpe_ctx *c, int64_t n) {
+    if ((int64_t)c->h_len16.size() < n) {
+        mark_len16(c, (int64_t)c->h_len16.size());
+        c->h_len16.resize(n, 1);
+        c->h_count.resize(n, 0);
+    }
+    return ensure_len16_cap(c, n);
+}
+
 // The UTF-16 length table is read on the device only by the max_length filter (core.ts:270-273),
 // so it is brought up to date lazily and incrementally (a merge adds one entry).
 int sync_len16(bpe_ctx *c, int64_t max_length) {
     const int64_t n = (int64_t)c->h_len16.size();
     if (!max_length || c->len16_lo >= n) return BPE_OK;
+    if (c->h_len16.empty()) return BPE_OK;
     HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
                            (n - c->len16_lo) * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     c->len16_lo = n;
@@ -324,9 +337,10 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     if ((rc = span_end(c, e_step, 0))) return rc;
     hipEvent_t e_red = span_begin(c);
     k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy);
+                                                          c->cold, c->d_heavy, nullptr);
     k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
-        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res);
+        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res,
+        nullptr);
     HIP_TRY(hipGetLastError());
     if ((rc = span_end(c, e_red, 1))) return rc;
     c->best_ready = true;
@@ -430,7 +444,7 @@ int exact_pass(bpe_ctx *c) {
         c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
         c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy);
+                                                          c->cold, c->d_heavy, nullptr);
     HIP_TRY(hipGetLastError());
     uint32_t flags[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
@@ -453,7 +467,7 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
         // heavy sketch buckets with the whole chip
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, 2 * sizeof(unsigned), s));
         k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(table, c->d_len16, max_length, c->d_res,
-                                                        c->d_cand, c->d_heavy);
+                                                        c->d_cand, c->d_heavy, nullptr);
     } else {
         k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand, c->d_heavy);
     }
@@ -486,6 +500,7 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
 }
 
 // R3 pass(es): last counted occurrence (slot + 1, 0 = none) of each candidate on this corpus.
+// cand: the candidate list in device memory.
 int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long long *last) {
     int rc;
     if (!c->carry_valid)
@@ -501,11 +516,9 @@ int tie_positions(bpe_ctx *c, const int2 *cand, unsigned n_cand, unsigned long l
         A.R = c->R;
         A.n_cand = (int)nb;
         A.carry = c->d_carry;
+        A.cand = cand + j0;
         A.res = c->d_res;
-        for (unsigned j = 0; j < nb; ++j) {
-            A.ca[j] = cand[j0 + j].x;
-            A.cb[j] = cand[j0 + j].y;
-        }
+        A.ctl = nullptr;
         HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
         c->best_ready = false;   // the Result is reused
         hipEvent_t e_tie = span_begin(c);
@@ -548,7 +561,7 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
         // R3: several pairs share W and a+b -> the one whose last counted occurrence is earliest
         // (the pair that reached W first in the reference's scan, core.ts:296-305)
         std::vector<unsigned long long> last(n_cand);
-        if ((rc = tie_positions(c, cand.data(), n_cand, last.data()))) return rc;
+        if ((rc = tie_positions(c, c->d_cand, n_cand, last.data()))) return rc;
         unsigned long long best_pos = ~0ull;
         for (unsigned j = 0; j < n_cand; ++j) {
             if (last[j] && last[j] < best_pos) {
@@ -582,6 +595,130 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     if (!c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     return run_pass(c, true, a, b, cc, replaced);
+}
+
+// Up to n mergeUntil iterations with the decisions kept on the device (core.ts:367-384): per
+// iteration k_select_multi, k_decide, [k_tie, k_decide] and the pass (k_step_loop, k_runs,
+// k_reduce_table), every kernel reading the merge from the LoopCtl, and one host sync at the end.
+// The merges go to out_abw[3 * i ...]; *status is the LoopStatus the batch ended with (LOOP_RUN:
+// all n done; LOOP_HOST: the next iteration needs the host path).  The host tables are brought up
+// to date from the log.
+int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, int64_t *out_abw,
+               int64_t *n_done, int *status) {
+    int rc;
+    *n_done = 0;
+    *status = LOOP_DONE;
+    if ((rc = settle(c))) return rc;
+    c->opt_max_length = max_length;
+    if (!c->counts_valid || !c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    const int64_t base = (int64_t)c->h_len16.size();
+    if ((rc = ensure_len16_cap(c, base + n))) return rc;
+    // the device table must be exact below `base`: k_decide extends it
+    if (c->len16_lo < base) {
+        HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
+                               (base - c->len16_lo) * sizeof(int32_t), hipMemcpyHostToDevice,
+                               c->stream));
+        c->len16_lo = base;
+    }
+    geometry(c);
+    hipStream_t s = c->stream;
+    if (c->best_ready && c->best_ml == max_length) {
+        // keep the reduce's best key, clear the rest of the Result
+        HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(Result) - offsetof(Result, n_cand), s));
+    } else {
+        HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+        k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res);
+    }
+    LoopCtl *h = c->h_ctl;
+    memset(h, 0, sizeof *h);
+    h->status = LOOP_RUN;
+    h->next_id = (int32_t)base;
+    h->w = -1;
+    h->min_weight = min_weight;
+    HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
+    TieArgs A;
+    memset(&A, 0, sizeof A);
+    A.ids = c->d_ids;
+    A.n_chunks = c->n_chunks;
+    A.cpr = c->cpr;
+    A.R = c->R;
+    A.carry = c->d_carry;
+    A.cand = c->d_cand;
+    A.res = c->d_res;
+    A.ctl = c->d_ctl;
+    for (int64_t i = 0; i < n; ++i) {
+        hipEvent_t e_sel = span_begin(c);
+        k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res,
+                                                        c->d_cand, c->d_heavy, c->d_ctl);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0);
+        k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1);
+        HIP_TRY(hipGetLastError());
+        if ((rc = span_end(c, e_sel, 1))) return rc;
+        hipEvent_t e_step = span_begin(c);
+        k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
+                                        c->d_partials, c->d_spill, c->cold, c->d_sums,
+                                        &c->d_res->replaced);
+        HIP_TRY(hipGetLastError());
+        if ((rc = span_end(c, e_step, 0))) return rc;
+        hipEvent_t e_red = span_begin(c);
+        k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                              c->d_spill, c->cold, c->d_heavy,
+                                                              c->d_ctl);
+        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+            c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, max_length, c->d_res, c->d_ctl);
+        HIP_TRY(hipGetLastError());
+        if ((rc = span_end(c, e_red, 1))) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(h, c->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_log, c->d_log, 3 * n * sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t nd = h->n_done;
+    if (h->status == LOOP_ERROR)
+        return fail(BPE_ERR_STATE, "bpe native: device loop: replacement count != W, or a tie "
+                                   "pass found no occurrence");
+    if (nd < 0 || nd > n) return fail(BPE_ERR_STATE, "bpe native: device loop: bad merge count");
+    // the last merge's replacement count is checked here (the others were, on the device)
+    if (h->status == LOOP_RUN && nd > 0 && c->h_res->replaced != (unsigned long long)h->w)
+        return fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+    c->h_len16.resize(base + nd, 1);
+    c->h_count.resize(base + nd, 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        const int32_t a = (int32_t)c->h_log[3 * i], b = (int32_t)c->h_log[3 * i + 1];
+        const int64_t W = c->h_log[3 * i + 2];
+        const int64_t cc = base + i;
+        c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                // core.ts:318
+        if (c->stats_on) {
+            c->stats.iterations += 1;
+            c->stats.live_tokens += c->n_live;
+        }
+        c->n_live -= W;
+        c->live_slots -= W;
+        c->h_count[a] -= W;
+        c->h_count[b] -= W;
+        c->h_count[cc] += W;
+        if (W) c->packed = false;
+        if (c->stats_on) {
+            c->stats.step_launches += 1;
+            c->stats.step_slots += c->n_chunks * CHUNK;
+            c->stats.step_live += c->n_live;
+        }
+        out_abw[3 * i] = a;
+        out_abw[3 * i + 1] = b;
+        out_abw[3 * i + 2] = W;
+    }
+    c->len16_lo = base + nd;   // k_decide wrote the new lengths on the device
+    if (c->stats_on) c->stats.tie_passes += h->n_tie;
+    c->last_replaced = nd ? c->h_log[3 * (nd - 1) + 2] : c->last_replaced;
+    // every early-ended batch leaves the last reduce's best key in the Result
+    c->best_ready = true;
+    c->best_ml = max_length;
+    c->counts_valid = c->carry_valid = true;
+    *n_done = nd;
+    *status = h->status;
+    return BPE_OK;
 }
 
 int append_begin(bpe_ctx *c, int64_t extra_slots) {
@@ -648,6 +785,12 @@ int bpe_create(bpe_ctx **out, int device) {
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
+    if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_log, 3 * LOOP_BATCH))) return bail(rc);
+    if (hipHostMalloc((void **)&c->h_ctl, sizeof(LoopCtl), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_log, 3 * LOOP_BATCH * sizeof(long long), hipHostMallocDefault) !=
+            hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipMemset(c->d_cold_flags, 0, 16) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
     if ((rc = ensure_chunks(c, 1))) return bail(rc);
@@ -664,10 +807,13 @@ int bpe_destroy(bpe_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
-                    c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used};
+                    c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used,
+                    c->d_ctl, c->d_log};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
+    if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->h_log) (void)hipHostFree(c->h_log);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &sp : c->spans) c->ev_pool.insert(c->ev_pool.end(), {sp.a, sp.b});
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -886,7 +1032,28 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     int rc = set_device(c);
     if (rc) return rc;
     int64_t n = 0;
-    for (int64_t it = 1; !max_iterations || it <= max_iterations; ++it) {   // core.ts:374-378
+    const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
+    int64_t abw[3 * LOOP_BATCH];
+    while (!max_iterations || n < max_iterations) {                      // core.ts:374-378
+        if ((rc = settle(c))) return rc;
+        if (c->n_live < 2) break;
+        if ((rc = maybe_compact(c))) return rc;
+        // batches on the device while the vocabulary has room (the host path reports the limit)
+        int64_t want = std::min<int64_t>(LOOP_BATCH, BPE_MAX_VOCAB - (int64_t)c->h_len16.size());
+        if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
+        if (want > 0) {
+            int64_t nd = 0;
+            int st = LOOP_DONE;
+            if ((rc = loop_batch(c, max_length, mw, want, abw, &nd, &st))) return rc;
+            for (int64_t i = 0; i < nd; ++i, ++n)
+                if (n < cap)
+                    for (int q = 0; q < 3; ++q) out_abw[3 * n + q] = abw[3 * i + q];
+            if (st == LOOP_DONE) break;
+            if (st == LOOP_RUN) continue;
+            if (max_iterations && n >= max_iterations) break;
+        }
+        // LOOP_HOST (heavy sketch buckets, many tied candidates) or no vocabulary room: one
+        // host-driven iteration
         int32_t a, b;
         int64_t w;
         rc = do_find(c, max_length, min_weight, &a, &b, &w);
@@ -934,8 +1101,9 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    *n_cold = 0;
+    *n_cold = -1;   // no heavy bucket: the same on every rank (bpe.h)
     if (!c->h_res->n_heavy) return BPE_OK;
+    *n_cold = 0;
     if ((rc = exact_pass(c))) return rc;
     uint32_t nu = 0;
     HIP_TRY(hipMemcpy(&nu, c->cold.n_used, sizeof nu, hipMemcpyDeviceToHost));
@@ -999,9 +1167,13 @@ int bpe_tie_positions(bpe_ctx *c, const int32_t *cand, int64_t n, uint64_t *last
         return fail(BPE_ERR_ARG, "bpe native: bad tie arguments");
     int rc = set_device(c);
     if (rc) return rc;
+    if (n > CAND_CAP) return fail(BPE_ERR_ARG, "bpe native: too many tie candidates");
+    if (n == 0) return BPE_OK;
     std::vector<int2> cv(n);
     for (int64_t i = 0; i < n; ++i) cv[i] = make_int2(cand[2 * i], cand[2 * i + 1]);
-    return tie_positions(c, cv.data(), (unsigned)n, (unsigned long long *)last);
+    if ((rc = settle(c))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_cand, cv.data(), n * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    return tie_positions(c, c->d_cand, (unsigned)n, (unsigned long long *)last);
 }
 
 int bpe_stats_enable(bpe_ctx *c, int on) {

@@ -87,6 +87,26 @@ struct Result {
     unsigned long long pad1;
 };
 
+// Device-resident mergeUntil loop (core.ts:367-384): the decision of each iteration stays in HBM and
+// the next pass reads it from there, so a batch of iterations runs without a host round trip.
+// Every kernel of the loop returns at once when status != LOOP_RUN (the batch has ended early).
+enum LoopStatus { LOOP_RUN = 0, LOOP_DONE = 1, LOOP_HOST = 2, LOOP_ERROR = 3 };
+
+struct LoopCtl {
+    int32_t status;
+    int32_t tie;          // the candidates wait for the tie pass (rule R3)
+    int32_t a, b, c;      // the merge the next pass applies
+    int32_t next_id;      // id of the next new token (token_table.length, core.ts:315)
+    int64_t w;            // its weight (-1: no merge applied yet in this batch)
+    int64_t n_done;       // merges decided in this batch (entries of the log)
+    int64_t min_weight;   // after the core.ts:256 default
+    int64_t n_tie;        // tie passes run in this batch
+};
+
+__device__ __forceinline__ bool loop_off(const LoopCtl *ctl) {
+    return ctl && ctl->status != LOOP_RUN;
+}
+
 __device__ __forceinline__ unsigned long long pack_key(unsigned long long w, int32_t a, int32_t b) {
     return w ? ((w << 17) | (unsigned long long)(0x1FFFF - (a + b))) : 0ull;
 }
@@ -826,15 +846,17 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
     ap.match = m_last;
 }
 
+// hist: the kernel's static LDS table (so, once inlined, LDS addresses are plain constants with no
+// symbol base to add per access)
 template <int MERGE, int MODE>
-__global__ void __launch_bounds__(WG)
-k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
-       const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
-       uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
-       const uint32_t *__restrict__ heavy_g, RegionSum *__restrict__ sums,
-       unsigned long long *__restrict__ replaced) {
-    // static, so LDS addresses are plain constants (no symbol base to add per access)
-    __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
+__device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ ids,
+                                          int64_t n_chunks, int64_t cpr, int R,
+                                          const RegionCarry *__restrict__ carry, int32_t ma,
+                                          int32_t mb, int32_t mc, uint32_t *__restrict__ partials,
+                                          unsigned long long *__restrict__ spill, ColdTable ct,
+                                          const uint32_t *__restrict__ heavy_g,
+                                          RegionSum *__restrict__ sums,
+                                          unsigned long long *__restrict__ replaced) {
     if (MODE == MODE_TABLE) {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
@@ -961,6 +983,35 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     }
 }
 
+template <int MERGE, int MODE>
+__global__ void __launch_bounds__(WG)
+k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
+       const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
+       uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
+       const uint32_t *__restrict__ heavy_g, RegionSum *__restrict__ sums,
+       unsigned long long *__restrict__ replaced) {
+    __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
+    step_body<MERGE, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill, ct,
+                           heavy_g, sums, replaced);
+}
+
+// The device loop's pass: the merge to apply is the one k_decide left in the LoopCtl.
+__global__ void __launch_bounds__(WG)
+k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
+            const RegionCarry *__restrict__ carry, const LoopCtl *__restrict__ ctl,
+            uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
+            RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced) {
+    __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
+    if (ctl->status != LOOP_RUN) return;
+    const int32_t ma = ctl->a, mb = ctl->b, mc = ctl->c;
+    if (ma == mb)
+        step_body<MERGE_XX, MODE_TABLE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
+                                        spill, ct, nullptr, sums, replaced);
+    else
+        step_body<MERGE_XY, MODE_TABLE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
+                                        spill, ct, nullptr, sums, replaced);
+}
+
 __device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
     while (q >= 0 && s[q].n_live == 0) --q;
     return q;
@@ -981,9 +1032,9 @@ __device__ __forceinline__ int next_nonempty(const RegionSum *s, int q, int R) {
 template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
                        unsigned long long *__restrict__ spill, ColdTable ct,
-                       const uint32_t *__restrict__ heavy) {
+                       const uint32_t *__restrict__ heavy, const LoopCtl *ctl) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
+    if (r >= R || loop_off(ctl)) return;
     Sink k;
     k.hist = nullptr;
     k.spill = spill;
@@ -1054,8 +1105,9 @@ __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len
 __global__ void __launch_bounds__(256)
 k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ spill,
                unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
-               int64_t max_length, Result *res) {
+               int64_t max_length, Result *res, const LoopCtl *ctl) {
     __shared__ uint32_t s_sum[8][32][8];
+    if (loop_off(ctl)) return;
     const int t = threadIdx.x;
     const int wl = t & 31, grp = t >> 5;
     const int w0 = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * wl;   // first of my 4 words
@@ -1200,7 +1252,9 @@ __global__ void __launch_bounds__(1024) k_select(const unsigned long long *__res
 __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *__restrict__ table,
                                                       const int32_t *__restrict__ len16,
                                                       int64_t max_length, Result *res, int2 *cand,
-                                                      uint32_t *__restrict__ heavy) {
+                                                      uint32_t *__restrict__ heavy,
+                                                      const LoopCtl *ctl) {
+    if (loop_off(ctl)) return;
     const int idx = blockIdx.x * 256 + threadIdx.x;   // grid covers TABLE_BINS exactly
     const unsigned long long best = res->best;
     if (idx < HOT_BINS) {
@@ -1220,6 +1274,77 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
             if (word) atomicAdd(&res->n_heavy, (unsigned)__popc(word));
         }
     }
+}
+
+// The device loop's decision: do_find's selection tail (core.ts:294-318) without leaving the GPU.
+// phase 0, after k_select_multi: checks the previous merge's replacement count against its W, then
+// ends the batch (no pair or W < min_weight: LOOP_DONE; heavy sketch buckets or more than MAX_CAND
+// candidates: LOOP_HOST, the host path takes that iteration), waits for the tie pass (several
+// candidates), or decides.  phase 1, after k_tie: the candidate whose last counted occurrence is
+// earliest (rule R3).  A decision logs (a, b, W), registers the new token's UTF-16 length
+// (core.ts:318) and clears the Result for the next pass.  One thread.
+__global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ cand,
+                         int32_t *len16, long long *log, int phase) {
+    if (threadIdx.x != 0 || ctl->status != LOOP_RUN) return;
+    const unsigned long long best = res->best;
+    const long long W = (long long)(best >> 17);
+    const unsigned n = res->n_cand;
+    int32_t a = -1, b = -1;
+    if (phase == 0) {
+        if (ctl->w >= 0 && res->replaced != (unsigned long long)ctl->w) {
+            ctl->status = LOOP_ERROR;
+            return;
+        }
+        ctl->w = -1;
+        if (best == 0 || W < ctl->min_weight) {                   // core.ts:312-313
+            ctl->status = LOOP_DONE;
+            return;
+        }
+        if (res->n_heavy || n == 0 || n > (unsigned)MAX_CAND) {
+            ctl->status = LOOP_HOST;
+            return;
+        }
+        if (n > 1) {
+            for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
+            ctl->tie = 1;
+            ctl->n_tie += 1;
+            return;
+        }
+        a = cand[0].x;
+        b = cand[0].y;
+    } else {
+        if (!ctl->tie) return;
+        unsigned long long bp = ~0ull;
+        for (unsigned j = 0; j < n; ++j) {
+            const unsigned long long p = res->last[j];
+            if (p && p < bp) {
+                bp = p;
+                a = cand[j].x;
+                b = cand[j].y;
+            }
+        }
+        if (a < 0) {
+            ctl->status = LOOP_ERROR;
+            return;
+        }
+        ctl->tie = 0;
+    }
+    const int32_t c = ctl->next_id;
+    len16[c] = len16[a] + len16[b];
+    const long long i = ctl->n_done;
+    log[3 * i] = a;
+    log[3 * i + 1] = b;
+    log[3 * i + 2] = W;
+    ctl->a = a;
+    ctl->b = b;
+    ctl->c = c;
+    ctl->w = W;
+    ctl->next_id = c + 1;
+    ctl->n_done = i + 1;
+    res->best = 0;
+    res->n_cand = 0;
+    res->n_heavy = 0;
+    res->replaced = 0;
 }
 
 __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, int32_t b) {
@@ -1314,10 +1439,11 @@ struct TieArgs {
     const int32_t *ids;
     int64_t n_chunks, cpr;
     int R;
-    int n_cand;
+    int n_cand;                  // host-driven passes (the device loop reads res->n_cand)
     const RegionCarry *carry;
-    int32_t ca[MAX_CAND], cb[MAX_CAND];
+    const int2 *cand;            // the candidates (a, b), at most MAX_CAND
     Result *res;
+    const LoopCtl *ctl;          // device loop: run only when ctl->tie is set
 };
 
 // (low 16 bits of x) << 16 | (low 16 bits of y): one v_perm.  Dead slots and SEPs have low halves
@@ -1326,38 +1452,68 @@ __device__ __forceinline__ uint32_t pack_pair(int32_t x, int32_t y) {
     return __builtin_amdgcn_perm((uint32_t)x, (uint32_t)y, 0x05040100u);
 }
 
+// The same packing on wave-uniform values, as scalar arithmetic.
+__device__ __forceinline__ uint32_t pack_pair_s(int32_t x, int32_t y) {
+    return ((uint32_t)x << 16) | ((uint32_t)y & 0xFFFFu);
+}
+
 struct TieState {
     int32_t prev;     // last live token before the chunk
     int32_t par;      // its run-offset parity (valid when it is an X X candidate's token)
-    int32_t any_xx;   // some candidate is an X X pair
-    int32_t pos[MAX_CAND];   // region slot + 1 of the last counted occurrence (0: none)
+    int32_t n;        // candidates
+    uint32_t xx;      // bit j: candidate j is an X X pair
+    uint32_t key[MAX_CAND];   // candidate j as a packed (a, b) word (wave-uniform registers)
+    int32_t pos[MAX_CAND];    // region slot + 1 of the last counted occurrence (0: none)
 };
 
 // Checks one chunk (w.len > 0) at chunk index c of the region; nxt = the first live token after it.
+// Every candidate costs four compares per chunk (the loops are unrolled, so keys and positions
+// stay in registers); only chunks that hold a candidate work out positions.
 __device__ __forceinline__ void tie_chunk(const Chunk &w, int32_t nxt, int c, int lane,
-                                          const TieArgs &A, TieState &ts) {
+                                          TieState &ts) {
     const int32_t r3 = from_next(w.t[0], nxt);
     const uint32_t k0 = pack_pair(w.t[0], w.t[1]), k1 = pack_pair(w.t[1], w.t[2]),
                    k2 = pack_pair(w.t[2], w.t[3]), k3 = pack_pair(w.t[3], r3);
+    const uint32_t kl_key = pack_pair_s(w.last, nxt);   // the last live slot's pair
     const int kl = w.len - 1;
+    uint32_t hit = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_CAND; ++j) {
+        if (j < ts.n) {
+            const uint32_t key = ts.key[j];
+            const unsigned long long m = __ballot(k0 == key) | __ballot(k1 == key) |
+                                         __ballot(k2 == key) | __ballot(k3 == key);
+            hit |= (uint32_t)((m != 0ull) | (kl_key == key)) << j;
+        }
+    }
     int par[4] = {0, 0, 0, 0};
     int have_par = 0;
-    for (int j = 0; j < A.n_cand; ++j) {
-        const int32_t a = A.ca[j], b = A.cb[j];
-        const uint32_t key = ((uint32_t)a << 16) | (uint32_t)b;
-        unsigned long long M0 = __ballot(k0 == key), M1 = __ballot(k1 == key),
-                           M2 = __ballot(k2 == key), M3 = __ballot(k3 == key);
-        int m_last = (w.last == a) & (nxt == b);
-        if (((M0 | M1 | M2 | M3) != 0ull) | m_last) {
-            // rare: keep pairs whose right-hand slot is live (slot < kl), add the last slot's pair
-            if (w.len < CHUNK) {
-                const int lim = kl;   // slots [0, kl) pair with a live in-register neighbour
-                M0 &= lanes_upto(lim, 0);
-                M1 &= lanes_upto(lim, 1);
-                M2 &= lanes_upto(lim, 2);
-                M3 &= lanes_upto(lim, 3);
-                if (m_last) {
-                    const unsigned long long bit = 1ull << (kl >> 2);
+    if (hit) {
+        // rare: the chunk holds a candidate.  Partial chunks keep the pairs whose right-hand slot
+        // is live (slot < kl) and add the last slot's pair; X X candidates keep even run offsets.
+        const int part = w.len < CHUNK;
+        const unsigned long long L0 = part ? lanes_upto(kl, 0) : ~0ull,
+                                 L1 = part ? lanes_upto(kl, 1) : ~0ull,
+                                 L2 = part ? lanes_upto(kl, 2) : ~0ull,
+                                 L3 = part ? lanes_upto(kl, 3) : ~0ull;
+        unsigned long long Q0 = ~0ull, Q1 = ~0ull, Q2 = ~0ull, Q3 = ~0ull;
+        if (hit & ts.xx) {
+            bool start[4];
+            run_parity(w.t, w.len, ts.prev, ts.par, lane, par, start);
+            have_par = 1;
+            Q0 = __ballot(par[0] == 0);
+            Q1 = __ballot(par[1] == 0);
+            Q2 = __ballot(par[2] == 0);
+            Q3 = __ballot(par[3] == 0);
+        }
+        const unsigned long long bit = 1ull << (kl >> 2);
+#pragma unroll
+        for (int j = 0; j < MAX_CAND; ++j) {
+            if ((hit >> j) & 1u) {
+                const uint32_t key = ts.key[j];
+                unsigned long long M0 = __ballot(k0 == key) & L0, M1 = __ballot(k1 == key) & L1,
+                                   M2 = __ballot(k2 == key) & L2, M3 = __ballot(k3 == key) & L3;
+                if (part & (kl_key == key)) {
                     switch (kl & 3) {
                     case 0: M0 |= bit; break;
                     case 1: M1 |= bit; break;
@@ -1365,34 +1521,31 @@ __device__ __forceinline__ void tie_chunk(const Chunk &w, int32_t nxt, int c, in
                     default: M3 |= bit; break;
                     }
                 }
-            }
-            if (a == b) {
-                // X X: only even run offsets count (core.ts:285-290)
-                if (!have_par) {
-                    bool start[4];
-                    run_parity(w.t, w.len, ts.prev, ts.par, lane, par, start);
-                    have_par = 1;
+                if ((ts.xx >> j) & 1u) {
+                    // X X: only even run offsets count (core.ts:285-290)
+                    M0 &= Q0;
+                    M1 &= Q1;
+                    M2 &= Q2;
+                    M3 &= Q3;
                 }
-                M0 &= __ballot(par[0] == 0);
-                M1 &= __ballot(par[1] == 0);
-                M2 &= __ballot(par[2] == 0);
-                M3 &= __ballot(par[3] == 0);
+                // highest matching slot of the chunk
+                int best = -1;
+                if (M0) best = max(best, 4 * (63 - __builtin_clzll(M0)) + 0);
+                if (M1) best = max(best, 4 * (63 - __builtin_clzll(M1)) + 1);
+                if (M2) best = max(best, 4 * (63 - __builtin_clzll(M2)) + 2);
+                if (M3) best = max(best, 4 * (63 - __builtin_clzll(M3)) + 3);
+                ts.pos[j] = best >= 0 ? c * CHUNK + best + 1 : ts.pos[j];
             }
-            // highest matching slot of the chunk
-            int best = -1;
-            if (M0) best = max(best, 4 * (63 - __builtin_clzll(M0)) + 0);
-            if (M1) best = max(best, 4 * (63 - __builtin_clzll(M1)) + 1);
-            if (M2) best = max(best, 4 * (63 - __builtin_clzll(M2)) + 2);
-            if (M3) best = max(best, 4 * (63 - __builtin_clzll(M3)) + 3);
-            if (best >= 0) ts.pos[j] = c * CHUNK + best + 1;
         }
     }
     // the parity of the last token matters only while it continues an X X candidate's run
     int par_last = 0;
-    if (ts.any_xx) {
-        int need = 0;
-        for (int j = 0; j < A.n_cand; ++j) need |= (A.ca[j] == A.cb[j]) & (A.ca[j] == w.last);
-        if (need) {
+    if (ts.xx) {
+        uint32_t need = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_CAND; ++j)
+            need |= (uint32_t)((ts.key[j] >> 16) == (uint32_t)w.last) << j;
+        if (need & ts.xx) {
             if (!have_par) {
                 bool start[4];
                 run_parity(w.t, w.len, ts.prev, ts.par, lane, par, start);
@@ -1408,6 +1561,11 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (r >= A.R) return;
+    int n = A.n_cand;
+    if (A.ctl) {
+        if (A.ctl->status != LOOP_RUN || !A.ctl->tie) return;
+        n = (int)A.res->n_cand;
+    }
     const int64_t c0 = (int64_t)r * A.cpr;
     const int64_t c1 = min(c0 + A.cpr, A.n_chunks);
     const int nc = (int)(c1 > c0 ? c1 - c0 : 0);
@@ -1416,11 +1574,17 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     TieState ts;
     ts.prev = rc.prev_tok;
     ts.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
-    ts.any_xx = 0;
+    ts.n = min(n, MAX_CAND);
+    ts.xx = 0;
+#pragma unroll
     for (int j = 0; j < MAX_CAND; ++j) {
         ts.pos[j] = 0;
-        if (j < A.n_cand) ts.any_xx |= A.ca[j] == A.cb[j];
+        // unused slots get a key no chunk word has (slot values >= 0xFF01 in both halves)
+        const int2 cj = j < ts.n ? A.cand[j] : make_int2(-1, -1);
+        ts.key[j] = __builtin_amdgcn_readfirstlane(pack_pair_s(cj.x, cj.y));
+        ts.xx |= (uint32_t)((j < ts.n) & (cj.x == cj.y)) << j;
     }
+    ts.xx = __builtin_amdgcn_readfirstlane(ts.xx);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<int32_t *>(A.ids) + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
     const int lo = lane * 16;
@@ -1441,7 +1605,7 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
             cur.last = NONE;
         }
         if (cur.len) {
-            if (prv.len) tie_chunk(prv, cur.first, pc, lane, A, ts);
+            if (prv.len) tie_chunk(prv, cur.first, pc, lane, ts);
             pc = c;
         } else {
             cur = prv;   // rare: hand the pending chunk on
@@ -1464,10 +1628,12 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         stage(S4, S3, c + 4);
         stage(S5, S4, c + 5);
     }
-    if (S5.len) tie_chunk(S5, rc.next_tok, pc, lane, A, ts);
+    if (S5.len) tie_chunk(S5, rc.next_tok, pc, lane, ts);
     if (lane == 0) {
-        for (int j = 0; j < A.n_cand; ++j)
-            if (ts.pos[j]) atomicMax(&A.res->last[j], (unsigned long long)(c0 * CHUNK + ts.pos[j]));
+#pragma unroll
+        for (int j = 0; j < MAX_CAND; ++j)
+            if (j < ts.n && ts.pos[j])
+                atomicMax(&A.res->last[j], (unsigned long long)(c0 * CHUNK + ts.pos[j]));
     }
 }
 

@@ -5,7 +5,8 @@ Pairs never cross samples (core.ts:265-267), so rank r owns a contiguous run of 
 counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exchange:
   1. the pair table (81920 x u64: exact counts of the pairs of ids < 256 + a count sketch of
      every other pair): one all-reduce(SUM) over RCCL/xGMI;
-  2. only when a sketch bucket could still reach the best hot count: every rank counts those cold
+  2. only when a sketch bucket could still reach the best hot count (every rank decides this
+     alike from the global table, so otherwise no collective runs): every rank counts those cold
      pairs exactly (one more streaming pass), then an all-gather of the (key, count) lists with
      duplicates summed on device;
   3. only when several pairs tie on (W, a+b): an all-reduce(MAX) of their last counted positions
@@ -66,6 +67,8 @@ class GpuShard:
         table = table.contiguous()
         n = self.engine.heavy_counts(table.data_ptr(), self.keys.data_ptr(), self.counts.data_ptr(),
                                      self.cap, max_length)
+        if n < 0:
+            return None   # no heavy bucket anywhere (same decision on every rank)
         if n > self.cap:
             self.cap = 1 << max(16, int(n - 1).bit_length())
             self.keys = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
@@ -99,14 +102,17 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
     table = table.to(dev, copy=True)
     dist.all_reduce(table)
     gtable = table.to(sdev)
-    keys, counts = shard.heavy(gtable, max_length)           # identical decision on every rank
-    keys = keys.to(dev)
-    counts = counts.to(dev)
-    n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(x.item()) for x in sizes]
-    m = max(sizes)
+    heavy = shard.heavy(gtable, max_length)                  # identical decision on every rank
+    m = 0
+    if heavy is not None:
+        keys, counts = heavy
+        keys = keys.to(dev)
+        counts = counts.to(dev)
+        n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n)
+        sizes = [int(x.item()) for x in sizes]
+        m = max(sizes)
     if m:
         kp = torch.full((m,), -1, dtype=torch.int32, device=dev)
         cp = torch.zeros(m, dtype=torch.int64, device=dev)
@@ -188,6 +194,25 @@ class ShardedTrainer:
             return self.engine.find_next_merge(max_length, min_weight)
         return exchange_and_select(self.shard, self.dist, self.rank, self.world, max_length,
                                    min_weight)
+
+    def run(self, n, max_length=0, min_weight=0):
+        """n merge iterations (fewer when no pair qualifies); returns the merges [(a, b, W)].
+        On one GPU this is the engine's mergeUntil (decisions stay on the device, one host sync
+        per batch of iterations); across ranks every iteration exchanges counts (step())."""
+        if self.world == 1:
+            ms = self.engine.merge_until(max_length, min_weight, n)
+            for m in ms:
+                self.n_tokens += 1
+                self.live -= m[2]
+            self.merges += ms
+            return ms
+        ms = []
+        for _ in range(n):
+            m = self.step(max_length, min_weight)
+            if m is None:
+                break
+            ms.append(m)
+        return ms
 
     def step(self, max_length=0, min_weight=0):
         """One findNextMerge + applyMerge on every rank; returns (a, b, W) or None."""

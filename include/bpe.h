@@ -124,9 +124,10 @@ int bpe_export_counts(bpe_ctx *ctx, uint64_t *table);
 
 /* Given the GLOBAL (summed) table: the cold pairs whose sketch bucket reaches the best hot count
  * (the only ones that can still win) are counted exactly on this shard (one streaming pass) and
- * written as cold_keys[i] = a<<16|b (u32), cold_counts[i] (u64).  *n_cold = entries (0 and no
- * pass when no bucket qualifies); when *n_cold > cap nothing is written and BPE_ERR_ARG is
- * returned (retry with a bigger buffer). */
+ * written as cold_keys[i] = a<<16|b (u32), cold_counts[i] (u64).  *n_cold = entries; -1 (and no
+ * pass) when no bucket qualifies, a decision every rank reaches alike from the same global table,
+ * so the cold-list exchange can be skipped; when *n_cold > cap nothing is written and
+ * BPE_ERR_ARG is returned (retry with a bigger buffer). */
 int bpe_heavy_counts(bpe_ctx *ctx, const uint64_t *table, int64_t max_length, uint32_t *cold_keys,
                      uint64_t *cold_counts, int64_t cap, int64_t *n_cold);
 

@@ -27,7 +27,7 @@ def index(a, b):
     if a < 256 and b < 256:
         return (a << 8) | b
     h = ((a & 0xFFFFFF) * 0x9E3779 & 0xFFFFFFFF) + ((b & 0xFFFFFF) * 0x85EBCB & 0xFFFFFFFF)
-    return 65536 + ((h & 0xFFFFFFFF) >> 18)
+    return 65536 + ((((h & 0xFFFFFFFF) >> 19) << 1) | (a & 1))
 
 
 class OracleShard:
@@ -51,6 +51,8 @@ class OracleShard:
         t = table.numpy()
         best = self.best_hot(t, max_length)
         T = max(best[0] if best else 0, 1)
+        if not (t[65536:] >= T).any():
+            return None   # no heavy bucket: every rank decides alike, no exchange
         keys, counts = [], []
         for a, b, c in self._cold:
             if t[index(a, b)] >= T:

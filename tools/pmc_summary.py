@@ -15,7 +15,9 @@ import json
 import os
 import sys
 
-KERNEL = 'k_step<1, 0>'   # the merge pass (MERGE_XY), the dominant kernel of the bench
+# the merge pass, the dominant kernel of the bench: the device loop's pass, or (host-driven
+# iterations) k_step<MERGE_XY>
+KERNELS = ('bpe::k_step_loop', 'k_step<1, 0>')
 
 
 def per_launch(path, counter):
@@ -29,9 +31,10 @@ def per_launch(path, counter):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    out = {'source': src, 'kernel': KERNEL}
     fetch, n_f = per_launch(os.path.join(src, 'fetch'), 'FETCH_SIZE')
     write, n_w = per_launch(os.path.join(src, 'write'), 'WRITE_SIZE')
+    KERNEL = next((k for k in KERNELS if k in fetch), KERNELS[0])
+    out = {'source': src, 'kernel': KERNEL}
     if KERNEL in fetch:
         out['fetch_bytes_per_launch'] = 2 * fetch[KERNEL] * 1024      # KiB, x2 (gfx950 wide reads)
         out['write_bytes_per_launch'] = write.get(KERNEL, 0.0) * 1024
