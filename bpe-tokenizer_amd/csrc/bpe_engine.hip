@@ -162,12 +162,9 @@ int ensure_chunks(bpe_ctx *c, int64_t chunks) {
 int seal_packed(bpe_ctx *c) {
     c->n_chunks = (c->live_slots + CHUNK - 1) / CHUNK;
     const int64_t end = c->n_chunks * CHUNK;
-    if (end > c->live_slots)
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + c->live_slots), TOMB,
-                                  end - c->live_slots, c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->d_ids + end), SEP, CHUNK, c->stream));
     if (end > c->live_slots) {
-        k_seal<<<1, 1, 0, c->stream>>>(c->d_ids, c->live_slots);
+        k_seal<<<1, CHUNK, 0, c->stream>>>(c->d_ids, c->live_slots);
         HIP_TRY(hipGetLastError());
     }
     c->packed = true;
@@ -423,7 +420,9 @@ int compact(bpe_ctx *c) {
 int maybe_compact(bpe_ctx *c) {
     const int64_t slots = c->n_chunks * CHUNK;
     if (c->packed || slots < (1 << 20)) return BPE_OK;
-    if (c->live_slots * 4 >= slots * 3) return BPE_OK;   // keep while >= 75% of slots are live
+    // dead slots cost a pass as much as live ones: re-pack once they are 3% of the stream (a
+    // compaction costs about three passes; at C3 merge rates that is every ~2000 merges)
+    if (c->live_slots * 100 >= slots * 97) return BPE_OK;
     int rc = compact(c);
     if (rc) return rc;
     return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout

@@ -29,6 +29,9 @@ constexpr int32_t NONE = -3;                // "no token" (register sentinel onl
 // Tail tags of a partial chunk (every stored value < SEP is a dead slot): slot 255 holds
 // LEN_TAG - len; slot 254, when dead, holds LAST_TAG - (the last live token), else TOMB.
 constexpr int32_t LEN_TAG = -16;
+// Dead slots alternate TOMB (even slots) and TOMB_ODD (odd slots), so no dead slot equals its
+// neighbour: equal-neighbour masks need no liveness masking.
+constexpr int32_t TOMB_ODD = -4;
 constexpr int32_t LAST_TAG = -1000;
 constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x int4)
 #ifndef BPE_WAVES
@@ -138,6 +141,19 @@ __device__ __forceinline__ int32_t from_next(int32_t x, int32_t fill) {
 
 __device__ __forceinline__ int32_t from_prev(int32_t x, int32_t fill) {
     return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);   // wave_shr:1
+}
+
+// A (token, right neighbour) pair as one word: (low 16 bits of x) << 16 | (low 16 bits of y), one
+// v_perm.  Token ids are < 55296; SEP, TOMB, TOMB_ODD and the LEN_TAG values have low halves
+// >= 0xFEF0, so they never alias one.  A LAST_TAG value (slot 254 only) can: code comparing packed
+// pairs must not trust a match involving slot 254 of a partial chunk.
+__device__ __forceinline__ uint32_t pack_pair(int32_t x, int32_t y) {
+    return __builtin_amdgcn_perm((uint32_t)x, (uint32_t)y, 0x05040100u);
+}
+
+// The same packing on wave-uniform values, as scalar arithmetic.
+__device__ __forceinline__ uint32_t pack_pair_s(int32_t x, int32_t y) {
+    return ((uint32_t)x << 16) | ((uint32_t)y & 0xFFFFu);
 }
 
 __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint32_t inc) {
@@ -458,7 +474,7 @@ __device__ __forceinline__ int compact_chunk(int32_t (&val)[4], const bool (&kee
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        val[e] = sel(4 * lane < total - e, (int32_t)(pk[e] & 0x1FFFFu) - 1, TOMB);
+        val[e] = sel(4 * lane < total - e, (int32_t)(pk[e] & 0x1FFFFu) - 1, (e & 1) ? TOMB_ODD : TOMB);
     return total;
 }
 
@@ -577,7 +593,7 @@ struct Tally {
 // select.  Pairs that do not count add 0; their address stays inside the table.
 template <bool COLD>
 __device__ __forceinline__ uint32_t pair_addr(int32_t x, int32_t y) {
-    const uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | (((uint32_t)y << 9) & 0x1FE00u);
+    const uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
     if (!COLD) return a;
     // both addresses computed, then selected: the lanes of a plane mix both classes, so a
     // branch would run both sides anyway and add exec-mask bookkeeping
@@ -636,26 +652,23 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     const int32_t r3 = from_next(t0, nxt);
     const int32_t l0 = from_prev(t3, s.prev);
     // E*: slot equals its right-hand neighbour (Em1: slot 0 equals the token before it)
-    unsigned long long Em1 = __ballot(t0 == l0), E0 = __ballot(t0 == t1), E1 = __ballot(t1 == t2),
-                       E2 = __ballot(t2 == t3), E3 = __ballot(t3 == r3);
-    if (!full) {
-        // dead slots equal each other: keep live non-SEP slots only
-        const unsigned long long P0 = __ballot(t0 >= 0), P1 = __ballot(t1 >= 0),
-                                 P2 = __ballot(t2 >= 0), P3 = __ballot(t3 >= 0);
-        Em1 &= P0;
-        E0 &= P0;
-        E1 &= P1;
-        E2 &= P2;
-        E3 &= P3;
-    }
+    // (no dead slot equals its neighbour, and slot 0 is live; an SEP next to an SEP only sends the
+    // chunk to the exact path)
+    const unsigned long long Em1 = __ballot(t0 == l0), E0 = __ballot(t0 == t1),
+                             E1 = __ballot(t1 == t2), E2 = __ballot(t2 == t3), E3 = __ballot(t3 == r3);
     const unsigned long long trip = (E0 & (Em1 | E1)) | (E2 & (E1 | E3));
     const int fast = (trip == 0ull) & (s.in_lead == 0) & (full | (w.last != nxt));
     if (fast) {
         // every X X pair starts its run, so every valid pair counts
         if (MODE == MODE_TABLE) {
-            const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1), max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
-            if (full & (__ballot(mx >= (uint32_t)HOT) == 0ull)) {
-                // hot tokens only, no SEP: unmasked adds
+            // full chunks of hot tokens only (a fresh corpus): unmasked adds
+            int hot_only = 0;
+            if (full) {
+                const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1),
+                                        max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
+                hot_only = __ballot(mx >= (uint32_t)HOT) == 0ull;
+            }
+            if (hot_only) {
                 const int32_t x[4] = {t0, t1, t2, t3}, y[4] = {t1, t2, t3, r3};
                 uint32_t o[4];
 #pragma unroll
@@ -670,13 +683,10 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                     }
                 }
             } else {
+                // mixed planes (partial chunks hold merged tokens: the steady state)
                 const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
                 const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
-                // any valid cold pair?  (x | y >= HOT as a signed value)
-                const int32_t smx = max(max((int32_t)(x[0] | y[0]), (int32_t)(x[1] | y[1])),
-                                        max((int32_t)(x[2] | y[2]), (int32_t)(x[3] | y[3])));
-                if (__ballot(smx >= HOT) == 0ull) add_pairs<false>(x, y, k);
-                else add_pairs<true>(x, y, k);
+                add_pairs<true>(x, y, k);
             }
         } else {
             const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
@@ -767,12 +777,31 @@ __device__ __forceinline__ void tag_tail(int32_t (&y)[4], int total, int32_t las
 
 // Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
 // in place: nxt = the first pre-merge live token after it (the next region's first for the last
-// chunk).  A touched chunk is re-packed and written back.  The common case (no match) is eight
-// compares and a handful of mask operations.
+// chunk).  A touched chunk is re-packed and written back.  key = pack_pair_s(ma, mb).
 template <int MERGE>
 __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, int32_t mb,
-                                            int32_t mc, const __amdgpu_buffer_rsrc_t rs, int c,
-                                            int lane, Apply &ap) {
+                                            int32_t mc, uint32_t key,
+                                            const __amdgpu_buffer_rsrc_t rs, int c, int lane,
+                                            Apply &ap) {
+    // The common case, no (a, b) in the chunk: four packed (slot, right neighbour) compares.  In a
+    // partial chunk lane 63's slot 3 (dead) stands in for the last live slot, paired with nxt.
+    // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)
+    {
+        const int32_t r3 = from_next(w.t[0], nxt);
+        const int32_t x3 = sel(lane_in(w.len == CHUNK ? 0ull : (1ull << 63)), w.last, w.t[3]);
+        const unsigned long long H =
+            __ballot(pack_pair(w.t[0], w.t[1]) == key) | __ballot(pack_pair(w.t[1], w.t[2]) == key) |
+            __ballot(pack_pair(w.t[2], w.t[3]) == key) | __ballot(pack_pair(x3, r3) == key);
+        unsigned long long T = H | (unsigned long long)(uint32_t)ap.match;
+        // (X X merges also carry the run parity while the chunk ends in `a`)
+        if (MERGE == MERGE_XX) T |= (unsigned long long)(uint32_t)(w.last == ma);
+        if (T == 0ull) {
+            ap.prev = w.last;
+            ap.par = 0;
+            ap.match = 0;
+            return;
+        }
+    }
     // M[e]: slot e is `a` and its in-register right-hand neighbour is `b`
     const unsigned long long A0 = __ballot(w.t[0] == ma), A1 = __ballot(w.t[1] == ma),
                              A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
@@ -915,7 +944,12 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             }
             return v;
         };
-        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, int c) {
+        const uint32_t key = pack_pair_s(ma, mb);
+        // Ring of seven: stage c applies chunk c (cur), counts chunk c-1 (prv) and loads chunk
+        // c+5 into the slot of chunk c-2 (fre), which the previous stage freed, so the load can
+        // issue at once without its registers overlapping a chunk still in use.
+        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c) {
+            load(fre, c + 5);
             if (c < nc) {
                 finish_load(cur);
             } else {
@@ -926,24 +960,22 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 cur.last = NONE;
             }
             if (MERGE && cur.len)
-                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs,
-                                   c, lane, ap);
+                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, key,
+                                   rs, c, lane, ap);
             if (cur.len) {
                 if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k);
             } else {
                 cur = prv;   // rare: hand the pending chunk on
             }
-            load(prv, c + 5);
-            prv.len = 0;
         };
         if (nc > 0) {
-            Chunk S0, S1, S2, S3, S4, S5;
+            Chunk S0, S1, S2, S3, S4, S5, S6;
             load(S0, 0);
             load(S1, 1);
             load(S2, 2);
             load(S3, 3);
             load(S4, 4);
-            S5.len = 0;
+            S6.len = 0;
             if (MERGE) {
                 // does the token before the region match the region's first live token?
                 const int32_t f = live_from(0, bcast(S0.t[0], 0));
@@ -951,17 +983,18 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 ap.match = (((uint32_t)(ap.prev ^ ma) | (uint32_t)(f ^ mb)) == 0u) &
                            ((MERGE == MERGE_XY) | (ap.par == 0));
             }
-            // whole rounds of six stages; stages past the region see empty chunks, so the pending
-            // chunk always ends in S5
-            for (int c = 0; c < nc; c += 6) {
-                stage(S0, S1, S5, c);
-                stage(S1, S2, S0, c + 1);
-                stage(S2, S3, S1, c + 2);
-                stage(S3, S4, S2, c + 3);
-                stage(S4, S5, S3, c + 4);
-                stage(S5, S0, S4, c + 5);
+            // whole rounds of seven stages; stages past the region see empty chunks, so the
+            // pending chunk always ends in S6
+            for (int c = 0; c < nc; c += 7) {
+                stage(S0, S1, S6, S5, c);
+                stage(S1, S2, S0, S6, c + 1);
+                stage(S2, S3, S1, S0, c + 2);
+                stage(S3, S4, S2, S1, c + 3);
+                stage(S4, S5, S3, S2, c + 4);
+                stage(S5, S6, S4, S3, c + 5);
+                stage(S6, S0, S5, S4, c + 6);
             }
-            if (S5.len) count_chunk<MODE>(S5, NONE, lane, s, k);
+            if (S6.len) count_chunk<MODE>(S6, NONE, lane, s, k);
         }
         if (lane == 0) {
             RegionSum o;
@@ -1446,17 +1479,6 @@ struct TieArgs {
     const LoopCtl *ctl;          // device loop: run only when ctl->tie is set
 };
 
-// (low 16 bits of x) << 16 | (low 16 bits of y): one v_perm.  Dead slots and SEPs have low halves
-// >= 0xFF01, which no token id (< 55296) has.
-__device__ __forceinline__ uint32_t pack_pair(int32_t x, int32_t y) {
-    return __builtin_amdgcn_perm((uint32_t)x, (uint32_t)y, 0x05040100u);
-}
-
-// The same packing on wave-uniform values, as scalar arithmetic.
-__device__ __forceinline__ uint32_t pack_pair_s(int32_t x, int32_t y) {
-    return ((uint32_t)x << 16) | ((uint32_t)y & 0xFFFFu);
-}
-
 struct TieState {
     int32_t prev;     // last live token before the chunk
     int32_t par;      // its run-offset parity (valid when it is an X X candidate's token)
@@ -1596,7 +1618,9 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         q.t[3] = (int)x[3];
     };
     int pc = 0;   // chunk index of the pending chunk
-    auto stage = [&](Chunk &cur, Chunk &prv, int c) {
+    // ring of seven, as in k_step: chunk c+5 loads into the slot chunk c-2 freed
+    auto stage = [&](Chunk &cur, Chunk &prv, Chunk &fre, int c) {
+        load(fre, c + 5);
         if (c < nc) {
             finish_load(cur);
         } else {
@@ -1610,25 +1634,24 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         } else {
             cur = prv;   // rare: hand the pending chunk on
         }
-        load(prv, c + 5);
-        prv.len = 0;
     };
-    Chunk S0, S1, S2, S3, S4, S5;
+    Chunk S0, S1, S2, S3, S4, S5, S6;
     load(S0, 0);
     load(S1, 1);
     load(S2, 2);
     load(S3, 3);
     load(S4, 4);
-    S5.len = 0;
-    for (int c = 0; c < nc; c += 6) {
-        stage(S0, S5, c);
-        stage(S1, S0, c + 1);
-        stage(S2, S1, c + 2);
-        stage(S3, S2, c + 3);
-        stage(S4, S3, c + 4);
-        stage(S5, S4, c + 5);
+    S6.len = 0;
+    for (int c = 0; c < nc; c += 7) {
+        stage(S0, S6, S5, c);
+        stage(S1, S0, S6, c + 1);
+        stage(S2, S1, S0, c + 2);
+        stage(S3, S2, S1, c + 3);
+        stage(S4, S3, S2, c + 4);
+        stage(S5, S4, S3, c + 5);
+        stage(S6, S5, S4, c + 6);
     }
-    if (S5.len) tie_chunk(S5, rc.next_tok, pc, lane, ts);
+    if (S6.len) tie_chunk(S6, rc.next_tok, pc, lane, ts);
     if (lane == 0) {
 #pragma unroll
         for (int j = 0; j < MAX_CAND; ++j)
@@ -1690,13 +1713,20 @@ __global__ void __launch_bounds__(256) k_compact(const int32_t *__restrict__ ids
     }
 }
 
-// Tail tags of the last chunk after a dense write of live_slots slots (TOMB already filled).
-__global__ void k_seal(int32_t *__restrict__ ids, int64_t live_slots) {
+// Dead tail + tail tags of the last chunk after a dense write of live_slots slots.  One block of
+// CHUNK threads.
+__global__ void __launch_bounds__(CHUNK) k_seal(int32_t *__restrict__ ids, int64_t live_slots) {
     const int len = (int)(live_slots % CHUNK);
     if (len == 0) return;
     int32_t *p = ids + (live_slots / CHUNK) * CHUNK;
-    p[CHUNK - 1] = LEN_TAG - len;
-    if (len < CHUNK - 1) p[CHUNK - 2] = LAST_TAG - p[len - 1];
+    const int t = threadIdx.x;
+    const int32_t last = p[len - 1];
+    if (t >= len) p[t] = (t & 1) ? TOMB_ODD : TOMB;
+    __syncthreads();
+    if (t == 0) {
+        p[CHUNK - 1] = LEN_TAG - len;
+        if (len < CHUNK - 1) p[CHUNK - 2] = LAST_TAG - last;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
