@@ -189,16 +189,27 @@ __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
     return ((uint32_t)x << 16) | (uint32_t)y;
 }
 
+// Sketch hash of a cold pair: h = x * SKETCH_K + y (one v_mad_u32_u24), sketch dword
+// h & 0x1FFF = (x * K + y) mod 8192 (K odd).  Consecutive ids land in consecutive dwords, so the
+// merged tokens (allocated in sequence) spread evenly.
+constexpr uint32_t SKETCH_K = 0x19B1u;
+__device__ __forceinline__ uint32_t sketch_hash(int32_t x, int32_t y) {
+    // (written out: left to itself the compiler may widen this to a 64-bit multiply-add)
+    uint32_t h;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(x), "s"(SKETCH_K), "v"(y));
+    return h;
+}
+
+// Sketch bucket: the dword from the hash, the half from x (as for hot pairs, see below).
+__device__ __forceinline__ uint32_t sketch_bucket(int32_t x, int32_t y) {
+    return ((sketch_hash(x, y) & 0x1FFFu) << 1) | ((uint32_t)x & 1u);
+}
+
 // Table index of a pair: its exact bin when both ids are hot, else its sketch bucket.
-// Branch-free: both forms are computed and selected (the sketch hash uses the full-rate 24-bit
-// multiplier; ids < 2^16).
-constexpr uint32_t SKETCH_MUL_A = 0x9E3779u, SKETCH_MUL_B = 0x85EBCBu;
+// Branch-free: both forms are computed and selected.
 __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
     const uint32_t hot = ((uint32_t)x << 8) | (uint32_t)y;
-    // (HIP's __umul24 returns int: the sum must be shifted as unsigned)
-    const uint32_t h = (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) +
-                       (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
-    const uint32_t cold = HOT_BINS + (((h >> 19) << 1) | ((uint32_t)x & 1u));
+    const uint32_t cold = HOT_BINS + sketch_bucket(x, y);
     return ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT ? (int)hot : (int)cold;
 }
 
@@ -234,7 +245,7 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
 //    ((x << 1) & 0x1FC) | (y << 9) and increment 1 << ((x << 4) & 16): five VALU operations, the
 //    half chosen by a bit the shift amount already carries;
 //  - sketch bucket b of a cold pair: dword HOT_BINS / 2 + (b >> 1), half b & 1, with
-//    b = ((hash >> 19) << 1) | (x & 1): the dword from the hash, the half from x, so both
+//    b = ((hash & 0x1FFF) << 1) | (x & 1): the dword from the hash, the half from x, so both
 //    classes share the increment.
 // A counter reaching 0x8000 spills 0x8000 to the global u64 table (indexed by table_index):
 // exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom absorbs
@@ -251,15 +262,16 @@ __device__ __forceinline__ uint32_t hot_inc(int32_t x) {
     return 1u << (((uint32_t)x << 4) & 31u);
 }
 
-__device__ __forceinline__ uint32_t sketch_hash(int32_t x, int32_t y) {
-    return (uint32_t)__umul24((uint32_t)x, SKETCH_MUL_A) + (uint32_t)__umul24((uint32_t)y, SKETCH_MUL_B);
-}
+// byte address of sketch dword HOT_BINS / 2 + (h & 0x1FFF)
+__device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | ((h & 0x1FFFu) << 2); }
 
-// sketch dword HOT_BINS / 2 + (h >> 19)
-__device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | ((h >> 17) & 0x7FFCu); }
-
-__device__ __forceinline__ uint32_t sketch_bucket(int32_t x, int32_t y) {
-    return ((sketch_hash(x, y) >> 19) << 1) | ((uint32_t)x & 1u);
+// The same from the pair, as two instructions (the compiler otherwise re-associates the mask and
+// the shift into three, for lack of a second literal operand)
+__device__ __forceinline__ uint32_t cold_addr_of(int32_t x, int32_t y) {
+    uint32_t b, a;
+    asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
+    asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(a) : "v"(b), "s"(HOT_BYTES));
+    return a;
 }
 
 __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
@@ -591,29 +603,27 @@ struct Tally {
 // address (three operations), the increment (two, shared by both classes: a sketch bucket's
 // half is also x & 1), and, when the chunk has cold pairs, the sketch address (four) and a
 // select.  Pairs that do not count add 0; their address stays inside the table.
-template <bool COLD>
-__device__ __forceinline__ uint32_t pair_addr(int32_t x, int32_t y) {
-    const uint32_t a = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
-    if (!COLD) return a;
-    // both addresses computed, then selected: the lanes of a plane mix both classes, so a
-    // branch would run both sides anyway and add exec-mask bookkeeping
-    const uint32_t c = cold_addr(sketch_hash(x, y));
-    return sel((uint32_t)(x | y) < (uint32_t)HOT, a, c);
+// Per pair: the hot address (three operations), the sketch address (three), u = ~(x | y) (one,
+// opaque to the compiler so both uses below read it as is), the class select (two), and the
+// increment (three): hot_inc(x) for a valid pair, 0 when a side is negative (SEP, dead), with the
+// validity bit (u's sign) as the value shifted.  Pairs with a cold side go to their sketch bucket.
+__device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, uint32_t &inc) {
+    uint32_t u = ~((uint32_t)x | (uint32_t)y);
+    asm("" : "+v"(u));
+    const uint32_t hot = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
+    addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of(x, y));   // both ids < 256
+    inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
 }
 
-template <bool COLD>
-__device__ __forceinline__ uint32_t pair_inc(int32_t x, int32_t y) {
-    const uint32_t u = (uint32_t)(x | y);
-    return (COLD ? (int32_t)u >= 0 : u < (uint32_t)HOT) ? hot_inc(x) : 0u;
-}
-
-template <bool COLD>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
                                           const Sink &k) {
     uint32_t o[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-        o[e] = atomicAdd(lds_word(k, pair_addr<COLD>(x[e], y[e])), pair_inc<COLD>(x[e], y[e]));
+    for (int e = 0; e < 4; ++e) {
+        uint32_t addr, inc;
+        pair_slot(x[e], y[e], addr, inc);
+        o[e] = atomicAdd(lds_word(k, addr), inc);
+    }
     // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
     if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
 #pragma unroll
@@ -621,13 +631,9 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
             // recomputed here (rare) rather than kept live across the adds
             int32_t xx = x[e], yy = y[e];
             asm volatile("" : "+v"(xx), "+v"(yy));
-            const uint32_t inc = pair_inc<COLD>(xx, yy);
-            if (inc) {
-                const bool hot = (uint32_t)(xx | yy) < (uint32_t)HOT;
-                const uint32_t bin = hot ? (((uint32_t)xx << 8) | (uint32_t)yy)
-                                         : HOT_BINS + sketch_bucket(xx, yy);
-                lds_fix(k, pair_addr<COLD>(xx, yy), inc, bin, o[e]);
-            }
+            uint32_t addr, inc;
+            pair_slot(xx, yy, addr, inc);
+            if (inc) lds_fix(k, addr, inc, (uint32_t)table_index(xx, yy), o[e]);
         }
     }
 }
@@ -686,7 +692,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 // mixed planes (partial chunks hold merged tokens: the steady state)
                 const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
                 const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
-                add_pairs<true>(x, y, k);
+                add_pairs(x, y, k);
             }
         } else {
             const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);

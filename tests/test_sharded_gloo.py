@@ -26,8 +26,8 @@ def index(a, b):
     """Table index of libbpe's pair table (include/bpe.h): hot bin, or cold sketch bucket."""
     if a < 256 and b < 256:
         return (a << 8) | b
-    h = ((a & 0xFFFFFF) * 0x9E3779 & 0xFFFFFFFF) + ((b & 0xFFFFFF) * 0x85EBCB & 0xFFFFFFFF)
-    return 65536 + ((((h & 0xFFFFFFFF) >> 19) << 1) | (a & 1))
+    h = ((a & 0xFFFFFF) * 0x19B1 + (b & 0xFFFFFF)) & 0xFFFFFFFF
+    return 65536 + (((h & 0x1FFF) << 1) | (a & 1))
 
 
 class OracleShard:
