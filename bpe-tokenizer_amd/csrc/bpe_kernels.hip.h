@@ -1344,8 +1344,11 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
             return;
         }
         if (n > 1) {
+            // X Y candidates only: the tail window first; else the full pass
+            int all_xy = 1;
+            for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
             for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
-            ctl->tie = 1;
+            ctl->tie = all_xy ? 1 : 2;
             ctl->n_tie += 1;
             return;
         }
@@ -1354,6 +1357,7 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
     } else {
         if (!ctl->tie) return;
         unsigned long long bp = ~0ull;
+        unsigned missing = 0;
         for (unsigned j = 0; j < n; ++j) {
             const unsigned long long p = res->last[j];
             if (p && p < bp) {
@@ -1361,6 +1365,20 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
                 a = cand[j].x;
                 b = cand[j].y;
             }
+            missing += p == 0;
+        }
+        if (ctl->tie == 1 && missing) {
+            if (missing > 1) {
+                // two or more occur only before the tail window: the host path's full pass
+                ctl->status = LOOP_HOST;
+                return;
+            }
+            // the only one missing occurs only earlier: its last occurrence is the earliest
+            for (unsigned j = 0; j < n; ++j)
+                if (res->last[j] == 0) {
+                    a = cand[j].x;
+                    b = cand[j].y;
+                }
         }
         if (a < 0) {
             ctl->status = LOOP_ERROR;
@@ -1585,23 +1603,23 @@ __device__ __forceinline__ void tie_chunk(const Chunk &w, int32_t nxt, int c, in
     ts.par = par_last;
 }
 
+// Tail mode of the tie pass (device loop, no X X candidate): the last TIE_TAIL_CHUNKS chunks, two
+// per wave, each chunk on its own (an X Y pair needs no run context, only the next live token).
+// The last occurrence of a candidate found there is its last occurrence in the corpus; a candidate
+// not found there occurs only earlier, so it wins if it is the only one missing (k_decide).
+constexpr int TIE_TAIL_PER_WAVE = 2;
+
 __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (r >= A.R) return;
     int n = A.n_cand;
+    int tail = 0;
     if (A.ctl) {
         if (A.ctl->status != LOOP_RUN || !A.ctl->tie) return;
         n = (int)A.res->n_cand;
+        tail = A.ctl->tie == 1;
     }
-    const int64_t c0 = (int64_t)r * A.cpr;
-    const int64_t c1 = min(c0 + A.cpr, A.n_chunks);
-    const int nc = (int)(c1 > c0 ? c1 - c0 : 0);
-    if (nc == 0) return;
-    const RegionCarry rc = A.carry[r];
     TieState ts;
-    ts.prev = rc.prev_tok;
-    ts.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
     ts.n = min(n, MAX_CAND);
     ts.xx = 0;
 #pragma unroll
@@ -1613,6 +1631,51 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         ts.xx |= (uint32_t)((j < ts.n) & (cj.x == cj.y)) << j;
     }
     ts.xx = __builtin_amdgcn_readfirstlane(ts.xx);
+    if (tail) {
+        const int64_t win = (int64_t)gridDim.x * 4 * TIE_TAIL_PER_WAVE;
+        const int64_t cw = max((int64_t)0, A.n_chunks - win) + (int64_t)r * TIE_TAIL_PER_WAVE;
+        if (cw >= A.n_chunks) return;
+        ts.prev = NONE;
+        ts.par = 0;
+        const int4 *v4 = reinterpret_cast<const int4 *>(A.ids);
+        for (int q = 0; q < TIE_TAIL_PER_WAVE; ++q) {
+            const int64_t c = cw + q;
+            if (c >= A.n_chunks) break;
+            const int4 v = v4[c * 64 + lane];
+            Chunk w;
+            w.t[0] = v.x;
+            w.t[1] = v.y;
+            w.t[2] = v.z;
+            w.t[3] = v.w;
+            finish_load(w);
+            if (w.len == 0) continue;
+            // the first live token after the chunk (SEP past the corpus end)
+            int32_t nxt = SEP;
+            for (int64_t q2 = c + 1; q2 < A.n_chunks; ++q2) {
+                const int32_t f = __builtin_amdgcn_readfirstlane(A.ids[q2 * CHUNK]);
+                if (f >= SEP) {
+                    nxt = f;
+                    break;
+                }
+            }
+            tie_chunk(w, nxt, q, lane, ts);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < MAX_CAND; ++j)
+                if (j < ts.n && ts.pos[j])
+                    atomicMax(&A.res->last[j], (unsigned long long)(cw * CHUNK + ts.pos[j]));
+        }
+        return;
+    }
+    if (r >= A.R) return;
+    const int64_t c0 = (int64_t)r * A.cpr;
+    const int64_t c1 = min(c0 + A.cpr, A.n_chunks);
+    const int nc = (int)(c1 > c0 ? c1 - c0 : 0);
+    if (nc == 0) return;
+    const RegionCarry rc = A.carry[r];
+    ts.prev = rc.prev_tok;
+    ts.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<int32_t *>(A.ids) + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
     const int lo = lane * 16;

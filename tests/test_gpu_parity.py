@@ -226,3 +226,31 @@ def test_compaction_under_heavy_merging():
     e, got = run_engine([sample], [1, 1], {})
     assert got == want
     assert e.samples() == st.samples()
+
+
+@pytest.mark.parametrize('early', [1, 2, 3])
+def test_ties_resolved_from_the_corpus_tail(early):
+    """R3 ties in a corpus larger than the device loop's tail window (8192 chunks): `early` of the
+    tied pairs occur only in the first quarter.  One such pair wins from the window alone; two or
+    more need the full pass (the loop hands the iteration to the host path)."""
+    rng = np.random.default_rng(early)
+    n, V = 4_000_000, 3000
+    seq = rng.integers(0, V, n, dtype=np.int32)      # filler: every filler pair is rare
+    S = 2 * V + 90                                  # common a + b of the tied pairs
+    pairs = [(V + i, S - V - i) for i in range(6)]   # ids in [V, V + 90]
+    W = 40
+    for k, (a, b) in enumerate(pairs):
+        hi = n // 4 if k < early else n - 200      # (the window is the last ~2.1M slots)
+        pos = rng.choice(np.arange(4, hi, 7), W, replace=False)
+        if k >= early:
+            pos[0] = n - 14 - 7 * k                 # one occurrence in the last chunks
+        for p in pos:
+            seq[p - 1], seq[p], seq[p + 1], seq[p + 2] = V + 95, a, b, V + 96
+    # (the breakers V+95 / V+96 keep the inserted pairs apart; their own pairs stay below W)
+    n_tok = V + 97
+    len16 = [1] * n_tok
+    st = OracleState(seq, np.array([0, n], np.int64), len16, n_tok)
+    want = st.merge_until(0, 2, 8)
+    e, got = run_engine([seq], len16, {'min_weight': 2, 'max_iterations': 8})
+    assert got == want
+    assert e.samples() == st.samples()
