@@ -26,13 +26,17 @@ namespace bpe {
 constexpr int32_t SEP = -1;                 // sample separator (live slot, never in a pair)
 constexpr int32_t TOMB = -2;                // dead slot in a chunk tail
 constexpr int32_t NONE = -3;                // "no token" (register sentinel only)
-// Tail tags of a partial chunk (every stored value < SEP is a dead slot): slot 255 holds
-// LEN_TAG - len; slot 254, when dead, holds LAST_TAG - (the last live token), else TOMB.
+// Tail tag of a partial chunk (every stored value < SEP is a dead slot): slot 255 holds
+// LEN_TAG - len - ((last + 3) << 8), i.e. its live length and its last live slot (NONE when empty)
+// in one value, read with one v_readlane.
 constexpr int32_t LEN_TAG = -16;
 // Dead slots alternate TOMB (even slots) and TOMB_ODD (odd slots), so no dead slot equals its
 // neighbour: equal-neighbour masks need no liveness masking.
 constexpr int32_t TOMB_ODD = -4;
-constexpr int32_t LAST_TAG = -1000;
+
+__host__ __device__ __forceinline__ int32_t tail_tag(int len, int32_t last) {
+    return LEN_TAG - len - (int32_t)((uint32_t)(last + 3) << 8);
+}
 constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x int4)
 #ifndef BPE_WAVES
 #define BPE_WAVES 16
@@ -144,9 +148,9 @@ __device__ __forceinline__ int32_t from_prev(int32_t x, int32_t fill) {
 }
 
 // A (token, right neighbour) pair as one word: (low 16 bits of x) << 16 | (low 16 bits of y), one
-// v_perm.  Token ids are < 55296; SEP, TOMB, TOMB_ODD and the LEN_TAG values have low halves
-// >= 0xFEF0, so they never alias one.  A LAST_TAG value (slot 254 only) can: code comparing packed
-// pairs must not trust a match involving slot 254 of a partial chunk.
+// v_perm.  Token ids are < 55296; SEP, TOMB and TOMB_ODD have low halves >= 0xFFFC, so they never
+// alias one.  A tail tag (slot 255 of a partial chunk) can: code comparing packed pairs must not
+// trust a match involving slot 255 of a partial chunk.
 __device__ __forceinline__ uint32_t pack_pair(int32_t x, int32_t y) {
     return __builtin_amdgcn_perm((uint32_t)x, (uint32_t)y, 0x05040100u);
 }
@@ -329,7 +333,7 @@ __device__ __forceinline__ View make_view(const int4 v) {
     if (__builtin_amdgcn_readlane(v.w, 63) >= SEP) {
         w.len = CHUNK;
     } else {
-        w.len = LEN_TAG - __builtin_amdgcn_readlane(v.w, 63);
+        w.len = (LEN_TAG - __builtin_amdgcn_readlane(v.w, 63)) & 255;
     }
     return w;
 }
@@ -543,18 +547,14 @@ __device__ __forceinline__ unsigned long long lanes_upto(int n, int e) {
     return m >= 64 ? ~0ull : m <= 0 ? 0ull : ((1ull << m) - 1ull);
 }
 
-// Wave-uniform facts of a freshly loaded chunk, from its tail (see LEN_TAG / LAST_TAG).
+// Wave-uniform facts of a freshly loaded chunk, from slot 255 (a live token, or the tail tag).
 __device__ __forceinline__ void finish_load(Chunk &c) {
     c.first = bcast(c.t[0], 0);
     const int32_t l3 = bcast(c.t[3], 63);
-    if (l3 >= SEP) {
-        c.len = CHUNK;
-        c.last = l3;
-    } else {
-        c.len = LEN_TAG - l3;
-        const int32_t l2 = bcast(c.t[2], 63);
-        c.last = c.len == CHUNK - 1 ? l2 : c.len ? LAST_TAG - l2 : NONE;
-    }
+    const int32_t v = LEN_TAG - l3;
+    const int live = l3 >= SEP;
+    c.len = live ? CHUNK : (v & 255);
+    c.last = live ? l3 : (v >> 8) - 3;
 }
 
 // Exact run-offset parity of every live slot (SEPs are runs of their own), and the run starts.
@@ -653,29 +653,37 @@ template <int MODE>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k) {
     const int len = w.len;
-    const int full = len == CHUNK;
     const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
+    // lane 63's bit when the chunk is partial (an integer mask, not a boolean: uniform booleans
+    // cost a lane-mask round trip per use)
+    const unsigned long long P63 = (unsigned long long)((int64_t)len - CHUNK) & (1ull << 63);
+    // slot 3 of lane 63 holds the last live slot (a partial chunk's slot 255 is its tail tag)
+    const int32_t x3 = sel(lane_in(P63), w.last, t3);
     const int32_t r3 = from_next(t0, nxt);
     const int32_t l0 = from_prev(t3, s.prev);
-    // E*: slot equals its right-hand neighbour (Em1: slot 0 equals the token before it)
-    // (no dead slot equals its neighbour, and slot 0 is live; an SEP next to an SEP only sends the
-    // chunk to the exact path)
+    // E*: slot equals its right-hand neighbour (Em1: slot 0 equals the token before it).  No
+    // dead slot equals its neighbour and slot 0 is live (an SEP next to an SEP only sends the chunk
+    // to the exact path); E3's lane-63 bit compares the last live slot with nxt.
     const unsigned long long Em1 = __ballot(t0 == l0), E0 = __ballot(t0 == t1),
-                             E1 = __ballot(t1 == t2), E2 = __ballot(t2 == t3), E3 = __ballot(t3 == r3);
+                             E1 = __ballot(t1 == t2), E2 = __ballot(t2 == t3), E3 = __ballot(x3 == r3);
     const unsigned long long trip = (E0 & (Em1 | E1)) | (E2 & (E1 | E3));
-    const int fast = (trip == 0ull) & (s.in_lead == 0) & (full | (w.last != nxt));
-    if (fast) {
+    // fast: no run of three, not in the region's first run, and a partial chunk does not end in
+    // an X X pair
+    // (readfirstlane: the compiler cannot see that in_lead is wave-uniform, and would branch on it
+    // per lane)
+    const unsigned long long lead = (uint32_t)__builtin_amdgcn_readfirstlane(s.in_lead);
+    if ((trip | (E3 & P63) | lead) == 0ull) {
         // every X X pair starts its run, so every valid pair counts
+        const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
         if (MODE == MODE_TABLE) {
             // full chunks of hot tokens only (a fresh corpus): unmasked adds
-            int hot_only = 0;
-            if (full) {
+            unsigned long long cold = 1;
+            if (P63 == 0ull) {
                 const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1),
                                         max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
-                hot_only = __ballot(mx >= (uint32_t)HOT) == 0ull;
+                cold = __ballot(mx >= (uint32_t)HOT);
             }
-            if (hot_only) {
-                const int32_t x[4] = {t0, t1, t2, t3}, y[4] = {t1, t2, t3, r3};
+            if (cold == 0ull) {
                 uint32_t o[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
@@ -690,25 +698,22 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 }
             } else {
                 // mixed planes (partial chunks hold merged tokens: the steady state)
-                const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
-                const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
                 add_pairs(x, y, k);
             }
         } else {
-            const int32_t x3 = sel(lane_in(full ? 0ull : (1ull << 63)), w.last, t3);
-            const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
 #pragma unroll
             for (int e = 0; e < 4; ++e)
                 if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
         }
-        // the parity of the last token only matters when the next chunk continues its run
-        // (a full chunk's last slot: E2's lane-63 bit says it continues its left neighbour)
+        // the last token starts its run here (a run continuing into the next chunk would be a run
+        // of three, or a partial chunk's X X end), so its offset parity is 0
         s.first_tok = s.n_live ? s.first_tok : w.first;
-        s.par = (int)((E2 >> 63) & (unsigned long long)(full & (w.last == nxt)));
+        s.par = 0;
         s.prev = w.last;
         s.n_live += len;
         return;
     }
+    const int full = len == CHUNK;
     // exact path
 #ifdef BPE_PROBE_COMMON
     s.in_lead = 0;   // (static instruction-count probe only: drop the exact path)
@@ -772,13 +777,9 @@ struct Apply {
 // (the only kind whose matches depend on run parity, so the only one carrying that code).
 enum MergeKind { NO_MERGE = 0, MERGE_XY = 1, MERGE_XX = 2 };
 
-// Writes the tail tags of a re-packed chunk (slots 254 and 255 live on lane 63).
+// Writes the tail tag of a re-packed chunk (slot 255 lives on lane 63).
 __device__ __forceinline__ void tag_tail(int32_t (&y)[4], int total, int32_t last) {
-    if (total < CHUNK) {
-        const bool l63 = lane_in(1ull << 63);
-        y[3] = sel(l63, LEN_TAG - total, y[3]);
-        if (total < CHUNK - 1) y[2] = sel(l63, total ? LAST_TAG - last : TOMB, y[2]);
-    }
+    if (total < CHUNK) y[3] = sel(lane_in(1ull << 63), tail_tag(total, last), y[3]);
 }
 
 // Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
@@ -794,7 +795,8 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
     // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)
     {
         const int32_t r3 = from_next(w.t[0], nxt);
-        const int32_t x3 = sel(lane_in(w.len == CHUNK ? 0ull : (1ull << 63)), w.last, w.t[3]);
+        const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
+        const int32_t x3 = sel(lane_in(P63), w.last, w.t[3]);
         const unsigned long long H =
             __ballot(pack_pair(w.t[0], w.t[1]) == key) | __ballot(pack_pair(w.t[1], w.t[2]) == key) |
             __ballot(pack_pair(w.t[2], w.t[3]) == key) | __ballot(pack_pair(x3, r3) == key);
@@ -1152,8 +1154,7 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
     const int w0 = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * wl;   // first of my 4 words
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                 // < 2^23 each: G <= 256 x 2^15
     const uint4 *p4 = reinterpret_cast<const uint4 *>(partials + w0);
-    for (int g = grp; g < G; g += 8) {
-        const uint4 p = p4[(size_t)g * (HIST_WORDS / 4)];
+    auto add = [&](const uint4 p) {
         acc[0] += p.x & 0xFFFFu;
         acc[1] += p.x >> 16;
         acc[2] += p.y & 0xFFFFu;
@@ -1162,7 +1163,17 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         acc[5] += p.z >> 16;
         acc[6] += p.w & 0xFFFFu;
         acc[7] += p.w >> 16;
+    };
+    int g = grp;
+    // eight slabs' loads in flight per thread, then their sums
+    for (; g + 56 < G; g += 64) {
+        uint4 p[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p[q] = p4[(size_t)(g + 8 * q) * (HIST_WORDS / 4)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) add(p[q]);
     }
+    for (; g < G; g += 8) add(p4[(size_t)g * (HIST_WORDS / 4)]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s_sum[grp][wl][i] = acc[i];
     __syncthreads();
@@ -1792,10 +1803,7 @@ __global__ void __launch_bounds__(CHUNK) k_seal(int32_t *__restrict__ ids, int64
     const int32_t last = p[len - 1];
     if (t >= len) p[t] = (t & 1) ? TOMB_ODD : TOMB;
     __syncthreads();
-    if (t == 0) {
-        p[CHUNK - 1] = LEN_TAG - len;
-        if (len < CHUNK - 1) p[CHUNK - 2] = LAST_TAG - last;
-    }
+    if (t == 0) p[CHUNK - 1] = tail_tag(len, last);
 }
 
 // ---------------------------------------------------------------------------------------------
