@@ -29,7 +29,7 @@ C_API = [
     'bpe_version', 'bpe_last_error', 'bpe_device_count', 'bpe_create', 'bpe_destroy',
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
-    'bpe_apply_merge', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
+    'bpe_apply_merge', 'bpe_apply_merges', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
     'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount', 'bpe_export_counts',
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions',
 ]
@@ -92,6 +92,7 @@ def lib():
                                 ctypes.c_int),
         'bpe_apply_merge': ([vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i64p],
                             ctypes.c_int),
+        'bpe_apply_merges': ([vp, i32p, ctypes.c_int64, i64p, ctypes.c_int], ctypes.c_int),
         'bpe_merge_until': ([vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, i64p,
                              ctypes.c_int64, i64p], ctypes.c_int),
         'bpe_stats_enable': ([vp, ctypes.c_int], ctypes.c_int),
@@ -231,6 +232,16 @@ class Engine:
         _check(lib().bpe_apply_merge(self._ctx, a, b, c, ctypes.byref(r)), 'bpe_apply_merge')
         return r.value
 
+    def apply_merges(self, merges, count_after=True):
+        """restoreMerge replay / batch encoding (bpe_apply_merges): applies the (a, b, c) triples
+        in order without counting pairs; returns the replacement counts."""
+        abc = np.ascontiguousarray(np.asarray(merges, np.int32).reshape(-1, 3))
+        rep = np.zeros(len(abc), np.int64)
+        _check(lib().bpe_apply_merges(self._ctx, abc.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                      len(abc), rep.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                      1 if count_after else 0), 'bpe_apply_merges')
+        return rep.tolist()
+
     def merge_until(self, max_length=0, min_weight=0, max_iterations=0, cap=1 << 16):
         out = np.zeros(3 * cap, np.int64)
         n = ctypes.c_int64()
@@ -297,3 +308,20 @@ class Engine:
 
     def reset_stats(self):
         _check(lib().bpe_reset_stats(self._ctx), 'bpe_reset_stats')
+
+
+def encode_samples(samples, merges, len16, device=0):
+    """Batch encoding with a trained merge list (encodeToCode, core.ts:392-409, for many texts at
+    once): the samples (base token ids) go into a fresh engine, the merges (a, b, c) are applied in
+    order by apply-only passes, and the encoded samples come back as id lists."""
+    e = Engine(device)
+    try:
+        for i, l in enumerate(len16):
+            e.set_token_len16(i, int(l))
+        for s in samples:
+            e.add_sample(s)
+        if len(merges):
+            e.apply_merges(merges, count_after=False)
+        return e.samples()
+    finally:
+        e.close()

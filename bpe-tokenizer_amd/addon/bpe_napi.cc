@@ -211,6 +211,24 @@ napi_value ApplyMerge(napi_env env, napi_callback_info info) {
     return num(env, (double)rep);
 }
 
+// applyMerges(h, Int32Array abc, countAfter): a run of (a, b, c) rewrites (bpe_apply_merges)
+napi_value ApplyMerges(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return throw_arg(env, "applyMerges(h, Int32Array, countAfter)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    napi_typedarray_type type;
+    size_t length = 0, offset = 0;
+    void *data = nullptr;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[1], &type, &length, &data, &ab, &offset) != napi_ok ||
+        type != napi_int32_array || length % 3 != 0)
+        return throw_arg(env, "applyMerges expects an Int32Array of (a, b, c) triples");
+    if (bpe_apply_merges(ctx, static_cast<const int32_t *>(data), (int64_t)(length / 3), nullptr,
+                         (int)get_i64(env, argv[2])) < 0)
+        return throw_native(env, "bpe_apply_merges");
+    return nullptr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     struct {
         const char *name;
@@ -221,6 +239,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"addLatin1", AddLatin1}, {"clearCorpus", ClearCorpus},
         {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},
         {"findNextMerge", FindNextMerge}, {"applyMerge", ApplyMerge},
+        {"applyMerges", ApplyMerges},
     };
     for (auto &f : fns) {
         napi_value fn;

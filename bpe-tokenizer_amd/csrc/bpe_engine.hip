@@ -44,6 +44,8 @@ inline void dfree(void *p) {
 
 // mergeUntil iterations the device runs per host round trip (each ends in one sync)
 constexpr int64_t LOOP_BATCH = 64;
+// apply-only replay: merges per host round trip (their replacement counts come back together)
+constexpr int64_t REPLAY_BATCH = 256;
 
 static_assert(TABLE_BINS == BPE_TABLE_BINS && HOT_BINS == BPE_HOT_BINS, "include/bpe.h table layout");
 
@@ -116,6 +118,8 @@ struct bpe_ctx {
     // device-resident mergeUntil loop: control block + merge log (pinned host mirrors)
     LoopCtl *d_ctl = nullptr, *h_ctl = nullptr;
     long long *d_log = nullptr, *h_log = nullptr;
+    // apply-only replay: per-merge replacement counts
+    unsigned long long *d_repl = nullptr, *h_repl = nullptr;
 };
 
 namespace {
@@ -577,16 +581,11 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
     return BPE_OK;
 }
 
+int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc);
+
 int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
-    if (a < 0 || b < 0 || cc < 0 || cc >= BPE_MAX_VOCAB)
-        return fail(cc >= BPE_MAX_VOCAB ? BPE_ERR_VOCAB : BPE_ERR_ARG,
-                    "bpe native: token id out of range (vocab is limited to 55295 tokens)");
-    if (a >= (int64_t)c->h_len16.size() || b >= (int64_t)c->h_len16.size())
-        return fail(BPE_ERR_ARG, "bpe native: apply_merge with an unregistered token");
     int rc;
-    if ((rc = ensure_vocab(c, (int64_t)cc + 1))) return rc;
-    c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                   // core.ts:318
-    mark_len16(c, cc);
+    if ((rc = register_merge(c, a, b, cc))) return rc;                 // core.ts:315-318
     if (replaced) *replaced = 0;
     if ((rc = settle(c))) return rc;
     if ((rc = maybe_compact(c))) return rc;
@@ -720,6 +719,95 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     return BPE_OK;
 }
 
+// Carries (RegionCarry) for the current corpus and geometry without counting pairs.
+int carry_pass(bpe_ctx *c) {
+    geometry(c);
+    hipStream_t s = c->stream;
+    k_apply<NO_MERGE><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1,
+                                          -1, c->d_sums, nullptr);
+    k_runs<MODE_NONE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, nullptr,
+                                                         c->cold, nullptr, nullptr);
+    HIP_TRY(hipGetLastError());
+    c->carry_valid = true;
+    return BPE_OK;
+}
+
+// Checks a merge (a, b) -> cc against the vocabulary and registers cc (core.ts:315-318).
+int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
+    if (a < 0 || b < 0 || cc < 0 || cc >= BPE_MAX_VOCAB)
+        return fail(cc >= BPE_MAX_VOCAB ? BPE_ERR_VOCAB : BPE_ERR_ARG,
+                    "bpe native: token id out of range (vocab is limited to 55295 tokens)");
+    if (a >= (int64_t)c->h_len16.size() || b >= (int64_t)c->h_len16.size())
+        return fail(BPE_ERR_ARG, "bpe native: apply_merge with an unregistered token");
+    int rc;
+    if ((rc = ensure_vocab(c, (int64_t)cc + 1))) return rc;
+    c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];
+    mark_len16(c, cc);
+    return BPE_OK;
+}
+
+// applyMerge without counting, for a run of merges (restoreMerge replay, core.ts:477-494; batch
+// encoding, core.ts:392-409): one apply-only streaming pass per merge (k_apply + k_runs for the
+// carries), their replacement counts read back once per REPLAY_BATCH merges.  With count_after
+// the last merge is applied by the fused apply + count pass, so a find that follows needs no
+// extra pass.  replaced (may be null) receives each merge's replacement count.
+int replay(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, bool count_after) {
+    int rc;
+    if ((rc = settle(c))) return rc;
+    const int64_t n_plain = count_after ? n - 1 : n;
+    for (int64_t i0 = 0; i0 < n_plain;) {
+        if ((rc = maybe_compact(c))) return rc;
+        if (!c->carry_valid)
+            if ((rc = carry_pass(c))) return rc;
+        const int64_t nb = std::min<int64_t>(REPLAY_BATCH, n_plain - i0);
+        for (int64_t j = 0; j < nb; ++j) {
+            const int32_t *m = abc + 3 * (i0 + j);
+            if ((rc = register_merge(c, m[0], m[1], m[2]))) return rc;
+        }
+        geometry(c);
+        hipStream_t s = c->stream;
+        HIP_TRY(hipMemsetAsync(c->d_repl, 0, nb * sizeof(unsigned long long), s));
+        for (int64_t j = 0; j < nb; ++j) {
+            const int32_t *m = abc + 3 * (i0 + j);
+            if (m[0] == m[1])
+                k_apply<MERGE_XX><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                      c->d_carry, m[0], m[1], m[2], c->d_sums,
+                                                      c->d_repl + j);
+            else
+                k_apply<MERGE_XY><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                      c->d_carry, m[0], m[1], m[2], c->d_sums,
+                                                      c->d_repl + j);
+            k_runs<MODE_NONE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                 nullptr, c->cold, nullptr, nullptr);
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_repl, c->d_repl, nb * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (int64_t j = 0; j < nb; ++j) {
+            const int32_t *m = abc + 3 * (i0 + j);
+            const int64_t R = (int64_t)c->h_repl[j];
+            c->n_live -= R;
+            c->live_slots -= R;
+            c->h_count[m[0]] -= R;
+            c->h_count[m[1]] -= R;
+            c->h_count[m[2]] += R;
+            if (R) c->packed = false;
+            if (replaced) replaced[i0 + j] = R;
+        }
+        c->counts_valid = false;
+        c->best_ready = false;
+        i0 += nb;
+    }
+    if (count_after && n > 0) {
+        const int32_t *m = abc + 3 * (n - 1);
+        int64_t R = 0;
+        if ((rc = do_apply(c, m[0], m[1], m[2], &R))) return rc;
+        if (replaced) replaced[n - 1] = R;
+    }
+    return BPE_OK;
+}
+
 int append_begin(bpe_ctx *c, int64_t extra_slots) {
     int rc;
     if ((rc = settle(c))) return rc;
@@ -785,6 +873,10 @@ int bpe_create(bpe_ctx **out, int device) {
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_repl, REPLAY_BATCH))) return bail(rc);
+    if (hipHostMalloc((void **)&c->h_repl, REPLAY_BATCH * sizeof(unsigned long long),
+                      hipHostMallocDefault) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_log, 3 * LOOP_BATCH))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_ctl, sizeof(LoopCtl), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&c->h_log, 3 * LOOP_BATCH * sizeof(long long), hipHostMallocDefault) !=
@@ -807,12 +899,13 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used,
-                    c->d_ctl, c->d_log};
+                    c->d_ctl, c->d_log, c->d_repl};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->h_log) (void)hipHostFree(c->h_log);
+    if (c->h_repl) (void)hipHostFree(c->h_repl);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &sp : c->spans) c->ev_pool.insert(c->ev_pool.end(), {sp.a, sp.b});
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1022,6 +1115,13 @@ int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *repla
     int rc = set_device(c);
     if (rc) return rc;
     return do_apply(c, a, b, cc, replaced);
+}
+
+int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, int count_after) {
+    if (!c || n < 0 || (n > 0 && !abc)) return fail(BPE_ERR_ARG, "bpe native: bad apply_merges arguments");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return replay(c, abc, n, replaced, count_after != 0);
 }
 
 int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,

@@ -51,7 +51,9 @@ constexpr int SKETCH_BINS = 16384;          // count sketch of the cold pairs (a
 constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, then the sketch
 constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword: 160 KiB, all of it
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
-enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1 };
+// What a streaming pass does with the pairs it sees: the pair table, exact counts of the cold
+// pairs in heavy sketch buckets, or nothing (apply-only replay: restoreMerge, batch encoding).
+enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1, MODE_NONE = 2 };
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -239,7 +241,7 @@ __device__ __forceinline__ bool exact_wanted(const Sink &k, int32_t x, int32_t y
 template <int MODE>
 __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32_t y,
                                                  unsigned long long n) {
-    if (n == 0) return;
+    if (n == 0 || MODE == MODE_NONE) return;
     if (MODE == MODE_TABLE) atomicAdd(&k.spill[table_index(x, y)], n);
     else if (exact_wanted<MODE>(k, x, y)) cold_add(k.ct, pair_key(x, y), (uint32_t)n);
 }
@@ -298,6 +300,7 @@ __device__ __forceinline__ void lds_fix(const Sink &k, uint32_t addr, uint32_t i
 // One counted occurrence of (x, y) (outside the streaming fast paths).
 template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
+    if (MODE == MODE_NONE) return;
     if (MODE == MODE_TABLE) {
         uint32_t addr, inc, bin;
         if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) {
@@ -649,7 +652,10 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
 // Per-slot conditions are wave masks combined with 64-bit bitwise operations and uniform
 // conditions are integers: no short-circuit operators on the common path (they become control
 // flow whose booleans round-trip through vector registers).
-template <int MODE>
+// TAIL: the region's last chunk (nxt = NONE).  It always takes the exact path: the parity of its
+// last token's run offset feeds RegionSum::trail_odd, which k_runs needs whenever that run goes on
+// in the next region, and the fast path does not work that parity out.
+template <int MODE, bool TAIL = false>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k) {
     const int len = w.len;
@@ -672,7 +678,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     // (readfirstlane: the compiler cannot see that in_lead is wave-uniform, and would branch on it
     // per lane)
     const unsigned long long lead = (uint32_t)__builtin_amdgcn_readfirstlane(s.in_lead);
-    if ((trip | (E3 & P63) | lead) == 0ull) {
+    if (!TAIL && (trip | (E3 & P63) | lead) == 0ull) {
         // every X X pair starts its run, so every valid pair counts
         const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
         if (MODE == MODE_TABLE) {
@@ -700,7 +706,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 // mixed planes (partial chunks hold merged tokens: the steady state)
                 add_pairs(x, y, k);
             }
-        } else {
+        } else if (MODE == MODE_EXACT) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
                 if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
@@ -897,10 +903,10 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     if (MODE == MODE_TABLE) {
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
-    } else {
+    } else if (MODE == MODE_EXACT) {
         for (int i = threadIdx.x; i < HEAVY_WORDS; i += WG) hist[i] = heavy_g[i];
     }
-    __syncthreads();
+    if (MODE != MODE_NONE) __syncthreads();
     Sink k;
     k.hist = hist;
     k.spill = spill;
@@ -1002,7 +1008,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 stage(S5, S6, S4, S3, c + 5);
                 stage(S6, S0, S5, S4, c + 6);
             }
-            if (S6.len) count_chunk<MODE>(S6, NONE, lane, s, k);
+            if (S6.len) count_chunk<MODE, true>(S6, NONE, lane, s, k);
         }
         if (lane == 0) {
             RegionSum o;
@@ -1034,6 +1040,18 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
     step_body<MERGE, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill, ct,
                            heavy_g, sums, replaced);
+}
+
+// Apply-only pass (restoreMerge replay, batch encoding, core.ts:477-494 / 392-409): the merge is
+// applied exactly as by k_step, and the region sums are kept (k_runs<MODE_NONE> turns them into the
+// carries of the next pass), but no pair is counted: no LDS table, no slab.
+template <int MERGE>
+__global__ void __launch_bounds__(WG)
+k_apply(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
+        const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
+        RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced) {
+    step_body<MERGE, MODE_NONE>(nullptr, ids, n_chunks, cpr, R, carry, ma, mb, mc, nullptr, nullptr,
+                                ColdTable{}, nullptr, sums, replaced);
 }
 
 // The device loop's pass: the merge to apply is the one k_decide left in the LoopCtl.

@@ -98,6 +98,8 @@ class BPETokenizer {
     this.from_vector_index = null
     Object.defineProperty(this, '_engine', { value: null, writable: true, enumerable: false })
     Object.defineProperty(this, '_registered', { value: 0, writable: true, enumerable: false })
+    // applyMerge rewrites queued for the engine, as (a, b, c) index triples
+    Object.defineProperty(this, '_pending', { value: [], writable: true, enumerable: false })
   }
 
   /** @description the HIP engine holding the corpus (created on first use) */
@@ -106,8 +108,20 @@ class BPETokenizer {
       this._engine = loadNative().createEngine(0)
       this._registered = 0
     }
+    this.flushMerges()
     this.registerTokens()
     return this._engine
+  }
+
+  /**
+   * @description runs the queued applyMerge rewrites on the engine: a run of them (restoreMerge
+   * replay) takes one apply-only pass each, the last one fused with the next count.
+   */
+  flushMerges() {
+    let pending = this._pending
+    if (pending.length === 0) return
+    this._pending = []
+    loadNative().applyMerges(this._engine, Int32Array.from(pending), 1)
   }
 
   /** @description tells the engine the UTF-16 length of every token it has not seen yet */
@@ -126,7 +140,7 @@ class BPETokenizer {
    */
   get corpus_in_code() {
     if (!this._engine) return []
-    let [ids, offsets] = loadNative().readCorpus(this._engine)
+    let [ids, offsets] = loadNative().readCorpus(this.engine())
     let samples = []
     for (let s = 0; s + 1 < offsets.length; s++) {
       let code = ''
@@ -187,6 +201,7 @@ class BPETokenizer {
     this.merge_codes = merge_codes
     this.to_vector_index = null
     this.from_vector_index = null
+    this._pending = []
     if (this._engine) loadNative().clearCorpus(this._engine)
     this._registered = 0
     for (let [chars, weight, original_weight] of json.token_table) {
@@ -322,8 +337,8 @@ class BPETokenizer {
     merge_codes.push([from_code, to_code])
 
     if (this._engine) {
-      let engine = this.engine()
-      loadNative().applyMerge(engine, a.index, b.index, c.index)
+      // (queued: the engine rewrites the corpus at its next use, see flushMerges)
+      this._pending.push(a.index, b.index, c.index)
     }
   }
 

@@ -101,6 +101,16 @@ int bpe_find_next_merge(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, in
  * `replaced` (may be NULL) receives the replacement count (== W for a merge from findNextMerge). */
 int bpe_apply_merge(bpe_ctx *ctx, int32_t a, int32_t b, int32_t c, int64_t *replaced);
 
+/* A run of applyMerge rewrites without counting pairs: restoreMerge replay (core.ts:477-494,
+ * `example/import-merge-log-to-ram.ts`) and batch encoding of a corpus with a trained merge list
+ * (encodeToCode, core.ts:392-409, applies the merges in order with replaceAll).  abc holds n
+ * triples (a, b, c), applied in order, each registering c as bpe_apply_merge does.  One
+ * apply-only streaming pass per merge.  count_after != 0: the last merge is applied by the fused
+ * apply + count pass, so a findNextMerge that follows streams nothing extra.  replaced (may be
+ * NULL) receives n replacement counts. */
+int bpe_apply_merges(bpe_ctx *ctx, const int32_t *abc, int64_t n, int64_t *replaced,
+                     int count_after);
+
 /* mergeUntil (core.ts:365-383).  max_iterations 0 = unlimited.  New tokens get ids
  * bpe_num_tokens(), bpe_num_tokens()+1, ...  (core.ts:315).  Writes (a, b, W) int64 triples into
  * out_abw (capacity `cap` triples) and the number of merges into *n_merges. */

@@ -254,3 +254,85 @@ def test_ties_resolved_from_the_corpus_tail(early):
     e, got = run_engine([seq], len16, {'min_weight': 2, 'max_iterations': 8})
     assert got == want
     assert e.samples() == st.samples()
+
+
+def _flat(samples):
+    ids = np.concatenate(samples).astype(np.int32) if samples else np.zeros(0, np.int32)
+    return ids, np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64)
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_apply_merges_replays_a_merge_log(seed):
+    """restoreMerge replay (core.ts:477-494) through bpe_apply_merges: the apply-only passes rewrite
+    the corpus exactly as the oracle's sequential applyMerge, with replacement counts == W; with
+    count_after, the merging that follows continues exactly as the oracle's."""
+    rng = random.Random(100 + seed)
+    alphabet = rng.choice([2, 3, 20, 256, 300])
+    samples = random_corpus(rng, rng.choice([5000, 200000, 2500000]), alphabet,
+                            rng.choice([0.0, 0.3, 0.7]), rng.choice([1, 5, 60]))
+    len16 = [rng.choice([1, 2]) for _ in range(alphabet)]
+    ids, off = _flat(samples)
+    st = OracleState(ids, off, len16, alphabet)
+    log = st.merge_until(0, 2, 40)
+    more = st.merge_until(0, 2, 10)
+    abc = [(a, b, alphabet + i) for i, (a, b, _) in enumerate(log)]
+    e = pkg.Engine(0)
+    for i, l in enumerate(len16):
+        e.set_token_len16(i, l)
+    for s in samples:
+        e.add_sample(s)
+    count_after = seed % 2 == 0
+    rep = e.apply_merges(abc, count_after=count_after)
+    assert rep == [w for _, _, w in log]
+    st2 = OracleState(ids, off, len16, alphabet)
+    for a, b, _ in log:
+        st2.apply_merge(a, b)
+    assert e.samples() == st2.samples()
+    n_tokens = alphabet + len(log)
+    got = []
+    for _ in range(10):
+        m = e.find_next_merge(0, 2)
+        if m is None:
+            break
+        assert e.apply_merge(m[0], m[1], n_tokens) == m[2]
+        n_tokens += 1
+        got.append(m)
+    assert got == more
+    e.close()
+
+
+def test_encode_samples_with_a_trained_merge_list():
+    """Batch encodeToCode (core.ts:392-409) of unseen texts with the merges trained on another
+    corpus: equal to applying the merges in order with the oracle."""
+    rng = random.Random(7)
+    alphabet = 40
+    train = random_corpus(rng, 300000, alphabet, 0.3, 20)
+    len16 = [1] * alphabet
+    ids, off = _flat(train)
+    log = OracleState(ids, off, len16, alphabet).merge_until(0, 2, 120)
+    abc = [(a, b, alphabet + i) for i, (a, b, _) in enumerate(log)]
+    texts = random_corpus(random.Random(8), 2_000_000, alphabet, 0.3, 300) + [np.zeros(0, np.int32)]
+    got = pkg.encode_samples(texts, abc, len16)
+    tid, toff = _flat(texts)
+    st = OracleState(tid, toff, len16, alphabet)
+    for a, b, _ in log:
+        st.apply_merge(a, b)
+    assert got == st.samples()
+
+
+def test_runs_across_region_boundaries_from_a_fast_chunk():
+    """x x | x y at every region boundary (two chunks per region): the trailing run of each
+    region has even length, which only the exact path of the region's last chunk works out
+    (RegionSum.trail_odd -> k_runs).  A wrong parity counts one (x, x) too many per boundary."""
+    n = 1_500_000                                   # 5860 chunks: two per region
+    rng = np.random.default_rng(3)
+    seq = rng.integers(0, 3000, n, dtype=np.int32)
+    x, y = 3000, 3001
+    for r in range(1, (n + 1) // 512):
+        p = 512 * r
+        seq[p - 3:p + 2] = [3002, x, x, x, y]
+    st = OracleState(seq, np.array([0, n], np.int64), [1] * 3003, 3003)
+    want = st.merge_until(0, 2, 3)
+    e, got = run_engine([seq], [1] * 3003, {'min_weight': 2, 'max_iterations': 3})
+    assert got == want
+    assert e.samples() == st.samples()
