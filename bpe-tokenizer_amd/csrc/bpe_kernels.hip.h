@@ -659,6 +659,18 @@ template <int MODE, bool TAIL = false>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k) {
     const int len = w.len;
+    if (MODE == MODE_NONE && !TAIL) {
+        // apply-only passes keep only the region sums: the chunk needs work only in the region's
+        // first run, or when its last token's run goes on in the next chunk (its parity)
+        const uint32_t lead0 = (uint32_t)__builtin_amdgcn_readfirstlane(s.in_lead);
+        if ((lead0 | (uint32_t)(w.last == nxt)) == 0u) {
+            s.first_tok = s.n_live ? s.first_tok : w.first;
+            s.par = 0;
+            s.prev = w.last;
+            s.n_live += len;
+            return;
+        }
+    }
     const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
     // lane 63's bit when the chunk is partial (an integer mask, not a boolean: uniform booleans
     // cost a lane-mask round trip per use)
