@@ -49,6 +49,11 @@ constexpr int HOT = 256;                    // ids < HOT form the dense LDS hist
 constexpr int HOT_BINS = HOT * HOT;
 constexpr int SKETCH_BINS = 16384;          // count sketch of the cold pairs (an id >= HOT)
 constexpr int TABLE_BINS = HOT_BINS + SKETCH_BINS;   // [0, 64K) exact hot pairs, then the sketch
+// Hot pair (a, b) sits at table bin b * 256 + a: the order of the LDS table's 16-bit counters
+// (dword (b << 7) | (a >> 1), half a & 1), so the reduction writes the table contiguously.
+__host__ __device__ constexpr uint32_t hot_bin(uint32_t a, uint32_t b) { return (b << 8) | a; }
+__host__ __device__ constexpr int32_t bin_a(uint32_t bin) { return (int32_t)(bin & 255); }
+__host__ __device__ constexpr int32_t bin_b(uint32_t bin) { return (int32_t)(bin >> 8); }
 constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword: 160 KiB, all of it
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
 // What a streaming pass does with the pairs it sees: the pair table, exact counts of the cold
@@ -214,7 +219,7 @@ __device__ __forceinline__ uint32_t sketch_bucket(int32_t x, int32_t y) {
 // Table index of a pair: its exact bin when both ids are hot, else its sketch bucket.
 // Branch-free: both forms are computed and selected.
 __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
-    const uint32_t hot = ((uint32_t)x << 8) | (uint32_t)y;
+    const uint32_t hot = hot_bin((uint32_t)x, (uint32_t)y);
     const uint32_t cold = HOT_BINS + sketch_bucket(x, y);
     return ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT ? (int)hot : (int)cold;
 }
@@ -306,7 +311,7 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) 
         if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) {
             addr = hot_addr(x, y);
             inc = hot_inc(x);
-            bin = ((uint32_t)x << 8) | (uint32_t)y;
+            bin = hot_bin((uint32_t)x, (uint32_t)y);
         } else {
             addr = cold_addr(sketch_hash(x, y));
             inc = hot_inc(x);
@@ -711,7 +716,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                     for (int e = 0; e < 4; ++e) {
                         int32_t xx = x[e], yy = y[e];
                         asm volatile("" : "+v"(xx), "+v"(yy));
-                        lds_fix(k, hot_addr(xx, yy), hot_inc(xx), ((uint32_t)xx << 8) | (uint32_t)yy, o[e]);
+                        lds_fix(k, hot_addr(xx, yy), hot_inc(xx), hot_bin((uint32_t)xx, (uint32_t)yy), o[e]);
                     }
                 }
             } else {
@@ -1173,6 +1178,9 @@ static_assert(HIST_WORDS % REDUCE_WORDS_PER_BLOCK == 0, "reduce tiling");
 __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len16,
                                         int64_t max_length);
 
+// A block owns 128 dwords (256 bins): 32 lanes x 4 dwords (512 contiguous bytes of a slab per
+// lane group), each of its 8 lane groups summing every 8th slab with eight 16-B loads in flight.
+// (Narrower column tiles, reading many slabs per wave-instruction, ran 2-3x slower.)
 __global__ void __launch_bounds__(256)
 k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ spill,
                unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
@@ -1195,7 +1203,6 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         acc[7] += p.w >> 16;
     };
     int g = grp;
-    // eight slabs' loads in flight per thread, then their sums
     for (; g + 56 < G; g += 64) {
         uint4 p[8];
 #pragma unroll
@@ -1212,16 +1219,14 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) sum += s_sum[q][bl][bi];
-    // hot dword w holds pairs ((w & 127) * 2 + half, w >> 7); sketch dwords hold buckets in order
-    const int wi = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * bl + (bi >> 1);
-    const int hf = bi & 1;
-    const int bin = wi < HOT_BINS / 2 ? (((((wi & 127) << 1) | hf) << 8) | (wi >> 7)) : 2 * wi + hf;
+    // dword w holds bins 2w and 2w + 1 (hot pairs and sketch buckets alike): contiguous writes
+    const int bin = blockIdx.x * (2 * REDUCE_WORDS_PER_BLOCK) + t;
     const unsigned long long v = (unsigned long long)sum + spill[bin];
     table[bin] = v;
     spill[bin] = 0;
     unsigned long long k = 0;
-    if (bin < HOT_BINS && v && pair_ok(bin >> 8, bin & 255, len16, max_length))
-        k = pack_key(v, bin >> 8, bin & 255);
+    if (bin < HOT_BINS && v && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
+        k = pack_key(v, bin_a(bin), bin_b(bin));
     k = wave_max_u64(k);
     if ((t & 63) == 0 && k) atomicMax(&res->best, k);
 }
@@ -1254,8 +1259,8 @@ __global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
                              const int32_t *__restrict__ len16, int64_t max_length, Result *res) {
     const int bin = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long k = 0;
-    if (bin < HOT_BINS && pair_ok(bin >> 8, bin & 255, len16, max_length))
-        k = pack_key(hot_counts[bin], bin >> 8, bin & 255);
+    if (bin < HOT_BINS && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
+        k = pack_key(hot_counts[bin], bin_a(bin), bin_b(bin));
     k = wave_max_u64(k);
     if ((threadIdx.x & 63) == 0 && k) atomicMax(&res->best, k);
 }
@@ -1288,7 +1293,7 @@ __global__ void __launch_bounds__(1024) k_select(const unsigned long long *__res
     const int t = threadIdx.x;
     unsigned long long best = 0;
     for (int bin = t; bin < HOT_BINS; bin += 1024) {
-        const int32_t a = bin >> 8, b = bin & 255;
+        const int32_t a = bin_a(bin), b = bin_b(bin);
         if (!pair_ok(a, b, len16, max_length)) continue;
         const unsigned long long k = pack_key(table[bin], a, b);
         best = k > best ? k : best;
@@ -1301,7 +1306,7 @@ __global__ void __launch_bounds__(1024) k_select(const unsigned long long *__res
     for (int i = 0; i < 16; ++i) best = s_best[i] > best ? s_best[i] : best;
     if (best)
         for (int bin = t; bin < HOT_BINS; bin += 1024) {
-            const int32_t a = bin >> 8, b = bin & 255;
+            const int32_t a = bin_a(bin), b = bin_b(bin);
             if (pair_ok(a, b, len16, max_length) && pack_key(table[bin], a, b) == best) {
                 const unsigned i = atomicAdd(&s_n, 1u);
                 if (i < CAND_CAP) cand[i] = make_int2(a, b);
@@ -1338,7 +1343,7 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
     const int idx = blockIdx.x * 256 + threadIdx.x;   // grid covers TABLE_BINS exactly
     const unsigned long long best = res->best;
     if (idx < HOT_BINS) {
-        const int32_t a = idx >> 8, b = idx & 255;
+        const int32_t a = bin_a(idx), b = bin_b(idx);
         if (best && pack_key(table[idx], a, b) == best && pair_ok(a, b, len16, max_length)) {
             const unsigned i = atomicAdd(&res->n_cand, 1u);
             if (i < CAND_CAP) cand[i] = make_int2(a, b);
@@ -1458,7 +1463,7 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
     if (best == 0) return;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid < HOT_BINS) {
-        const int32_t a = tid >> 8, b = tid & 255;
+        const int32_t a = bin_a(tid), b = bin_b(tid);
         if (pair_ok(a, b, len16, max_length) && pack_key(hot_counts[tid], a, b) == best)
             push_cand(res, cand, a, b);
     }
@@ -1506,7 +1511,7 @@ __global__ void k_collect_list(const unsigned long long *__restrict__ hot,
     if (best == 0) return;
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (tid < HOT_BINS) {
-        const int32_t a = (int32_t)(tid >> 8), b = (int32_t)(tid & 255);
+        const int32_t a = bin_a((uint32_t)tid), b = bin_b((uint32_t)tid);
         if (pair_ok(a, b, len16, max_length) && pack_key(hot[tid], a, b) == best)
             push_cand(res, cand, a, b);
     }
