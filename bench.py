@@ -9,7 +9,8 @@ synthetic latin1 corpus (xorshift32 seed 12345, 256-char alphabet, 1 MiB samples
 merges, then the remaining K = 7995 merges of the config are timed (every pass, tie pass and
 exact pass of the run is inside the timed region).
 With N > 1 GPUs each rank holds its own contiguous 1 GiB shard of one corpus stream (weak
-scaling); the per-iteration pair-count exchange is an RCCL all-reduce (bpe-tokenizer_amd/sharded.py).
+scaling); the per-iteration pair-count exchange is an RCCL all-reduce enqueued on the engine's
+stream between the selection and apply kernels (the rank loop, bpe-tokenizer_amd/sharded.py).
 
 Prints ONE JSON line (rank 0).
 """

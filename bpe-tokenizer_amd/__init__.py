@@ -31,10 +31,13 @@ C_API = [
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_apply_merges', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
     'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount', 'bpe_export_counts',
-    'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions',
+    'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions', 'bpe_rank_loop_begin',
+    'bpe_rank_loop_select', 'bpe_rank_loop_decide', 'bpe_rank_loop_count', 'bpe_rank_loop_end',
 ]
 HOT_BINS = 65536
 TABLE_BINS = 81920
+MAX_CAND = 16       # BPE_MAX_CAND
+LOOP_BATCH = 64     # BPE_LOOP_BATCH
 
 
 class BpeError(RuntimeError):
@@ -105,6 +108,13 @@ def lib():
         'bpe_select_counts': ([vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                i32p, ctypes.c_int64, i64p, i64p], ctypes.c_int),
         'bpe_tie_positions': ([vp, i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)],
+                              ctypes.c_int),
+        'bpe_rank_loop_begin': ([vp, ctypes.c_int64, ctypes.c_int64, vp, vp, ctypes.c_int],
+                                ctypes.c_int),
+        'bpe_rank_loop_select': ([vp], ctypes.c_int),
+        'bpe_rank_loop_decide': ([vp], ctypes.c_int),
+        'bpe_rank_loop_count': ([vp], ctypes.c_int),
+        'bpe_rank_loop_end': ([vp, i64p, ctypes.c_int64, i64p, ctypes.POINTER(ctypes.c_int)],
                               ctypes.c_int),
         'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                               ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
@@ -301,6 +311,36 @@ class Engine:
                                        len(cands), last.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
                'bpe_tie_positions')
         return last
+
+    # device-resident loop on one rank (bpe.h: bpe_rank_loop_*); the caller all-reduces `table`
+    # and `tie` in order on stream() between the calls
+    def stream(self):
+        st = ctypes.c_void_p()
+        _check(lib().bpe_get_stream(self._ctx, ctypes.byref(st)), 'bpe_get_stream')
+        return st.value or 0
+
+    def rank_loop_begin(self, max_length, min_weight, table_ptr, tie_ptr, rank):
+        _check(lib().bpe_rank_loop_begin(self._ctx, int(max_length or 0), int(min_weight or 0),
+                                         table_ptr, tie_ptr, rank), 'bpe_rank_loop_begin')
+
+    def rank_loop_select(self):
+        _check(lib().bpe_rank_loop_select(self._ctx), 'bpe_rank_loop_select')
+
+    def rank_loop_decide(self):
+        _check(lib().bpe_rank_loop_decide(self._ctx), 'bpe_rank_loop_decide')
+
+    def rank_loop_count(self):
+        _check(lib().bpe_rank_loop_count(self._ctx), 'bpe_rank_loop_count')
+
+    def rank_loop_end(self):
+        """Syncs; returns ([(a, b, W)] merged in this batch, status) with status 0 = run on,
+        1 = no pair qualifies, 2 = the next iteration needs the host protocol."""
+        out = np.zeros(3 * LOOP_BATCH, np.int64)
+        n, st = ctypes.c_int64(), ctypes.c_int()
+        _check(lib().bpe_rank_loop_end(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                       LOOP_BATCH, ctypes.byref(n), ctypes.byref(st)),
+               'bpe_rank_loop_end')
+        return [tuple(int(v) for v in out[3 * i:3 * i + 3]) for i in range(n.value)], st.value
 
     def recount(self):
         """One plain streaming count pass (K1 alone; measurement helper)."""

@@ -48,6 +48,7 @@ constexpr int64_t LOOP_BATCH = 64;
 constexpr int64_t REPLAY_BATCH = 256;
 
 static_assert(TABLE_BINS == BPE_TABLE_BINS && HOT_BINS == BPE_HOT_BINS, "include/bpe.h table layout");
+static_assert(MAX_CAND == BPE_MAX_CAND && LOOP_BATCH == BPE_LOOP_BATCH, "include/bpe.h rank loop sizes");
 
 template <typename T>
 int dev_alloc(T **p, size_t n) {
@@ -120,6 +121,11 @@ struct bpe_ctx {
     long long *d_log = nullptr, *h_log = nullptr;
     // apply-only replay: per-merge replacement counts
     unsigned long long *d_repl = nullptr, *h_repl = nullptr;
+    // sharded device loop (one rank): the caller's all-reduced table and tie positions
+    unsigned long long *rl_table = nullptr, *rl_tie = nullptr;
+    int rl_rank = 0;
+    int64_t rl_base = 0, rl_enqueued = 0, rl_max_length = 0;
+    bool rl_open = false;
 };
 
 namespace {
@@ -649,9 +655,9 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         hipEvent_t e_sel = span_begin(c);
         k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res,
                                                         c->d_cand, c->d_heavy, c->d_ctl);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
         k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr);
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
@@ -671,7 +677,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     }
     HIP_TRY(hipMemcpyAsync(h, c->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(c->h_log, c->d_log, 3 * n * sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_log, c->d_log, LOG_WORDS * n * sizeof(long long),
+                           hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const int64_t nd = h->n_done;
     if (h->status == LOOP_ERROR)
@@ -684,8 +691,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     c->h_len16.resize(base + nd, 1);
     c->h_count.resize(base + nd, 0);
     for (int64_t i = 0; i < nd; ++i) {
-        const int32_t a = (int32_t)c->h_log[3 * i], b = (int32_t)c->h_log[3 * i + 1];
-        const int64_t W = c->h_log[3 * i + 2];
+        const int32_t a = (int32_t)c->h_log[LOG_WORDS * i], b = (int32_t)c->h_log[LOG_WORDS * i + 1];
+        const int64_t W = c->h_log[LOG_WORDS * i + 2];
         const int64_t cc = base + i;
         c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                // core.ts:318
         if (c->stats_on) {
@@ -709,11 +716,173 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     }
     c->len16_lo = base + nd;   // k_decide wrote the new lengths on the device
     if (c->stats_on) c->stats.tie_passes += h->n_tie;
-    c->last_replaced = nd ? c->h_log[3 * (nd - 1) + 2] : c->last_replaced;
+    c->last_replaced = nd ? c->h_log[LOG_WORDS * (nd - 1) + 2] : c->last_replaced;
     // every early-ended batch leaves the last reduce's best key in the Result
     c->best_ready = true;
     c->best_ml = max_length;
     c->counts_valid = c->carry_valid = true;
+    *n_done = nd;
+    *status = h->status;
+    return BPE_OK;
+}
+
+// ---- the device loop on one rank of a sharded corpus ------------------------
+// Per iteration the caller enqueues, on this context's stream: all-reduce(SUM) of `table`,
+// rank_loop_select, all-reduce(MAX) of `tie`, rank_loop_decide, rank_loop_count.  Nothing syncs
+// the host until rank_loop_end, which reads the batch's merges back.
+int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *table,
+                    unsigned long long *tie, int rank) {
+    int rc;
+    if ((rc = settle(c))) return rc;
+    if ((rc = maybe_compact(c))) return rc;
+    c->opt_max_length = max_length;
+    if (!c->counts_valid || !c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    const int64_t base = (int64_t)c->h_len16.size();
+    if ((rc = ensure_len16_cap(c, base + LOOP_BATCH))) return rc;
+    if (c->len16_lo < base) {
+        HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
+                               (base - c->len16_lo) * sizeof(int32_t), hipMemcpyHostToDevice,
+                               c->stream));
+        c->len16_lo = base;
+    }
+    geometry(c);
+    hipStream_t s = c->stream;
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    LoopCtl *h = c->h_ctl;
+    memset(h, 0, sizeof *h);
+    h->status = LOOP_RUN;
+    h->next_id = (int32_t)base;
+    h->w = -1;
+    h->min_weight = min_weight == 0 ? 2 : min_weight;                   // core.ts:256
+    h->sharded = 1;
+    HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
+    // this shard's table, to be summed over the ranks
+    HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
+                           hipMemcpyDeviceToDevice, s));
+    c->rl_table = table;
+    c->rl_tie = tie;
+    c->rl_rank = rank;
+    c->rl_base = base;
+    c->rl_enqueued = 0;
+    c->rl_max_length = max_length;
+    c->rl_open = true;
+    c->best_ready = false;
+    return BPE_OK;
+}
+
+// From the all-reduced table: the best key, its pairs, the decision (or the tie pass, whose
+// positions go to `tie` for the all-reduce(MAX)).
+int rank_loop_select(bpe_ctx *c) {
+    if (!c->rl_open || c->rl_enqueued >= LOOP_BATCH)
+        return fail(BPE_ERR_STATE, "bpe native: rank loop not begun, or its batch is full");
+    hipStream_t s = c->stream;
+    const int64_t ml = c->rl_max_length;
+    hipEvent_t e_sel = span_begin(c);
+    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->rl_table, c->d_len16, ml, c->d_res, c->d_ctl);
+    k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->rl_table, c->d_len16, ml, c->d_res,
+                                                    c->d_cand, c->d_heavy, c->d_ctl);
+    k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
+    TieArgs A;
+    memset(&A, 0, sizeof A);
+    A.ids = c->d_ids;
+    A.n_chunks = c->n_chunks;
+    A.cpr = c->cpr;
+    A.R = c->R;
+    A.carry = c->d_carry;
+    A.cand = c->d_cand;
+    A.res = c->d_res;
+    A.ctl = c->d_ctl;
+    k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
+    k_tie_export<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->rl_tie, c->rl_rank);
+    HIP_TRY(hipGetLastError());
+    return span_end(c, e_sel, 1);
+}
+
+// After the all-reduce(MAX) of `tie`: the decision of a tied iteration.
+int rank_loop_decide(bpe_ctx *c) {
+    if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    k_decide<<<1, 64, 0, c->stream>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1,
+                                      c->rl_tie);
+    HIP_TRY(hipGetLastError());
+    return BPE_OK;
+}
+
+// Applies the decided merge to this shard and counts it: this shard's table into `table`.
+int rank_loop_count(bpe_ctx *c) {
+    if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    hipStream_t s = c->stream;
+    hipEvent_t e_step = span_begin(c);
+    k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
+                                    c->d_partials, c->d_spill, c->cold, c->d_sums,
+                                    &c->d_res->replaced);
+    HIP_TRY(hipGetLastError());
+    int rc;
+    if ((rc = span_end(c, e_step, 0))) return rc;
+    hipEvent_t e_red = span_begin(c);
+    k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
+                                                          c->cold, c->d_heavy, c->d_ctl);
+    k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->rl_max_length, nullptr, c->d_ctl);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->rl_table, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
+                           hipMemcpyDeviceToDevice, s));
+    c->rl_enqueued += 1;
+    return span_end(c, e_red, 1);
+}
+
+// Syncs, reads the batch's merges back (out_abw: (a, b, W) triples) and updates the host tables
+// with this shard's replacement counts.  *status: LOOP_RUN (every enqueued iteration merged),
+// LOOP_DONE (no pair qualifies), LOOP_HOST (the next iteration needs the host protocol).
+int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, int *status) {
+    if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    c->rl_open = false;
+    hipStream_t s = c->stream;
+    LoopCtl *h = c->h_ctl;
+    HIP_TRY(hipMemcpyAsync(h, c->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_log, c->d_log, LOG_WORDS * LOOP_BATCH * sizeof(long long),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->status == LOOP_ERROR) return fail(BPE_ERR_STATE, "bpe native: rank loop: tie pass found no occurrence");
+    const int64_t nd = h->n_done;
+    if (nd < 0 || nd > c->rl_enqueued) return fail(BPE_ERR_STATE, "bpe native: rank loop: bad merge count");
+    const int64_t base = c->rl_base;
+    c->h_len16.resize(base + nd, 1);
+    c->h_count.resize(base + nd, 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        const long long *m = c->h_log + LOG_WORDS * i;
+        const int32_t a = (int32_t)m[0], b = (int32_t)m[1];
+        const int64_t W = m[2];
+        // this shard's replacement count (the last merge's is still in the Result)
+        const int64_t R = m[3] >= 0 ? m[3] : (int64_t)c->h_res->replaced;
+        const int64_t cc = base + i;
+        c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                // core.ts:318
+        if (c->stats_on) {
+            c->stats.iterations += 1;
+            c->stats.live_tokens += c->n_live;
+        }
+        c->n_live -= R;
+        c->live_slots -= R;
+        c->h_count[a] -= R;
+        c->h_count[b] -= R;
+        c->h_count[cc] += R;
+        if (R) c->packed = false;
+        if (c->stats_on) {
+            c->stats.step_launches += 1;
+            c->stats.step_slots += c->n_chunks * CHUNK;
+            c->stats.step_live += c->n_live;
+        }
+        if (i < cap) {
+            out_abw[3 * i] = a;
+            out_abw[3 * i + 1] = b;
+            out_abw[3 * i + 2] = W;
+        }
+    }
+    c->len16_lo = base + nd;
+    if (c->stats_on) c->stats.tie_passes += h->n_tie;
+    c->counts_valid = c->carry_valid = true;   // d_hot: this shard's table after the last merge
+    c->best_ready = false;
     *n_done = nd;
     *status = h->status;
     return BPE_OK;
@@ -877,9 +1046,9 @@ int bpe_create(bpe_ctx **out, int device) {
     if (hipHostMalloc((void **)&c->h_repl, REPLAY_BATCH * sizeof(unsigned long long),
                       hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
-    if ((rc = dev_alloc(&c->d_log, 3 * LOOP_BATCH))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_log, LOG_WORDS * LOOP_BATCH))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_ctl, sizeof(LoopCtl), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_log, 3 * LOOP_BATCH * sizeof(long long), hipHostMallocDefault) !=
+        hipHostMalloc((void **)&c->h_log, LOG_WORDS * LOOP_BATCH * sizeof(long long), hipHostMallocDefault) !=
             hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipMemset(c->d_cold_flags, 0, 16) != hipSuccess)
@@ -1115,6 +1284,40 @@ int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *repla
     int rc = set_device(c);
     if (rc) return rc;
     return do_apply(c, a, b, cc, replaced);
+}
+
+int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint64_t *table,
+                        uint64_t *tie, int rank) {
+    if (!c || !table || !tie || rank < 0) return fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return rank_loop_begin(c, max_length, min_weight, (unsigned long long *)table,
+                           (unsigned long long *)tie, rank);
+}
+
+int bpe_rank_loop_select(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    return rc ? rc : rank_loop_select(c);
+}
+
+int bpe_rank_loop_decide(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    return rc ? rc : rank_loop_decide(c);
+}
+
+int bpe_rank_loop_count(bpe_ctx *c) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    int rc = set_device(c);
+    return rc ? rc : rank_loop_count(c);
+}
+
+int bpe_rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status) {
+    if (!c || !n_merges || !status || (cap > 0 && !out_abw))
+        return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    return rc ? rc : rank_loop_end(c, out_abw, cap, n_merges, status);
 }
 
 int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, int count_after) {

@@ -114,8 +114,14 @@ struct LoopCtl {
     int64_t w;            // its weight (-1: no merge applied yet in this batch)
     int64_t n_done;       // merges decided in this batch (entries of the log)
     int64_t min_weight;   // after the core.ts:256 default
-    int64_t n_tie;        // tie passes run in this batch
+    int32_t n_tie;        // tie passes run in this batch
+    // one rank of a sharded corpus: W is global (this shard's replacement count is logged, not
+    // checked), ties take the full pass and their positions come from the all-reduced tie table
+    int32_t sharded;
 };
+
+// Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
+constexpr int LOG_WORDS = 4;
 
 __device__ __forceinline__ bool loop_off(const LoopCtl *ctl) {
     return ctl && ctl->status != LOOP_RUN;
@@ -1228,7 +1234,7 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
     if (bin < HOT_BINS && v && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
         k = pack_key(v, bin_a(bin), bin_b(bin));
     k = wave_max_u64(k);
-    if ((t & 63) == 0 && k) atomicMax(&res->best, k);
+    if ((t & 63) == 0 && k && res) atomicMax(&res->best, k);
 }
 
 // Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there
@@ -1256,7 +1262,9 @@ __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len
 
 // argmax over the dense hot table: best = max packed key.
 __global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
-                             const int32_t *__restrict__ len16, int64_t max_length, Result *res) {
+                             const int32_t *__restrict__ len16, int64_t max_length, Result *res,
+                             const LoopCtl *ctl = nullptr) {
+    if (loop_off(ctl)) return;
     const int bin = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long k = 0;
     if (bin < HOT_BINS && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
@@ -1368,17 +1376,21 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
 // candidates), or decides.  phase 1, after k_tie: the candidate whose last counted occurrence is
 // earliest (rule R3).  A decision logs (a, b, W), registers the new token's UTF-16 length
 // (core.ts:318) and clears the Result for the next pass.  One thread.
-__global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ cand,
-                         int32_t *len16, long long *log, int phase) {
+__global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
+                         long long *log, int phase, const unsigned long long *__restrict__ tie_pos) {
     if (threadIdx.x != 0 || ctl->status != LOOP_RUN) return;
     const unsigned long long best = res->best;
     const long long W = (long long)(best >> 17);
     const unsigned n = res->n_cand;
     int32_t a = -1, b = -1;
     if (phase == 0) {
-        if (ctl->w >= 0 && res->replaced != (unsigned long long)ctl->w) {
-            ctl->status = LOOP_ERROR;
-            return;
+        if (ctl->w >= 0) {
+            // the previous merge's replacement count: == W on the whole corpus, logged per shard
+            if (!ctl->sharded && res->replaced != (unsigned long long)ctl->w) {
+                ctl->status = LOOP_ERROR;
+                return;
+            }
+            log[LOG_WORDS * (ctl->n_done - 1) + 3] = (long long)res->replaced;
         }
         ctl->w = -1;
         if (best == 0 || W < ctl->min_weight) {                   // core.ts:312-313
@@ -1390,8 +1402,16 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
             return;
         }
         if (n > 1) {
-            // X Y candidates only: the tail window first; else the full pass
-            int all_xy = 1;
+            // the same candidate order on every rank (the collection order is not): by (a, b)
+            for (unsigned j = 1; j < n; ++j) {
+                const int2 v = cand[j];
+                unsigned i = j;
+                for (; i > 0 && (cand[i - 1].x > v.x || (cand[i - 1].x == v.x && cand[i - 1].y > v.y)); --i)
+                    cand[i] = cand[i - 1];
+                cand[i] = v;
+            }
+            // X Y candidates only (one corpus): the tail window first; else the full pass
+            int all_xy = !ctl->sharded;
             for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
             for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
             ctl->tie = all_xy ? 1 : 2;
@@ -1405,7 +1425,7 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
         unsigned long long bp = ~0ull;
         unsigned missing = 0;
         for (unsigned j = 0; j < n; ++j) {
-            const unsigned long long p = res->last[j];
+            const unsigned long long p = tie_pos ? tie_pos[j] : res->last[j];
             if (p && p < bp) {
                 bp = p;
                 a = cand[j].x;
@@ -1421,7 +1441,7 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
             }
             // the only one missing occurs only earlier: its last occurrence is the earliest
             for (unsigned j = 0; j < n; ++j)
-                if (res->last[j] == 0) {
+                if ((tie_pos ? tie_pos[j] : res->last[j]) == 0) {
                     a = cand[j].x;
                     b = cand[j].y;
                 }
@@ -1435,9 +1455,10 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, const int2 *__restrict__ can
     const int32_t c = ctl->next_id;
     len16[c] = len16[a] + len16[b];
     const long long i = ctl->n_done;
-    log[3 * i] = a;
-    log[3 * i + 1] = b;
-    log[3 * i + 2] = W;
+    log[LOG_WORDS * i] = a;
+    log[LOG_WORDS * i + 1] = b;
+    log[LOG_WORDS * i + 2] = W;
+    log[LOG_WORDS * i + 3] = -1;   // (filled in by the next decision or at the batch end)
     ctl->a = a;
     ctl->b = b;
     ctl->c = c;
@@ -1773,6 +1794,19 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
             if (j < ts.n && ts.pos[j])
                 atomicMax(&A.res->last[j], (unsigned long long)(c0 * CHUNK + ts.pos[j]));
     }
+}
+
+// Sharded loop: this shard's last tie positions as corpus-wide ones (rank << 40 | position; 0:
+// none) for the all-reduce(MAX) that follows.  One thread per candidate slot.
+constexpr int RANK_SHIFT = 40;
+__global__ void k_tie_export(const LoopCtl *ctl, const Result *res, unsigned long long *tie_pos,
+                             int rank) {
+    const int j = threadIdx.x;
+    if (j >= MAX_CAND) return;
+    unsigned long long v = 0;
+    if (ctl->status == LOOP_RUN && ctl->tie == 2 && res->last[j])
+        v = ((unsigned long long)rank << RANK_SHIFT) | res->last[j];
+    tie_pos[j] = v;
 }
 
 // ---------------------------------------------------------------------------------------------

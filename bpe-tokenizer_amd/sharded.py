@@ -14,6 +14,12 @@ counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exc
 Every rank then selects the same merge (libbpe's argmax over the global tables) and applies it to
 its own shard.  world == 1 is the plain single-GPU loop.
 
+ShardedTrainer.run() keeps that exchange on the device (libbpe's rank loop, include/bpe.h
+bpe_rank_loop_*): per iteration the table all-reduce(SUM), the selection kernels, the tie
+all-reduce(MAX), the decision and the fused apply+count pass are enqueued in order on the
+engine's HIP stream, with no host sync until the end of a batch of BPE_LOOP_BATCH iterations.
+Only an iteration with heavy sketch buckets or too many tied pairs takes the host protocol above.
+
 The protocol only needs a `shard` object with export()/select()/tie_positions()/apply(); GpuShard
 wraps libbpe on a HIP device, and tests/test_sharded_gloo.py drives the same protocol on CPU
 with gloo.
@@ -26,6 +32,8 @@ pkg = importlib.import_module('bpe-tokenizer_amd')
 
 HOT_BINS = 256 * 256
 TABLE_BINS = HOT_BINS + 16384
+MAX_CAND = 16            # BPE_MAX_CAND: tie positions all-reduced per iteration
+LOOP_BATCH = 64          # BPE_LOOP_BATCH: iterations per host round trip of the rank loop
 RANK_SHIFT = 40          # global position = rank << 40 | shard-local position
 
 
@@ -158,6 +166,7 @@ class ShardedTrainer:
         self.n_tokens = n_tokens          # token_table.length (next new id, core.ts:315)
         self.live = live_global           # live corpus tokens over all ranks
         self.merges = []
+        self._rl = None                   # rank loop buffers (table, tie, stream)
 
     @classmethod
     def synthetic(cls, device, rank, world, bytes_per_rank, sample_bytes, seed, alphabet, base,
@@ -206,12 +215,55 @@ class ShardedTrainer:
                 self.live -= m[2]
             self.merges += ms
             return ms
+        return self.run_rank_loop(n, max_length, min_weight)
+
+    def run_rank_loop(self, n, max_length=0, min_weight=0):
+        """n iterations across the ranks with the exchange on the device (bpe_rank_loop_*): no
+        host sync inside a batch of LOOP_BATCH iterations.  Returns the merges [(a, b, W)]."""
+        import torch
+        dist = self.dist
+        eng = self.engine
+        if self._rl is None:
+            dev = self.shard.device
+            self._rl = (torch.zeros(TABLE_BINS, dtype=torch.int64, device=dev),
+                        torch.zeros(MAX_CAND, dtype=torch.int64, device=dev),
+                        torch.cuda.ExternalStream(eng.stream(), device=dev))
+        table, tie, stream = self._rl
+        gloo = dist.get_backend() == 'gloo'
+
+        def all_reduce(t, op):
+            if gloo:           # (host copies, in order on the engine's stream; tests only)
+                h = t.cpu()
+                dist.all_reduce(h, op=op)
+                t.copy_(h)
+            else:              # RCCL, ordered after the stream's kernels by events
+                dist.all_reduce(t, op=op)
+
         ms = []
-        for _ in range(n):
-            m = self.step(max_length, min_weight)
-            if m is None:
+        while len(ms) < n:
+            k = min(LOOP_BATCH, n - len(ms))
+            with torch.cuda.stream(stream):
+                eng.rank_loop_begin(max_length, min_weight, table.data_ptr(), tie.data_ptr(),
+                                    self.rank)
+                for _ in range(k):
+                    all_reduce(table, dist.ReduceOp.SUM)
+                    eng.rank_loop_select()
+                    all_reduce(tie, dist.ReduceOp.MAX)
+                    eng.rank_loop_decide()
+                    eng.rank_loop_count()
+                got, status = eng.rank_loop_end()
+            for m in got:
+                self.n_tokens += 1
+                self.live -= m[2]
+            self.merges += got
+            ms += got
+            if status == 1:
                 break
-            ms.append(m)
+            if status == 2 and len(ms) < n:
+                m = self.step(max_length, min_weight)     # the host protocol for this iteration
+                if m is None:
+                    break
+                ms.append(m)
         return ms
 
     def step(self, max_length=0, min_weight=0):

@@ -154,6 +154,30 @@ int bpe_select_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *cold_
  * last counted occurrence (0 when none) into host last[n].  Positions grow in corpus order. */
 int bpe_tie_positions(bpe_ctx *ctx, const int32_t *cand, int64_t n, uint64_t *last);
 
+/* ---- the device-resident loop on one rank of a sharded corpus ---------------------------------
+ * mergeUntil (core.ts:365-383) over shards with no host sync per iteration.  `table`
+ * (BPE_TABLE_BINS u64) and `tie` (BPE_MAX_CAND u64) are DEVICE buffers the caller all-reduces IN
+ * ORDER on this context's stream (bpe_get_stream; e.g. RCCL on that stream).  Per iteration:
+ *   all-reduce(SUM, table); bpe_rank_loop_select; all-reduce(MAX, tie); bpe_rank_loop_decide;
+ *   bpe_rank_loop_count
+ * at most BPE_LOOP_BATCH times between bpe_rank_loop_begin and bpe_rank_loop_end.  Every rank takes
+ * the same decisions from the same global tables, so all ranks run the same collectives; an
+ * iteration after the batch has ended is a no-op (its collectives still run).
+ * bpe_rank_loop_begin writes this shard's table into `table`; `rank` orders the tie positions
+ * (rank r's occurrences come after rank r-1's, rule R3).  bpe_rank_loop_end syncs and writes the
+ * batch's merges as (a, b, W) triples into host out_abw (capacity cap triples), *status:
+ * 0 = every enqueued iteration merged, 1 = no pair qualifies (stop), 2 = the next iteration needs
+ * the host protocol (heavy sketch buckets or more than BPE_MAX_CAND tied pairs: export / heavy /
+ * select / tie_positions above). */
+#define BPE_MAX_CAND 16
+#define BPE_LOOP_BATCH 64
+int bpe_rank_loop_begin(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, uint64_t *table,
+                        uint64_t *tie, int rank);
+int bpe_rank_loop_select(bpe_ctx *ctx);
+int bpe_rank_loop_decide(bpe_ctx *ctx);
+int bpe_rank_loop_count(bpe_ctx *ctx);
+int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status);
+
 /* ---- measurement -------------------------------------------------------------------------------
  * HIP-event timings of the kernels, recorded on the context's own stream. */
 typedef struct {

@@ -9,7 +9,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def worker(rank, world, port, q):
+def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
+           mib=3):
     import importlib
     import sys
     import torch
@@ -23,40 +24,67 @@ def worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
         tr = sharded.ShardedTrainer.synthetic(device=0, rank=rank, world=world,
-                                              bytes_per_rank=3 << 20, sample_bytes=1 << 20,
-                                              seed=777, alphabet=40, base=60, dist=dist)
-        for _ in range(60):
-            if tr.step(0, 2) is None:
-                break
+                                              bytes_per_rank=mib << 20, sample_bytes=1 << 20,
+                                              seed=seed, alphabet=A, base=base, dist=dist)
+        if mode == 'step':
+            for _ in range(n):
+                if tr.step(max_length, 2) is None:
+                    break
+        else:
+            tr.run(n, max_length, 2)     # the device-resident rank loop
         ids, off = tr.engine.read_corpus()
         q.put((rank, tr.merges, ids.tolist(), off.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_single_engine():
-    import importlib
+def run_ranks(world, **kw):
     import torch.multiprocessing as mp
-    from bpe_amd import pkg
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, rest) for r, *rest in (q.get(timeout=300) for _ in procs))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    data = pkg.synth_latin1(6 << 20, seed=777, A=40, base=60)
+    return res
+
+
+def single_engine(world, n=60, max_length=0, seed=777, A=40, base=60, mib=3, **_):
+    from bpe_amd import pkg
+    data = pkg.synth_latin1((mib * world) << 20, seed=seed, A=A, base=base)
     e = pkg.Engine(0)
     e.add_latin1(data, sample_bytes=1 << 20)
-    want = e.merge_until(0, 2, 60)
-    assert [tuple(m) for m in res[0][0]] == want
-    assert [tuple(m) for m in res[1][0]] == want
-    ids, off = e.read_corpus()
-    n0 = len(res[0][1])
-    assert res[0][1] + res[1][1] == ids.tolist()
+    want = e.merge_until(max_length, 2, n)
+    ids, _ = e.read_corpus()
+    e.close()
+    return want, ids.tolist()
+
+
+def check(world, **kw):
+    res = run_ranks(world, **kw)
+    want, ids = single_engine(world, **kw)
+    for r in range(world):
+        assert [tuple(m) for m in res[r][0]] == want, 'rank %d merges' % r
+    assert sum((res[r][1] for r in range(world)), []) == ids
+
+
+def test_two_ranks_on_one_gpu_match_single_engine():
+    check(2)
+
+
+def test_rank_loop_two_ranks_match_single_engine():
+    """The device-resident exchange (bpe_rank_loop_*): 300 merges, past the 256 base ids (cold
+    sketch pairs, heavy-bucket iterations through the host protocol) and many tied iterations
+    (full tie pass per shard, all-reduce(MAX) of the positions)."""
+    check(2, mode='loop', n=300)
+
+
+def test_rank_loop_three_ranks_max_length():
+    check(3, mode='loop', n=200, max_length=3, seed=4242, A=12, base=97, mib=2)
