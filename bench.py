@@ -29,14 +29,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ALG_BYTES_PER_PAIR_SCAN = 4    # K1 reads each int32 token once
 
 
-def cpu_baseline(sample_mib, budget_s):
+def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
     """The C restatement (oracle/, single thread) on a bounded sample of the same workload."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     from oracle import OracleState
     pkg = importlib.import_module('bpe-tokenizer_amd')
     n = sample_mib << 20
-    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    data = (pkg.synth_zipf(n, seed=12345) if corpus == 'zipf' else
+            pkg.synth_latin1(n, seed=12345, A=256, base=0))
     lut = np.full(256, -1, np.int32)
     uniq, idx = np.unique(data, return_index=True)
     for k, u in enumerate(uniq[np.argsort(idx)]):
@@ -69,6 +70,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--corpus-mib', type=int, default=1024, help='corpus MiB per GPU')
     ap.add_argument('--alphabet', type=int, default=256)
+    ap.add_argument('--corpus', choices=['uniform', 'zipf'], default='uniform',
+                    help='uniform: the C3 byte stream; zipf: the skewed variant (Zipf 1.1 words)')
     ap.add_argument('--cpu-sample-mib', type=int, default=64)
     ap.add_argument('--cpu-budget-s', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -95,7 +98,7 @@ def main():
     trainer = sharded.ShardedTrainer.synthetic(device=local_rank, rank=rank, world=world,
                                                bytes_per_rank=n, sample_bytes=1 << 20,
                                                seed=12345, alphabet=args.alphabet, base=base,
-                                               dist=dist)
+                                               dist=dist, corpus=args.corpus)
 
     if len(trainer.run(args.warmup, max_length=0, min_weight=2)) != args.warmup:
         raise SystemExit('corpus exhausted during warmup')
@@ -151,10 +154,13 @@ def main():
             'dtype': 'int32',
             'data': 'synthetic',
             'config': {
-                'workload': 'C3: %d MiB/GPU latin1 corpus, xorshift32 seed 12345, %d-char alphabet, '
-                            '1 MiB samples; merges %d..%d of mergeUntil({min_weight:2})'
-                            % (args.corpus_mib, args.alphabet, args.warmup + 1,
-                               args.warmup + args.steps),
+                'workload': (('C3: %d MiB/GPU latin1 corpus, xorshift32 seed 12345, %d-char '
+                              'alphabet' % (args.corpus_mib, args.alphabet))
+                             if args.corpus == 'uniform' else
+                             ('C3-zipf (skewed variant): %d MiB/GPU of Zipf(1.1) words over a '
+                              '32768-word list, seed 12345' % args.corpus_mib))
+                            + '; 1 MiB samples; merges %d..%d of mergeUntil({min_weight:2})'
+                            % (args.warmup + 1, args.warmup + args.steps),
                 'corpus_tokens': live0,
                 'parallelism': 'corpus-sharded x%d' % world,
             },
@@ -182,7 +188,7 @@ def main():
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s)
+            out['cpu_baseline'] = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s, args.corpus)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

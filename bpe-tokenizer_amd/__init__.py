@@ -30,7 +30,7 @@ C_API = [
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_apply_merges', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
-    'bpe_get_stream', 'bpe_synth_latin1', 'bpe_recount', 'bpe_export_counts',
+    'bpe_get_stream', 'bpe_synth_latin1', 'bpe_synth_zipf', 'bpe_recount', 'bpe_export_counts',
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions', 'bpe_rank_loop_begin',
     'bpe_rank_loop_select', 'bpe_rank_loop_decide', 'bpe_rank_loop_count', 'bpe_rank_loop_end',
 ]
@@ -116,6 +116,8 @@ def lib():
         'bpe_rank_loop_count': ([vp], ctypes.c_int),
         'bpe_rank_loop_end': ([vp, i64p, ctypes.c_int64, i64p, ctypes.POINTER(ctypes.c_int)],
                               ctypes.c_int),
+        'bpe_synth_zipf': ([ctypes.c_uint32, ctypes.c_double, ctypes.c_uint32, ctypes.c_uint64,
+                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
         'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                               ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     }
@@ -149,6 +151,15 @@ def synth_latin1(n, seed=12345, A=256, base=0, skip=0):
     """SURVEY.md §8(d) synthetic corpus: xorshift32 bytes (jump-ahead `skip` outputs)."""
     out = np.empty(n, dtype=np.uint8)
     _check(lib().bpe_synth_latin1(seed, A, base, skip, out.ctypes.data, n), 'bpe_synth_latin1')
+    return out
+
+
+def synth_zipf(n, seed=12345, s=1.1, n_words=32768, sample_bytes=1 << 20, first_sample=0):
+    """Skewed synthetic corpus (include/bpe_tools.h bpe_synth_zipf): Zipf(s) words from a fixed
+    word list, samples of sample_bytes starting at sample `first_sample`."""
+    out = np.empty(n, dtype=np.uint8)
+    _check(lib().bpe_synth_zipf(seed, s, n_words, first_sample, sample_bytes, out.ctypes.data, n),
+           'bpe_synth_zipf')
     return out
 
 

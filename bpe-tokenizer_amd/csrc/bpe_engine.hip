@@ -99,6 +99,11 @@ struct bpe_ctx {
     int64_t pend_expect = -1;    // W the replacement count must equal (mergeUntil), -1 = any
     int2 *h_cand = nullptr;      // pinned: first MAX_CAND candidates come back with the Result
     bool counts_valid = false;   // d_hot + cold table describe the current corpus
+    // The cold table holds the exact count of EVERY cold pair and is kept so merge by merge
+    // (cold_refresh) instead of being rebuilt by exact passes: entered after consecutive exact
+    // passes (a corpus whose winners are pairs of merged tokens, e.g. Zipf words)
+    bool cold_exact = false;
+    int exact_streak = 0;
     bool carry_valid = false;    // d_sums / d_carry describe the current corpus and geometry
     int64_t cpr = 0;
     int R = 0, G = 0;
@@ -179,6 +184,7 @@ int seal_packed(bpe_ctx *c) {
     }
     c->packed = true;
     c->counts_valid = c->carry_valid = false;
+    c->cold_exact = false;
     geometry(c);
     return BPE_OK;
 }
@@ -252,6 +258,7 @@ int ensure_cold(bpe_ctx *c, uint64_t extra) {
     c->cold.n_used = c->d_cold_flags;
     c->cold.overflow = c->d_cold_flags + 1;
     c->counts_valid = false;
+    c->cold_exact = false;
     return BPE_OK;
 }
 
@@ -420,9 +427,10 @@ int compact(bpe_ctx *c) {
     if ((int64_t)total != c->live_slots)
         return fail(BPE_ERR_STATE, "bpe native: compaction lost slots");
     std::swap(c->d_ids, c->d_tmp);
-    const bool counts = c->counts_valid;
+    const bool counts = c->counts_valid, cold_exact = c->cold_exact;
     if ((rc = seal_packed(c))) return rc;
     c->counts_valid = counts;
+    c->cold_exact = cold_exact;
     if (c->stats_on) c->stats.compactions += 1;
     return BPE_OK;
 }
@@ -442,6 +450,7 @@ int maybe_compact(bpe_ctx *c) {
 // (one more streaming pass; only when some bucket could still reach the best hot count).
 int exact_pass(bpe_ctx *c) {
     int rc;
+    c->cold_exact = false;   // (the table is rebuilt for the marked buckets only)
     if ((rc = ensure_cold(c, 0))) return rc;
     if (!c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
@@ -460,6 +469,33 @@ int exact_pass(bpe_ctx *c) {
     HIP_TRY(hipStreamSynchronize(s));
     if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
     if (c->stats_on) c->stats.exact_passes += 1;
+    return BPE_OK;
+}
+
+// The maintained cold table after the merge (a, b) -> cc has been applied (and counted): only
+// pairs with a side in {a, b, cc} changed count (every other pair keeps its occurrences and its
+// run parity), so those lose their count and one streaming pass counts every cold pair touching
+// a, b or cc exactly on the merged corpus (LDS-aggregated, no table clear).  When the table has
+// to grow, it is rebuilt by a full exact pass at the next selection instead.
+int cold_refresh(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
+    int rc;
+    const uint64_t cap0 = c->cold_cap;
+    if ((rc = ensure_cold(c, 0))) return rc;
+    if (c->cold_cap != cap0 || !c->cold_exact) {
+        c->cold_exact = false;
+        return BPE_OK;
+    }
+    if (!c->carry_valid)
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    geometry(c);
+    hipStream_t s = c->stream;
+    k_cold_invalidate<<<256, 256, 0, s>>>(c->cold, a, b);
+    k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
+        c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
+        c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+    k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
+                                                          c->cold, c->d_heavy, nullptr, a, b, cc);
+    HIP_TRY(hipGetLastError());
     return BPE_OK;
 }
 
@@ -487,9 +523,27 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     if ((rc = span_end(c, e_sel, 1))) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     if ((rc = settle_with(c, c->h_res->replaced))) return rc;   // a pending apply's R came along
-    if (c->h_res->n_heavy && local) {
-        // some cold pair may still reach W: count those exactly, then recollect hot + cold
-        if ((rc = exact_pass(c))) return rc;
+    if (local && !c->h_res->n_heavy && !c->cold_exact) c->exact_streak = 0;
+    if (local && (c->h_res->n_heavy || c->cold_exact)) {
+        // some cold pair may still reach W: count those exactly (or read the maintained table),
+        // then recollect hot + cold
+        if (!c->cold_exact) {
+            // the second exact pass in a row counts every cold pair and keeps the table
+            const bool full = ++c->exact_streak >= 2;
+            if (full) HIP_TRY(hipMemsetAsync(c->d_heavy, 0xFF, HEAVY_WORDS * sizeof(uint32_t), s));
+            if ((rc = exact_pass(c))) return rc;
+            c->cold_exact = full;
+        } else {
+            uint32_t flags[2] = {0, 0};
+            HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+            if ((uint64_t)flags[0] * 4 > c->cold_cap * 3) {
+                // too full to probe well: this selection still reads it, the next one rebuilds it
+                c->cold_exact = false;
+                c->exact_streak = 1;
+            }
+        }
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
         k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
         k_collect<<<HOT_BINS / 256, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
@@ -598,7 +652,8 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     if (c->n_live < 2) return BPE_OK;
     if (!c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    return run_pass(c, true, a, b, cc, replaced);
+    if ((rc = run_pass(c, true, a, b, cc, replaced))) return rc;
+    return c->cold_exact ? cold_refresh(c, a, b, cc) : BPE_OK;
 }
 
 // Up to n mergeUntil iterations with the decisions kept on the device (core.ts:367-384): per
@@ -612,6 +667,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     int rc;
     *n_done = 0;
     *status = LOOP_DONE;
+    c->cold_exact = false;   // (its merges do not refresh a maintained cold table)
     if ((rc = settle(c))) return rc;
     c->opt_max_length = max_length;
     if (!c->counts_valid || !c->carry_valid)
@@ -733,6 +789,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
 int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *table,
                     unsigned long long *tie, int rank) {
     int rc;
+    c->cold_exact = false;
     if ((rc = settle(c))) return rc;
     if ((rc = maybe_compact(c))) return rc;
     c->opt_max_length = max_length;
@@ -965,6 +1022,7 @@ int replay(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, bool co
             if (replaced) replaced[i0 + j] = R;
         }
         c->counts_valid = false;
+        c->cold_exact = false;
         c->best_ready = false;
         i0 += nb;
     }
@@ -1336,13 +1394,23 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     int64_t n = 0;
     const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
     int64_t abw[3 * LOOP_BATCH];
+    // Batch size adapts to how often the host path is needed: a batch that ends early leaves its
+    // remaining iterations' launches as no-ops, so after an early end the next batch is sized to
+    // about twice the merges that one finished; after a batch that finished none, the device loop
+    // rests for a few host iterations (backing off up to 16) before it is tried again.
+    int64_t batch = LOOP_BATCH, rest = 0, backoff = 0;
     while (!max_iterations || n < max_iterations) {                      // core.ts:374-378
         if ((rc = settle(c))) return rc;
         if (c->n_live < 2) break;
         if ((rc = maybe_compact(c))) return rc;
         // batches on the device while the vocabulary has room (the host path reports the limit)
-        int64_t want = std::min<int64_t>(LOOP_BATCH, BPE_MAX_VOCAB - (int64_t)c->h_len16.size());
+        int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)c->h_len16.size());
         if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
+        if (rest > 0) {
+            --rest;
+            want = 0;
+        }
+        if (c->cold_exact) want = 0;   // (the maintained cold table is refreshed by the host path)
         if (want > 0) {
             int64_t nd = 0;
             int st = LOOP_DONE;
@@ -1351,7 +1419,14 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
                 if (n < cap)
                     for (int q = 0; q < 3; ++q) out_abw[3 * n + q] = abw[3 * i + q];
             if (st == LOOP_DONE) break;
-            if (st == LOOP_RUN) continue;
+            if (st == LOOP_RUN) {
+                batch = std::min<int64_t>(LOOP_BATCH, 2 * batch);
+                backoff = 0;
+                continue;
+            }
+            batch = std::max<int64_t>(1, std::min<int64_t>(LOOP_BATCH, 2 * nd));
+            if (nd == 0) rest = backoff = std::min<int64_t>(16, 2 * backoff + 1);
+            else backoff = 0;
             if (max_iterations && n >= max_iterations) break;
         }
         // LOOP_HOST (heavy sketch buckets, many tied candidates) or no vocabulary room: one

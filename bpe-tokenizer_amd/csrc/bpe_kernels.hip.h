@@ -238,12 +238,17 @@ struct Sink {
     unsigned long long *spill;       // global u64 [TABLE_BINS]
     ColdTable ct;
     const uint32_t *heavy;           // LDS bitmap [HEAVY_WORDS] (MODE_EXACT)
+    // MODE_EXACT with ma >= 0: the maintained cold table's refresh after the merge (ma, mb) -> mc:
+    // every cold pair with a side in {ma, mb, mc}, whatever its bucket (heavy is then unused)
+    int32_t ma, mb, mc;
 };
 
 template <int MODE>
 __device__ __forceinline__ bool exact_wanted(const Sink &k, int32_t x, int32_t y) {
     const int idx = table_index(x, y);
     if (idx < HOT_BINS) return false;
+    if (k.ma >= 0)
+        return (x == k.ma) | (x == k.mb) | (x == k.mc) | (y == k.ma) | (y == k.mb) | (y == k.mc);
     const int b = idx - HOT_BINS;
     return (k.heavy[b >> 5] >> (b & 31)) & 1u;
 }
@@ -308,6 +313,31 @@ __device__ __forceinline__ void lds_fix(const Sink &k, uint32_t addr, uint32_t i
     atomicAdd(&k.spill[bin], (unsigned long long)big);
 }
 
+// MODE_EXACT: each workgroup first sums its cold-pair counts in an LDS hash (open addressing,
+// after the heavy bitmap; the table's LDS is free in that mode) and adds each distinct key to the
+// global sparse table once at the end, so a skewed corpus's frequent cold pairs do not serialise
+// on one global counter.  A key that finds no slot within LH_PROBES goes to the global table.
+constexpr int LH_BITS = 14;
+constexpr int LH_SLOTS = 1 << LH_BITS;   // (key, count) dword pairs: 128 KiB
+constexpr int LH_PROBES = 8;
+static_assert(HEAVY_WORDS + 2 * LH_SLOTS <= HIST_WORDS, "LDS cold hash does not fit");
+
+__device__ __forceinline__ void lds_cold_add(const Sink &k, uint32_t key, uint32_t inc) {
+    uint32_t *keys = k.hist + HEAVY_WORDS;
+    uint32_t *cnt = keys + LH_SLOTS;
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - LH_BITS);
+    for (int p = 0; p < LH_PROBES; ++p) {
+        uint32_t kk = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kk == EMPTY) kk = atomicCAS(&keys[h], EMPTY, key);   // (EMPTY: this lane claimed it)
+        if (kk == EMPTY || kk == key) {
+            atomicAdd(&cnt[h], inc);
+            return;
+        }
+        h = (h + 1) & (LH_SLOTS - 1);
+    }
+    cold_add(k.ct, key, inc);
+}
+
 // One counted occurrence of (x, y) (outside the streaming fast paths).
 template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
@@ -325,7 +355,7 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) 
         }
         lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
     } else if (exact_wanted<MODE>(k, x, y)) {
-        cold_add(k.ct, pair_key(x, y), 1u);
+        lds_cold_add(k, pair_key(x, y), 1u);
     }
 }
 
@@ -928,6 +958,10 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
     } else if (MODE == MODE_EXACT) {
         for (int i = threadIdx.x; i < HEAVY_WORDS; i += WG) hist[i] = heavy_g[i];
+        for (int i = threadIdx.x; i < LH_SLOTS; i += WG) {
+            hist[HEAVY_WORDS + i] = EMPTY;
+            hist[HEAVY_WORDS + LH_SLOTS + i] = 0;
+        }
     }
     if (MODE != MODE_NONE) __syncthreads();
     Sink k;
@@ -935,6 +969,9 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.spill = spill;
     k.ct = ct;
     k.heavy = hist;
+    k.ma = MODE == MODE_EXACT ? ma : -1;
+    k.mb = mb;
+    k.mc = mc;
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6)));
     if (r < R) {
@@ -1050,6 +1087,12 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         uint4 *out = reinterpret_cast<uint4 *>(partials + (size_t)blockIdx.x * HIST_WORDS);
         const uint4 *h4 = reinterpret_cast<const uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
+    } else if (MODE == MODE_EXACT) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < LH_SLOTS; i += WG) {
+            const uint32_t key = hist[HEAVY_WORDS + i];
+            if (key != EMPTY) cold_add(ct, key, hist[HEAVY_WORDS + LH_SLOTS + i]);
+        }
     }
 }
 
@@ -1114,7 +1157,8 @@ __device__ __forceinline__ int next_nonempty(const RegionSum *s, int q, int R) {
 template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
                        unsigned long long *__restrict__ spill, ColdTable ct,
-                       const uint32_t *__restrict__ heavy, const LoopCtl *ctl) {
+                       const uint32_t *__restrict__ heavy, const LoopCtl *ctl, int32_t ma = -1,
+                       int32_t mb = -1, int32_t mc = -1) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R || loop_off(ctl)) return;
     Sink k;
@@ -1122,6 +1166,9 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.spill = spill;
     k.ct = ct;
     k.heavy = heavy;
+    k.ma = MODE == MODE_EXACT ? ma : -1;
+    k.mb = mb;
+    k.mc = mc;
     const int p = prev_nonempty(s, r - 1);
     const int nx = next_nonempty(s, r + 1, R);
     RegionCarry rc;
@@ -1282,8 +1329,9 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
         const uint32_t h = ct.used[i];
         const uint32_t key = ct.keys[h];
         const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        if (!pair_ok(a, b, len16, max_length)) continue;
-        const unsigned long long k = pack_key(ct.counts[h], a, b);
+        const uint32_t n_ab = ct.counts[h];
+        if (!n_ab || !pair_ok(a, b, len16, max_length)) continue;
+        const unsigned long long k = pack_key(n_ab, a, b);
         best = k > best ? k : best;
     }
     best = wave_max_u64(best);
@@ -1540,6 +1588,19 @@ __global__ void k_collect_list(const unsigned long long *__restrict__ hot,
         const int32_t a = (int32_t)(keys[i] >> 16), b = (int32_t)(keys[i] & 0xFFFFu);
         if (pair_ok(a, b, len16, max_length) && pack_key(counts[i], a, b) == best)
             push_cand(res, cand, a, b);
+    }
+}
+
+// The maintained cold table before its refresh after the merge (a, b) -> c: the pairs with a side
+// a or b lose their count (the refresh pass counts them again on the merged corpus; every other
+// pair's count is unchanged by the merge).
+__global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b) {
+    const uint32_t n = *ct.n_used;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t h = ct.used[i];
+        const uint32_t key = ct.keys[h];
+        const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
+        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.counts[h] = 0;
     }
 }
 

@@ -1,6 +1,8 @@
 // bpe_tools.cpp — synthetic corpus generator for the bench and tests (include/bpe_tools.h).
 #include "bpe_tools.h"
 
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -68,6 +70,77 @@ extern "C" int bpe_synth_latin1(uint32_t seed, uint32_t A, uint32_t base, uint64
             }
         });
     }
+    for (auto &t : th) t.join();
+    return 0;
+}
+
+// ---- skewed variant: Zipf-distributed words ("Zipf s=1.1 words") -------------
+namespace {
+
+inline uint32_t mix32(uint32_t x) {   // (murmur3 finaliser; seeds the per-word / per-sample streams)
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x ? x : 1u;
+}
+
+inline uint32_t below(uint32_t x, uint32_t n) { return (uint32_t)(((uint64_t)x * n) >> 32); }
+
+}  // namespace
+
+extern "C" int bpe_synth_zipf(uint32_t seed, double s, uint32_t n_words, uint64_t first_sample,
+                              int64_t sample_bytes, uint8_t *out, int64_t n) {
+    if (!out || n < 0 || sample_bytes <= 0 || n_words == 0 || n_words > (1u << 24) || !(s > 0))
+        return -1;
+    // the word list: word w is 2..8 letters a-z from its own stream
+    std::vector<uint32_t> woff(n_words + 1, 0);
+    std::vector<uint8_t> wchars;
+    wchars.reserve((size_t)n_words * 5);
+    for (uint32_t w = 0; w < n_words; ++w) {
+        uint32_t x = mix32(seed ^ mix32(0x9E3779B9u * (w + 1)));
+        x = step(x);
+        const uint32_t len = 2 + below(x, 7);
+        for (uint32_t i = 0; i < len; ++i) {
+            x = step(x);
+            wchars.push_back((uint8_t)('a' + below(x, 26)));
+        }
+        woff[w + 1] = (uint32_t)wchars.size();
+    }
+    // rank r (1-based) has weight r^-s
+    std::vector<double> cdf(n_words);
+    double acc = 0;
+    for (uint32_t r = 0; r < n_words; ++r) cdf[r] = (acc += std::pow((double)(r + 1), -s));
+    for (auto &v : cdf) v /= acc;
+    const int64_t n_samples = (n + sample_bytes - 1) / sample_bytes;
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt == 0) nt = 1;
+    if (nt > 16) nt = 16;
+    if (n_samples < (int64_t)nt) nt = (unsigned)std::max<int64_t>(1, n_samples);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+            for (int64_t k = t; k < n_samples; k += nt) {
+                // sample first_sample + k: words from its own stream, one separator after each
+                // (a newline after 1 word in 16, else a space), cut at sample_bytes
+                uint32_t x = mix32((uint32_t)seed + 0x9E3779B9u * (uint32_t)(first_sample + k + 1) +
+                                   (uint32_t)((first_sample + k) >> 32));
+                uint8_t *p = out + k * sample_bytes;
+                const int64_t len = std::min<int64_t>(sample_bytes, n - k * sample_bytes);
+                int64_t i = 0;
+                while (i < len) {
+                    x = step(x);
+                    const double u = (double)x * (1.0 / 4294967296.0);
+                    const uint32_t w = (uint32_t)(std::lower_bound(cdf.begin(), cdf.end(), u) -
+                                                  cdf.begin());
+                    const uint32_t wi = w < n_words ? w : n_words - 1;
+                    for (uint32_t j = woff[wi]; j < woff[wi + 1] && i < len; ++j) p[i++] = wchars[j];
+                    x = step(x);
+                    if (i < len) p[i++] = (x & 15u) == 0 ? '\n' : ' ';
+                }
+            }
+        });
     for (auto &t : th) t.join();
     return 0;
 }

@@ -170,10 +170,18 @@ class ShardedTrainer:
 
     @classmethod
     def synthetic(cls, device, rank, world, bytes_per_rank, sample_bytes, seed, alphabet, base,
-                  dist=None):
-        """Rank r holds bytes [r*B, (r+1)*B) of one xorshift32 corpus stream."""
-        data = pkg.synth_latin1(bytes_per_rank, seed=seed, A=alphabet, base=base,
-                                skip=rank * bytes_per_rank)
+                  dist=None, corpus='uniform'):
+        """Rank r holds bytes [r*B, (r+1)*B) of one synthetic corpus: the
+        xorshift32 byte stream ('uniform') or Zipf(1.1) words ('zipf', bpe_synth_zipf; whole
+        samples per rank)."""
+        if corpus == 'zipf':
+            if bytes_per_rank % sample_bytes:
+                raise ValueError('zipf shards hold whole samples')
+            data = pkg.synth_zipf(bytes_per_rank, seed=seed, sample_bytes=sample_bytes,
+                                  first_sample=rank * (bytes_per_rank // sample_bytes))
+        else:
+            data = pkg.synth_latin1(bytes_per_rank, seed=seed, A=alphabet, base=base,
+                                    skip=rank * bytes_per_rank)
         eng = pkg.Engine(device)
         if world == 1:
             cmap, nt, _ = eng.add_latin1(data, sample_bytes=sample_bytes)
@@ -240,8 +248,9 @@ class ShardedTrainer:
                 dist.all_reduce(t, op=op)
 
         ms = []
+        batch = LOOP_BATCH      # (as bpe_merge_until: about twice what an early-ended batch did)
         while len(ms) < n:
-            k = min(LOOP_BATCH, n - len(ms))
+            k = min(batch, n - len(ms))
             with torch.cuda.stream(stream):
                 eng.rank_loop_begin(max_length, min_weight, table.data_ptr(), tie.data_ptr(),
                                     self.rank)
@@ -259,6 +268,7 @@ class ShardedTrainer:
             ms += got
             if status == 1:
                 break
+            batch = min(LOOP_BATCH, 2 * batch) if status == 0 else max(1, 2 * len(got))
             if status == 2 and len(ms) < n:
                 m = self.step(max_length, min_weight)     # the host protocol for this iteration
                 if m is None:

@@ -52,3 +52,18 @@ def test_synthetic_generator_matches_oracle_and_jumps():
     assert np.array_equal(b, full[5000:])
     big = pkg.synth_latin1(1 << 23, seed=7, A=256)           # multithreaded path
     assert np.array_equal(big[-100:], pkg.synth_latin1(100, seed=7, A=256, skip=(1 << 23) - 100))
+
+
+def test_synth_zipf_is_deterministic_and_shardable():
+    from bpe_amd import pkg
+    import numpy as np
+    a = pkg.synth_zipf(6 << 16, seed=7, sample_bytes=1 << 16)
+    assert np.array_equal(a, pkg.synth_zipf(6 << 16, seed=7, sample_bytes=1 << 16))
+    b = pkg.synth_zipf(2 << 16, seed=7, sample_bytes=1 << 16, first_sample=4)
+    assert np.array_equal(a[4 << 16:], b)
+    letters = set(range(ord('a'), ord('z') + 1)) | {ord(' '), ord('\n')}
+    assert set(np.unique(a).tolist()) <= letters
+    # Zipf: the most frequent word dominates
+    words = bytes(a[:1 << 16]).split()
+    top = max(set(words), key=words.count)
+    assert words.count(top) > len(words) // 20

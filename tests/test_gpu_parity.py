@@ -336,3 +336,27 @@ def test_runs_across_region_boundaries_from_a_fast_chunk():
     e, got = run_engine([seq], [1] * 3003, {'min_weight': 2, 'max_iterations': 3})
     assert got == want
     assert e.samples() == st.samples()
+
+
+@pytest.mark.parametrize('mib,n,max_length', [(4, 600, 0), (3, 400, 5), (8, 1500, 0)])
+def test_zipf_words_vs_oracle(mib, n, max_length):
+    """Skewed corpus (bpe_synth_zipf): a 28-symbol alphabet whose merges soon
+    build whole words, so most winning pairs are pairs of merged tokens (ids >= 256: the cold
+    sketch, heavy buckets) and long equal-pair runs are rare.  After two exact passes in a row the
+    engine keeps an exact table of every cold pair, refreshed merge by merge for the pairs touching
+    the merged tokens.  mergeUntil against the C restatement: merges and final corpus bit-exact,
+    and the exact passes stay few (the maintained table answers the rest)."""
+    data = pkg.synth_zipf(mib << 20, seed=2024)
+    e = pkg.Engine(0)
+    e.stats_enable(True)
+    cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    ids = cmap[data]
+    off = np.arange(0, (mib << 20) + 1, 1 << 20, dtype=np.int64)
+    st = OracleState(ids, off, [1] * nt, nt, extra=n + 8)
+    want = st.merge_until(max_length, 2, n)
+    got = e.merge_until(max_length, 2, n)
+    assert got == [tuple(m) for m in want]
+    flat, eoff = e.read_corpus()
+    assert eoff.tolist() == st.off.tolist()
+    assert np.array_equal(flat, st.ids[:st.off[-1]])
+    assert e.stats()['exact_passes'] <= 10
