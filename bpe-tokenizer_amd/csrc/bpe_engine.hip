@@ -89,6 +89,7 @@ struct bpe_ctx {
     RegionCarry *d_carry = nullptr;
     int64_t *d_outoff = nullptr;
     Result *d_res = nullptr, *h_res = nullptr;
+    uint32_t *h_cold_flags = nullptr;   // pinned copy of d_cold_flags
     int2 *d_cand = nullptr;
     ColdTable cold{};
     uint32_t *d_cold_flags = nullptr;   // [0] n_used, [1] overflow
@@ -228,6 +229,10 @@ int sync_len16(bpe_ctx *c, int64_t max_length) {
 // Upper bound on distinct cold pairs in the next pass: every counted pair with an id >= HOT
 // involves a cold-token occurrence, and each occurrence sits in at most two pairs.  `extra` bounds
 // the occurrences of a token created by the pass itself.
+// grid of the scans over the cold table's dense view (>= HOT_BINS / 256 for k_collect)
+constexpr int COLD_GRID = 1024;
+static_assert(COLD_GRID * 256 >= HOT_BINS, "k_collect covers the hot bins");
+
 int ensure_cold(bpe_ctx *c, uint64_t extra) {
     uint64_t s = extra;
     for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
@@ -243,10 +248,14 @@ int ensure_cold(bpe_ctx *c, uint64_t extra) {
     dfree(c->cold.keys);
     dfree(c->cold.counts);
     dfree(c->cold.used);
+    dfree(c->cold.dkeys);
+    dfree(c->cold.dcounts);
     int rc;
     if ((rc = dev_alloc(&c->cold.keys, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.counts, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.used, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.dkeys, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.dcounts, cap))) return rc;
     HIP_TRY(hipMemsetAsync(c->cold.keys, 0xFF, cap * sizeof(uint32_t), c->stream));
     HIP_TRY(hipMemsetAsync(c->cold.counts, 0, cap * sizeof(uint32_t), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), c->stream));
@@ -468,6 +477,8 @@ int exact_pass(bpe_ctx *c) {
     HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    k_cold_sync<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, -1, 1);
+    HIP_TRY(hipGetLastError());
     if (c->stats_on) c->stats.exact_passes += 1;
     return BPE_OK;
 }
@@ -489,12 +500,13 @@ int cold_refresh(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     geometry(c);
     hipStream_t s = c->stream;
-    k_cold_invalidate<<<256, 256, 0, s>>>(c->cold, a, b);
+    k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, a, b);
     k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
         c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
         c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
                                                           c->cold, c->d_heavy, nullptr, a, b, cc);
+    k_cold_sync<<<COLD_GRID, 256, 0, s>>>(c->cold, a, b, cc, 0);
     HIP_TRY(hipGetLastError());
     return BPE_OK;
 }
@@ -507,7 +519,35 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     int rc;
     if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
-    if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
+    const bool maintained = local && c->cold_exact;
+    if (maintained) {
+        // the maintained cold table holds every cold pair exactly (the sketch is not consulted):
+        // best hot key, then the cold argmax and every pair sharing the best, one host round trip
+        if (table == c->d_hot && c->best_ready && c->best_ml == max_length)
+            HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, 2 * sizeof(unsigned), s));
+        else
+            k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand,
+                                       c->d_heavy);
+        c->best_ready = false;
+        HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
+        k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
+        k_collect<<<COLD_GRID, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
+                                            c->d_cand);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c->h_cold_flags, c->d_cold_flags, 2 * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s));
+        if ((rc = span_end(c, e_sel, 1))) return rc;
+        HIP_TRY(hipStreamSynchronize(s));
+        if ((rc = settle_with(c, c->h_res->replaced))) return rc;
+        if (c->h_cold_flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+        if ((uint64_t)c->h_cold_flags[0] * 4 > c->cold_cap * 3) {
+            // too full to probe well: this selection still reads it, the next one rebuilds it
+            c->cold_exact = false;
+            c->exact_streak = 1;
+        }
+    } else if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
         // the reduce already left the best hot key in the Result: collect its pairs and the
         // heavy sketch buckets with the whole chip
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, 2 * sizeof(unsigned), s));
@@ -516,6 +556,7 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     } else {
         k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand, c->d_heavy);
     }
+    if (!maintained) {
     c->best_ready = false;
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
@@ -545,13 +586,14 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
             }
         }
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
-        k_argmax_cold<<<256, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
-        k_collect<<<HOT_BINS / 256, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
+        k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
+        k_collect<<<COLD_GRID, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
                                                  c->d_cand);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+    }
     }
     const unsigned n_cand = std::min<unsigned>(c->h_res->n_cand, CAND_CAP);
     cand.assign(c->h_cand, c->h_cand + std::min<unsigned>(n_cand, MAX_CAND));
@@ -1097,7 +1139,9 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = dev_alloc(&c->d_cold_flags, 4))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_cand, MAX_CAND * sizeof(int2), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
-    if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_cold_flags, 4 * sizeof(uint32_t), hipHostMallocDefault) !=
+            hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
     if ((rc = dev_alloc(&c->d_repl, REPLAY_BATCH))) return bail(rc);
@@ -1126,9 +1170,11 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used,
+                    c->cold.dkeys, c->cold.dcounts,
                     c->d_ctl, c->d_log, c->d_repl};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
+    if (c->h_cold_flags) (void)hipHostFree(c->h_cold_flags);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->h_log) (void)hipHostFree(c->h_log);

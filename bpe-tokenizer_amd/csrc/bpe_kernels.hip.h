@@ -86,6 +86,10 @@ struct ColdTable {
     uint32_t *keys;
     uint32_t *counts;
     uint32_t *used;      // slots claimed this pass (for clearing and for argmax)
+    // the dense view, entry i = the i-th claimed slot: scans (argmax, collect, invalidate) stream
+    // these instead of gathering keys[used[i]] / counts[used[i]] one random line at a time
+    uint32_t *dkeys;     // written at claim time
+    uint32_t *dcounts;   // counts[used[i]] as of the last k_cold_sync
     uint32_t *n_used;
     uint32_t *overflow;  // set when a probe sequence wraps the table (capacity bug guard)
     uint32_t mask;
@@ -190,6 +194,7 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint
             if (old == EMPTY) {
                 uint32_t i = atomicAdd(ct.n_used, 1u);
                 ct.used[i] = h;
+                ct.dkeys[i] = key;
                 atomicAdd(&ct.counts[h], inc);
                 return;
             }
@@ -1320,22 +1325,29 @@ __global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
     if ((threadIdx.x & 63) == 0 && k) atomicMax(&res->best, k);
 }
 
-// argmax over the claimed cold slots.
+// argmax over the claimed cold slots (dense view, coalesced).
 __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, int64_t max_length,
                               Result *res) {
+    __shared__ unsigned long long s_best[4];
     const uint32_t n = *ct.n_used;
     unsigned long long best = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t h = ct.used[i];
-        const uint32_t key = ct.keys[h];
+        const uint32_t n_ab = ct.dcounts[i];
+        if (!n_ab || n_ab < (uint32_t)(best >> 17)) continue;   // (the key only when it can win)
+        const uint32_t key = ct.dkeys[i];
         const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        const uint32_t n_ab = ct.counts[h];
-        if (!n_ab || !pair_ok(a, b, len16, max_length)) continue;
+        if (!pair_ok(a, b, len16, max_length)) continue;
         const unsigned long long k = pack_key(n_ab, a, b);
         best = k > best ? k : best;
     }
+    // one atomic per workgroup (a wave each would queue thousands on one address)
     best = wave_max_u64(best);
-    if ((threadIdx.x & 63) == 0 && best) atomicMax(&res->best, best);
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = s_best[w] > best ? s_best[w] : best;
+        if (best) atomicMax(&res->best, best);
+    }
 }
 
 // One workgroup: best hot key (wave + LDS max), the hot pairs sharing it, and the heavy sketch
@@ -1536,12 +1548,12 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
         if (pair_ok(a, b, len16, max_length) && pack_key(hot_counts[tid], a, b) == best)
             push_cand(res, cand, a, b);
     }
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = *ct.n_used, w = (uint32_t)(best >> 17);
     for (uint32_t i = tid; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t h = ct.used[i];
-        const uint32_t key = ct.keys[h];
+        if (ct.dcounts[i] != w) continue;   // (dense view; the key only for count matches)
+        const uint32_t key = ct.dkeys[i];
         const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        if (pair_ok(a, b, len16, max_length) && pack_key(ct.counts[h], a, b) == best)
+        if (pair_ok(a, b, len16, max_length) && pack_key(w, a, b) == best)
             push_cand(res, cand, a, b);
     }
 }
@@ -1550,9 +1562,8 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
 __global__ void k_export_cold(ColdTable ct, uint32_t *keys, unsigned long long *counts) {
     const uint32_t n = *ct.n_used;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t h = ct.used[i];
-        keys[i] = ct.keys[h];
-        counts[i] = ct.counts[h];
+        keys[i] = ct.dkeys[i];
+        counts[i] = ct.counts[ct.used[i]];
     }
 }
 
@@ -1597,10 +1608,25 @@ __global__ void k_collect_list(const unsigned long long *__restrict__ hot,
 __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b) {
     const uint32_t n = *ct.n_used;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t h = ct.used[i];
-        const uint32_t key = ct.keys[h];
+        const uint32_t key = ct.dkeys[i];
         const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.counts[h] = 0;
+        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.counts[ct.used[i]] = 0;
+    }
+}
+
+// Brings the dense counts up to date after a counting pass: every entry (full, after an exact
+// pass) or only those whose count the refresh of the merge (a, b) -> cc can have changed (a side
+// in {a, b, cc}; every entry that refresh claimed has one).  Random reads for those entries only.
+__global__ void k_cold_sync(ColdTable ct, int32_t a, int32_t b, int32_t cc, int full) {
+    const uint32_t n = *ct.n_used;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        bool t = full;
+        if (!t) {
+            const uint32_t key = ct.dkeys[i];
+            const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
+            t = (x == a) | (x == b) | (x == cc) | (y == a) | (y == b) | (y == cc);
+        }
+        if (t) ct.dcounts[i] = ct.counts[ct.used[i]];
     }
 }
 
