@@ -328,7 +328,10 @@ int settle(bpe_ctx *c);
 int settle_with(bpe_ctx *c, unsigned long long R);
 int maybe_compact(bpe_ctx *c);
 
-int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
+// fused: a merge pass that also refreshes the maintained cold table (MODE_FUSED; the caller
+// invalidates the pairs with a side a or b before it and syncs the dense view after it)
+int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced,
+             bool fused = false) {
     int rc;
     if (merge && c->pending)
         if ((rc = settle(c))) return rc;
@@ -344,7 +347,15 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     hipEvent_t e_step = span_begin(c);
-    if (merge && a == b)
+    if (merge && fused && a == b)
+        k_step<MERGE_XX, MODE_FUSED><<<c->G, WG, 0, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
+            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+    else if (merge && fused)
+        k_step<MERGE_XY, MODE_FUSED><<<c->G, WG, 0, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
+            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+    else if (merge && a == b)
         k_step<MERGE_XX, MODE_TABLE><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
@@ -359,8 +370,12 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     HIP_TRY(hipGetLastError());
     if ((rc = span_end(c, e_step, 0))) return rc;
     hipEvent_t e_red = span_begin(c);
-    k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy, nullptr);
+    if (merge && fused)
+        k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(
+            c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr, a, b, cc);
+    else
+        k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(
+            c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr);
     k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
         c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res,
         nullptr);
@@ -480,34 +495,6 @@ int exact_pass(bpe_ctx *c) {
     k_cold_sync<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, -1, 1);
     HIP_TRY(hipGetLastError());
     if (c->stats_on) c->stats.exact_passes += 1;
-    return BPE_OK;
-}
-
-// The maintained cold table after the merge (a, b) -> cc has been applied (and counted): only
-// pairs with a side in {a, b, cc} changed count (every other pair keeps its occurrences and its
-// run parity), so those lose their count and one streaming pass counts every cold pair touching
-// a, b or cc exactly on the merged corpus (LDS-aggregated, no table clear).  When the table has
-// to grow, it is rebuilt by a full exact pass at the next selection instead.
-int cold_refresh(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
-    int rc;
-    const uint64_t cap0 = c->cold_cap;
-    if ((rc = ensure_cold(c, 0))) return rc;
-    if (c->cold_cap != cap0 || !c->cold_exact) {
-        c->cold_exact = false;
-        return BPE_OK;
-    }
-    if (!c->carry_valid)
-        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    geometry(c);
-    hipStream_t s = c->stream;
-    k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, a, b);
-    k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
-        c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
-        c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
-    k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy, nullptr, a, b, cc);
-    k_cold_sync<<<COLD_GRID, 256, 0, s>>>(c->cold, a, b, cc, 0);
-    HIP_TRY(hipGetLastError());
     return BPE_OK;
 }
 
@@ -694,8 +681,27 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     if (c->n_live < 2) return BPE_OK;
     if (!c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
-    if ((rc = run_pass(c, true, a, b, cc, replaced))) return rc;
-    return c->cold_exact ? cold_refresh(c, a, b, cc) : BPE_OK;
+    // a maintained cold table is refreshed by the merge pass itself: the pairs with a side in
+    // {a, b, cc} are the only ones whose count the merge changes (every other pair keeps its
+    // occurrences and its run parity), so those lose their count before the pass and the pass
+    // counts them again on the merged corpus.  A table that has to grow is rebuilt by a full
+    // exact pass at the next selection instead.
+    bool fused = false;
+    if (c->cold_exact) {
+        const uint64_t cap0 = c->cold_cap;
+        const int64_t na = c->h_count[a], nb = c->h_count[b];
+        const uint64_t bound = (uint64_t)std::max<int64_t>(0, a == b ? na / 2 : std::min(na, nb));
+        if ((rc = ensure_cold(c, bound))) return rc;
+        fused = c->cold_exact && c->cold_cap == cap0 && !getenv("BPE_DEBUG_NO_FUSED");
+        if (!fused) c->cold_exact = false;
+    }
+    if (fused) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
+    if ((rc = run_pass(c, true, a, b, cc, replaced, fused))) return rc;
+    if (fused) {
+        k_cold_sync<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b, cc, 0);
+        HIP_TRY(hipGetLastError());
+    }
+    return BPE_OK;
 }
 
 // Up to n mergeUntil iterations with the decisions kept on the device (core.ts:367-384): per

@@ -58,7 +58,9 @@ constexpr int HIST_WORDS = TABLE_BINS / 2;  // two 16-bit counters per LDS dword
 constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets needing exact counts
 // What a streaming pass does with the pairs it sees: the pair table, exact counts of the cold
 // pairs in heavy sketch buckets, or nothing (apply-only replay: restoreMerge, batch encoding).
-enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1, MODE_NONE = 2 };
+// MODE_FUSED: a merge pass that also refreshes the maintained cold table (the table counts plus
+// MODE_EXACT's refresh of the pairs with a side in {ma, mb, mc}, in one stream of the corpus)
+enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1, MODE_NONE = 2, MODE_FUSED = 3 };
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -195,6 +197,7 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint
                 uint32_t i = atomicAdd(ct.n_used, 1u);
                 ct.used[i] = h;
                 ct.dkeys[i] = key;
+                ct.dcounts[i] = 0;   // (set by the k_cold_sync that follows the pass)
                 atomicAdd(&ct.counts[h], inc);
                 return;
             }
@@ -263,8 +266,9 @@ template <int MODE>
 __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32_t y,
                                                  unsigned long long n) {
     if (n == 0 || MODE == MODE_NONE) return;
-    if (MODE == MODE_TABLE) atomicAdd(&k.spill[table_index(x, y)], n);
-    else if (exact_wanted<MODE>(k, x, y)) cold_add(k.ct, pair_key(x, y), (uint32_t)n);
+    if (MODE == MODE_TABLE || MODE == MODE_FUSED) atomicAdd(&k.spill[table_index(x, y)], n);
+    if (MODE != MODE_TABLE && exact_wanted<MODE>(k, x, y))
+        cold_add(k.ct, pair_key(x, y), (uint32_t)n);
 }
 
 // The LDS table: 16-bit counters, two per dword.
@@ -294,9 +298,15 @@ __device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | (
 
 // The same from the pair, as two instructions (the compiler otherwise re-associates the mask and
 // the shift into three, for lack of a second literal operand)
+template <bool FUSED = false>
 __device__ __forceinline__ uint32_t cold_addr_of(int32_t x, int32_t y) {
     uint32_t b, a;
-    asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
+    // MODE_FUSED folds the sketch into its lower half (the maintained cold table makes the sketch
+    // unused; the upper half holds the refresh's LDS hash)
+    if (FUSED)
+        asm("v_bfe_u32 %0, %1, 0, 12" : "=v"(b) : "v"(sketch_hash(x, y)));
+    else
+        asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
     asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(a) : "v"(b), "s"(HOT_BYTES));
     return a;
 }
@@ -343,22 +353,45 @@ __device__ __forceinline__ void lds_cold_add(const Sink &k, uint32_t key, uint32
     cold_add(k.ct, key, inc);
 }
 
+// MODE_FUSED's LDS hash: the upper half of the sketch dwords, (key, count) x 2048.
+constexpr int FH_BITS = 11;
+constexpr int FH_SLOTS = 1 << FH_BITS;
+constexpr int FH_BASE = HOT_BINS / 2 + 2 * FH_SLOTS;   // dword index of the first key
+static_assert(FH_BASE + 2 * FH_SLOTS == HIST_WORDS, "fused LDS hash = upper half of the sketch");
+
+__device__ __forceinline__ void lds_fused_add(const Sink &k, uint32_t key, uint32_t inc) {
+    uint32_t *keys = k.hist + FH_BASE;
+    uint32_t *cnt = keys + FH_SLOTS;
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - FH_BITS);
+    for (int p = 0; p < LH_PROBES; ++p) {
+        uint32_t kk = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kk == EMPTY) kk = atomicCAS(&keys[h], EMPTY, key);
+        if (kk == EMPTY || kk == key) {
+            atomicAdd(&cnt[h], inc);
+            return;
+        }
+        h = (h + 1) & (FH_SLOTS - 1);
+    }
+    cold_add(k.ct, key, inc);
+}
+
 // One counted occurrence of (x, y) (outside the streaming fast paths).
 template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
     if (MODE == MODE_NONE) return;
-    if (MODE == MODE_TABLE) {
+    if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         uint32_t addr, inc, bin;
         if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) {
             addr = hot_addr(x, y);
             inc = hot_inc(x);
             bin = hot_bin((uint32_t)x, (uint32_t)y);
         } else {
-            addr = cold_addr(sketch_hash(x, y));
+            addr = cold_addr(MODE == MODE_FUSED ? sketch_hash(x, y) & 0xFFFu : sketch_hash(x, y));
             inc = hot_inc(x);
             bin = HOT_BINS + sketch_bucket(x, y);
         }
         lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
+        if (MODE == MODE_FUSED && exact_wanted<MODE>(k, x, y)) lds_fused_add(k, pair_key(x, y), 1u);
     } else if (exact_wanted<MODE>(k, x, y)) {
         lds_cold_add(k, pair_key(x, y), 1u);
     }
@@ -656,21 +689,23 @@ struct Tally {
 // opaque to the compiler so both uses below read it as is), the class select (two), and the
 // increment (three): hot_inc(x) for a valid pair, 0 when a side is negative (SEP, dead), with the
 // validity bit (u's sign) as the value shifted.  Pairs with a cold side go to their sketch bucket.
+template <bool FUSED = false>
 __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, uint32_t &inc) {
     uint32_t u = ~((uint32_t)x | (uint32_t)y);
     asm("" : "+v"(u));
     const uint32_t hot = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
-    addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of(x, y));   // both ids < 256
+    addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of<FUSED>(x, y));   // both ids < 256
     inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
 }
 
+template <bool FUSED = false>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
                                           const Sink &k) {
     uint32_t o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t addr, inc;
-        pair_slot(x[e], y[e], addr, inc);
+        pair_slot<FUSED>(x[e], y[e], addr, inc);
         o[e] = atomicAdd(lds_word(k, addr), inc);
     }
     // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
@@ -681,10 +716,38 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
             int32_t xx = x[e], yy = y[e];
             asm volatile("" : "+v"(xx), "+v"(yy));
             uint32_t addr, inc;
-            pair_slot(xx, yy, addr, inc);
+            pair_slot<FUSED>(xx, yy, addr, inc);
             if (inc) lds_fix(k, addr, inc, (uint32_t)table_index(xx, yy), o[e]);
         }
     }
+}
+
+// The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (a cold-table refresh,
+// MODE_EXACT with ma >= 0, or MODE_FUSED): per-token membership masks (compares into lane masks,
+// combined on the scalar unit), one wave-wide test, and the LDS hash only in chunks that hold
+// such a cold pair.  (t3 differs from x3 only in lane 63 of a partial chunk, where pair 2's right
+// side is the tail tag, negative: that pair is not live either way.)
+template <int MODE>
+__device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t t1, int32_t t2,
+                                              int32_t x3, int32_t r3, const int32_t (&x)[4],
+                                              const int32_t (&y)[4]) {
+    const int32_t ma = k.ma, mb = k.mb, mc = k.mc;
+    const unsigned long long M0 = __ballot((t0 == ma) | (t0 == mb) | (t0 == mc)),
+                             M1 = __ballot((t1 == ma) | (t1 == mb) | (t1 == mc)),
+                             M2 = __ballot((t2 == ma) | (t2 == mb) | (t2 == mc)),
+                             M3 = __ballot((x3 == ma) | (x3 == mb) | (x3 == mc)),
+                             M4 = __ballot((r3 == ma) | (r3 == mb) | (r3 == mc));
+    const unsigned long long W0 = M0 | M1, W1 = M1 | M2, W2 = M2 | M3, W3 = M3 | M4;
+    if ((W0 | W1 | W2 | W3) == 0ull) return;
+    const unsigned long long Wm[4] = {W0, W1, W2, W3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (lane_in(Wm[e]) & ((x[e] | y[e]) >= HOT)) {
+            if (MODE == MODE_FUSED)
+                lds_fused_add(k, pair_key(x[e], y[e]), 1u);
+            else
+                lds_cold_add(k, pair_key(x[e], y[e]), 1u);
+        }
 }
 
 // Counts the pairs of one post-merge chunk (len > 0) whose right side lies inside the region:
@@ -739,7 +802,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     if (!TAIL && (trip | (E3 & P63) | lead) == 0ull) {
         // every X X pair starts its run, so every valid pair counts
         const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
-        if (MODE == MODE_TABLE) {
+        if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
             // full chunks of hot tokens only (a fresh corpus): unmasked adds
             unsigned long long cold = 1;
             if (P63 == 0ull) {
@@ -762,12 +825,17 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 }
             } else {
                 // mixed planes (partial chunks hold merged tokens: the steady state)
-                add_pairs(x, y, k);
+                add_pairs<MODE == MODE_FUSED>(x, y, k);
+                if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
             }
         } else if (MODE == MODE_EXACT) {
+            if (k.ma >= 0) {
+                refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
+                for (int e = 0; e < 4; ++e)
+                    if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
+            }
         }
         // the last token starts its run here (a run continuing into the next chunk would be a run
         // of three, or a partial chunk's X X end), so its offset parity is 0
@@ -958,9 +1026,15 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                                           const uint32_t *__restrict__ heavy_g,
                                           RegionSum *__restrict__ sums,
                                           unsigned long long *__restrict__ replaced) {
-    if (MODE == MODE_TABLE) {
+    if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
+        // (MODE_FUSED: the LDS hash's keys start EMPTY; one store per dword, so no two threads
+        // write the same dword before the barrier)
         uint4 *h4 = reinterpret_cast<uint4 *>(hist);
-        for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) h4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) {
+            const bool key = MODE == MODE_FUSED && i >= FH_BASE / 4 && i < (FH_BASE + FH_SLOTS) / 4;
+            const uint32_t v = key ? EMPTY : 0u;
+            h4[i] = make_uint4(v, v, v, v);
+        }
     } else if (MODE == MODE_EXACT) {
         for (int i = threadIdx.x; i < HEAVY_WORDS; i += WG) hist[i] = heavy_g[i];
         for (int i = threadIdx.x; i < LH_SLOTS; i += WG) {
@@ -974,7 +1048,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.spill = spill;
     k.ct = ct;
     k.heavy = hist;
-    k.ma = MODE == MODE_EXACT ? ma : -1;
+    k.ma = MODE == MODE_EXACT || MODE == MODE_FUSED ? ma : -1;
     k.mb = mb;
     k.mc = mc;
     const int lane = threadIdx.x & 63;
@@ -1087,11 +1161,16 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             if (MERGE && ap.n_match) atomicAdd(replaced, (unsigned long long)ap.n_match);
         }
     }
-    if (MODE == MODE_TABLE) {
+    if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         __syncthreads();
         uint4 *out = reinterpret_cast<uint4 *>(partials + (size_t)blockIdx.x * HIST_WORDS);
         const uint4 *h4 = reinterpret_cast<const uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
+        if (MODE == MODE_FUSED)   // (the slab's sketch dwords are then garbage: unused)
+            for (int i = threadIdx.x; i < FH_SLOTS; i += WG) {
+                const uint32_t key = hist[FH_BASE + i];
+                if (key != EMPTY) cold_add(ct, key, hist[FH_BASE + FH_SLOTS + i]);
+            }
     } else if (MODE == MODE_EXACT) {
         __syncthreads();
         for (int i = threadIdx.x; i < LH_SLOTS; i += WG) {
@@ -1171,7 +1250,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.spill = spill;
     k.ct = ct;
     k.heavy = heavy;
-    k.ma = MODE == MODE_EXACT ? ma : -1;
+    k.ma = MODE == MODE_EXACT || MODE == MODE_FUSED ? ma : -1;
     k.mb = mb;
     k.mc = mc;
     const int p = prev_nonempty(s, r - 1);
