@@ -134,7 +134,8 @@ def main():
         # from inside the timed run)
         traffic = {}
         tpath = os.path.join(ROOT, 'profiles', 'current_pmc.json')
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and args.corpus == 'uniform':
+            # (the committed passes were taken on the uniform C3 run: no traffic for other corpora)
             traffic = json.load(open(tpath))
         k1_ms = st['step_ms'] / max(1, st['step_launches'])
         live_per_launch = st['step_live'] / max(1, st['step_launches'])

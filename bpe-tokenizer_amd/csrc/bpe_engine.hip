@@ -233,6 +233,14 @@ int sync_len16(bpe_ctx *c, int64_t max_length) {
 constexpr int COLD_GRID = 1024;
 static_assert(COLD_GRID * 256 >= HOT_BINS, "k_collect covers the hot bins");
 
+// Empties the cold table: free slots, zero dense counts (the invariant past n_used), n_used = 0.
+int cold_clear(bpe_ctx *c) {
+    HIP_TRY(hipMemsetAsync(c->cold.slots, 0xFF, c->cold_cap * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->cold.dcounts, 0, c->cold_cap * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), c->stream));
+    return BPE_OK;
+}
+
 int ensure_cold(bpe_ctx *c, uint64_t extra) {
     uint64_t s = extra;
     for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
@@ -245,20 +253,13 @@ int ensure_cold(bpe_ctx *c, uint64_t extra) {
     if (cap <= c->cold_cap) return BPE_OK;
     if (cap > (1ull << 31)) return fail(BPE_ERR_OOM, "bpe native: cold pair table too large");
     HIP_TRY(hipStreamSynchronize(c->stream));
-    dfree(c->cold.keys);
-    dfree(c->cold.counts);
-    dfree(c->cold.used);
+    dfree(c->cold.slots);
     dfree(c->cold.dkeys);
     dfree(c->cold.dcounts);
     int rc;
-    if ((rc = dev_alloc(&c->cold.keys, cap))) return rc;
-    if ((rc = dev_alloc(&c->cold.counts, cap))) return rc;
-    if ((rc = dev_alloc(&c->cold.used, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.slots, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.dkeys, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.dcounts, cap))) return rc;
-    HIP_TRY(hipMemsetAsync(c->cold.keys, 0xFF, cap * sizeof(uint32_t), c->stream));
-    HIP_TRY(hipMemsetAsync(c->cold.counts, 0, cap * sizeof(uint32_t), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), c->stream));
     c->cold_cap = cap;
     c->cold.mask = (uint32_t)(cap - 1);
     int lg = 0;
@@ -268,7 +269,7 @@ int ensure_cold(bpe_ctx *c, uint64_t extra) {
     c->cold.overflow = c->d_cold_flags + 1;
     c->counts_valid = false;
     c->cold_exact = false;
-    return BPE_OK;
+    return cold_clear(c);
 }
 
 float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -480,8 +481,7 @@ int exact_pass(bpe_ctx *c) {
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     geometry(c);
     hipStream_t s = c->stream;
-    k_cold_clear<<<1024, 256, 0, s>>>(c->cold);
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), s));
+    if ((rc = cold_clear(c))) return rc;
     k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
         c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
         c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
@@ -492,8 +492,6 @@ int exact_pass(bpe_ctx *c) {
     HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
-    k_cold_sync<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, -1, 1);
-    HIP_TRY(hipGetLastError());
     if (c->stats_on) c->stats.exact_passes += 1;
     return BPE_OK;
 }
@@ -697,10 +695,6 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     }
     if (fused) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
     if ((rc = run_pass(c, true, a, b, cc, replaced, fused))) return rc;
-    if (fused) {
-        k_cold_sync<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b, cc, 0);
-        HIP_TRY(hipGetLastError());
-    }
     return BPE_OK;
 }
 
@@ -1175,8 +1169,7 @@ int bpe_destroy(bpe_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
-                    c->d_heavy, c->d_cold_flags, c->cold.keys, c->cold.counts, c->cold.used,
-                    c->cold.dkeys, c->cold.dcounts,
+                    c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
                     c->d_ctl, c->d_log, c->d_repl};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);

@@ -85,16 +85,17 @@ struct RegionCarry {
 
 // Sparse pair table for pairs with an id >= HOT: open addressing on key = a << 16 | b.
 struct ColdTable {
-    uint32_t *keys;
-    uint32_t *counts;
-    uint32_t *used;      // slots claimed this pass (for clearing and for argmax)
-    // the dense view, entry i = the i-th claimed slot: scans (argmax, collect, invalidate) stream
-    // these instead of gathering keys[used[i]] / counts[used[i]] one random line at a time
-    uint32_t *dkeys;     // written at claim time
-    uint32_t *dcounts;   // counts[used[i]] as of the last k_cold_sync
+    // open-addressing hash of the claimed pairs: slot = (key << 32) | dense index, EMPTY64 = free
+    unsigned long long *slots;
+    // the dense arrays, entry i = the i-th claimed index (claim order): every scan (argmax,
+    // collect, invalidate, export) streams these coalesced, and the counts live here, so a scan
+    // never gathers hashed slots.  A claim that loses its slot race leaves a hole (key EMPTY,
+    // count 0).  dcounts[i] == 0 for every i >= *n_used (zeroed with the table).
+    uint32_t *dkeys;
+    uint32_t *dcounts;
     uint32_t *n_used;
-    uint32_t *overflow;  // set when a probe sequence wraps the table (capacity bug guard)
-    uint32_t mask;
+    uint32_t *overflow;  // set when a probe sequence wraps the table or the dense arrays fill up
+    uint32_t mask;       // slots - 1 (= dense capacity - 1)
     uint32_t shift;
 };
 
@@ -179,35 +180,37 @@ __device__ __forceinline__ uint32_t pack_pair_s(int32_t x, int32_t y) {
     return ((uint32_t)x << 16) | ((uint32_t)y & 0xFFFFu);
 }
 
+constexpr unsigned long long EMPTY64 = ~0ull;
+
 __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint32_t inc) {
     uint32_t h = (key * 0x9E3779B1u) >> ct.shift;
-    for (uint32_t probes = 0;; ++probes) {
-        if (probes > ct.mask) {
-            atomicOr(ct.overflow, 1u);
-            return;
-        }
-        uint32_t k = __hip_atomic_load(&ct.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == key) {
-            atomicAdd(&ct.counts[h], inc);
-            return;
-        }
-        if (k == EMPTY) {
-            uint32_t old = atomicCAS(&ct.keys[h], EMPTY, key);
-            if (old == EMPTY) {
-                uint32_t i = atomicAdd(ct.n_used, 1u);
-                ct.used[i] = h;
-                ct.dkeys[i] = key;
-                ct.dcounts[i] = 0;   // (set by the k_cold_sync that follows the pass)
-                atomicAdd(&ct.counts[h], inc);
+    uint32_t mine = EMPTY;   // the dense index this call reserved (at its first free slot)
+    for (uint32_t probes = 0; probes <= ct.mask; ++probes) {
+        unsigned long long v =
+            __hip_atomic_load(&ct.slots[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == EMPTY64) {
+            if (mine == EMPTY) {
+                mine = atomicAdd(ct.n_used, 1u);
+                if (mine > ct.mask) {
+                    atomicOr(ct.overflow, 1u);
+                    return;
+                }
+                ct.dkeys[mine] = key;
+            }
+            v = atomicCAS(&ct.slots[h], EMPTY64, ((unsigned long long)key << 32) | mine);
+            if (v == EMPTY64) {
+                atomicAdd(&ct.dcounts[mine], inc);
                 return;
             }
-            if (old == key) {
-                atomicAdd(&ct.counts[h], inc);
-                return;
-            }
+        }
+        if ((uint32_t)(v >> 32) == key) {
+            atomicAdd(&ct.dcounts[(uint32_t)v], inc);
+            if (mine != EMPTY) ct.dkeys[mine] = EMPTY;   // (lost the race for this key: a hole)
+            return;
         }
         h = (h + 1) & ct.mask;
     }
+    atomicOr(ct.overflow, 1u);
 }
 
 __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
@@ -1642,7 +1645,7 @@ __global__ void k_export_cold(ColdTable ct, uint32_t *keys, unsigned long long *
     const uint32_t n = *ct.n_used;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         keys[i] = ct.dkeys[i];
-        counts[i] = ct.counts[ct.used[i]];
+        counts[i] = ct.dcounts[i];   // (a hole exports count 0)
     }
 }
 
@@ -1652,6 +1655,7 @@ __global__ void k_argmax_list(const uint32_t *__restrict__ keys,
     unsigned long long best = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
+        if (!counts[i]) continue;   // (holes: count 0, key EMPTY)
         const int32_t a = (int32_t)(keys[i] >> 16), b = (int32_t)(keys[i] & 0xFFFFu);
         if (!pair_ok(a, b, len16, max_length)) continue;
         const unsigned long long k = pack_key(counts[i], a, b);
@@ -1675,6 +1679,7 @@ __global__ void k_collect_list(const unsigned long long *__restrict__ hot,
             push_cand(res, cand, a, b);
     }
     for (int64_t i = tid; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (counts[i] != (best >> 17)) continue;   // (holes: count 0)
         const int32_t a = (int32_t)(keys[i] >> 16), b = (int32_t)(keys[i] & 0xFFFFu);
         if (pair_ok(a, b, len16, max_length) && pack_key(counts[i], a, b) == best)
             push_cand(res, cand, a, b);
@@ -1689,34 +1694,10 @@ __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t key = ct.dkeys[i];
         const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.counts[ct.used[i]] = 0;
+        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.dcounts[i] = 0;
     }
 }
 
-// Brings the dense counts up to date after a counting pass: every entry (full, after an exact
-// pass) or only those whose count the refresh of the merge (a, b) -> cc can have changed (a side
-// in {a, b, cc}; every entry that refresh claimed has one).  Random reads for those entries only.
-__global__ void k_cold_sync(ColdTable ct, int32_t a, int32_t b, int32_t cc, int full) {
-    const uint32_t n = *ct.n_used;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        bool t = full;
-        if (!t) {
-            const uint32_t key = ct.dkeys[i];
-            const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-            t = (x == a) | (x == b) | (x == cc) | (y == a) | (y == b) | (y == cc);
-        }
-        if (t) ct.dcounts[i] = ct.counts[ct.used[i]];
-    }
-}
-
-__global__ void k_cold_clear(ColdTable ct) {
-    const uint32_t n = *ct.n_used;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t h = ct.used[i];
-        ct.keys[h] = EMPTY;
-        ct.counts[h] = 0;
-    }
-}
 
 // ---------------------------------------------------------------------------------------------
 // K3 tie pass (rule R3): last counted occurrence (slot + 1) of up to MAX_CAND tied pairs on the

@@ -24,9 +24,9 @@ def hot_diff(e, st):
     want = np.zeros(65536, np.int64)
     for a, b, c in zip(pa.tolist(), pb.tolist(), pc.tolist()):
         if a < 256 and b < 256:
-            want[(a << 8) | b] += c
+            want[(b << 8) | a] += c   # hot bin b*256 + a (the LDS counter order)
     d = np.nonzero(t[:65536] != want)[0]
-    return [(int(i >> 8), int(i & 255), int(t[i]), int(want[i])) for i in d[:10]]
+    return [(int(i & 255), int(i >> 8), int(t[i]), int(want[i])) for i in d[:10]]
 
 
 def main():

@@ -10,5 +10,6 @@ fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
     -- python3 bench.py --corpus zipf --no-cpu-baseline > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kstats.csv" \;
+python3 tools/ktrace_buckets.py "$(find "$OUT/trace" -name "*kernel_trace.csv" | head -1)" 1000 6 || true
 rm -f "$OUT"/trace/*kernel_trace.csv
 python3 tools/kstats.py "$OUT/kstats.csv" "$OUT/bench.jsonl"
