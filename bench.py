@@ -137,7 +137,9 @@ def main():
         if os.path.exists(tpath) and args.corpus == 'uniform':
             # (the committed passes were taken on the uniform C3 run: no traffic for other corpora)
             traffic = json.load(open(tpath))
-        k1_ms = st['step_ms'] / max(1, st['step_launches'])
+        # (the device loop times every 8th iteration: step_ms and select_ms cover step_timed passes)
+        k1_ms = st['step_ms'] / max(1, st['step_timed'])
+        timed_frac = st['step_timed'] / max(1, st['step_launches'])
         live_per_launch = st['step_live'] / max(1, st['step_launches'])
         slots_per_launch = st['step_slots'] / max(1, st['step_launches'])
         achieved = ALG_BYTES_PER_PAIR_SCAN * live_per_launch / (k1_ms * 1e-3) / 1e9
@@ -181,8 +183,8 @@ def main():
                 'traffic_source': traffic.get('source'),
             },
             'breakdown_ms_per_step': {
-                'stream_pass': st['step_ms'] / max(1, args.steps),
-                'select': st['select_ms'] / max(1, args.steps),
+                'stream_pass': k1_ms * st['step_launches'] / max(1, args.steps),
+                'select': st['select_ms'] / max(1e-9, timed_frac) / max(1, args.steps),
                 'tie_passes': st['tie_passes'],
                 'compactions': st['compactions'],
                 'exact_passes': st['exact_passes'],

@@ -244,12 +244,13 @@ __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
 // Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup LDS table (exact hot bins +
 // cold sketch buckets, 16-bit counters) with a global u64 spill.  MODE_EXACT: exact counts of the
 // cold pairs whose sketch bucket is marked heavy, into the sparse table; the rest is ignored.
+// MODE_FUSED: the table (sketch folded) plus the cold pairs with a side in {ma, mb, mc}.
 struct Sink {
     uint32_t *hist;                  // LDS table (MODE_TABLE)
     unsigned long long *spill;       // global u64 [TABLE_BINS]
     ColdTable ct;
     const uint32_t *heavy;           // LDS bitmap [HEAVY_WORDS] (MODE_EXACT)
-    // MODE_EXACT with ma >= 0: the maintained cold table's refresh after the merge (ma, mb) -> mc:
+    // MODE_FUSED (ma >= 0): the maintained cold table's refresh after the merge (ma, mb) -> mc,
     // every cold pair with a side in {ma, mb, mc}, whatever its bucket (heavy is then unused)
     int32_t ma, mb, mc;
 };
@@ -725,8 +726,8 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
     }
 }
 
-// The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (a cold-table refresh,
-// MODE_EXACT with ma >= 0, or MODE_FUSED): per-token membership masks (compares into lane masks,
+// The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (MODE_FUSED's refresh
+// of the maintained cold table): per-token membership masks (compares into lane masks,
 // combined on the scalar unit), one wave-wide test, and the LDS hash only in chunks that hold
 // such a cold pair.  (t3 differs from x3 only in lane 63 of a partial chunk, where pair 2's right
 // side is the tail tag, negative: that pair is not live either way.)
@@ -746,10 +747,7 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
 #pragma unroll
     for (int e = 0; e < 4; ++e)
         if (lane_in(Wm[e]) & ((x[e] | y[e]) >= HOT)) {
-            if (MODE == MODE_FUSED)
-                lds_fused_add(k, pair_key(x[e], y[e]), 1u);
-            else
-                lds_cold_add(k, pair_key(x[e], y[e]), 1u);
+            lds_fused_add(k, pair_key(x[e], y[e]), 1u);
         }
 }
 
@@ -832,13 +830,9 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
             }
         } else if (MODE == MODE_EXACT) {
-            if (k.ma >= 0) {
-                refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
-            } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
-            }
+            for (int e = 0; e < 4; ++e)
+                if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
         }
         // the last token starts its run here (a run continuing into the next chunk would be a run
         // of three, or a partial chunk's X X end), so its offset parity is 0
@@ -1051,7 +1045,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.spill = spill;
     k.ct = ct;
     k.heavy = hist;
-    k.ma = MODE == MODE_EXACT || MODE == MODE_FUSED ? ma : -1;
+    k.ma = MODE == MODE_FUSED ? ma : -1;
     k.mb = mb;
     k.mc = mc;
     const int lane = threadIdx.x & 63;
@@ -1253,7 +1247,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.spill = spill;
     k.ct = ct;
     k.heavy = heavy;
-    k.ma = MODE == MODE_EXACT || MODE == MODE_FUSED ? ma : -1;
+    k.ma = MODE == MODE_FUSED ? ma : -1;
     k.mb = mb;
     k.mc = mc;
     const int p = prev_nonempty(s, r - 1);
@@ -1343,6 +1337,15 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         acc[7] += p.w >> 16;
     };
     int g = grp;
+    // 16 slab loads in flight per thread (the slabs were just written: latency-bound, not
+    // bandwidth-bound)
+    for (; g + 120 < G; g += 128) {
+        uint4 p[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[q] = p4[(size_t)(g + 8 * q) * (HIST_WORDS / 4)];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) add(p[q]);
+    }
     for (; g + 56 < G; g += 64) {
         uint4 p[8];
 #pragma unroll
@@ -1367,8 +1370,15 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
     unsigned long long k = 0;
     if (bin < HOT_BINS && v && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
         k = pack_key(v, bin_a(bin), bin_b(bin));
+    // one atomic per workgroup (a wave each would queue over a thousand on one address)
     k = wave_max_u64(k);
-    if ((t & 63) == 0 && k && res) atomicMax(&res->best, k);
+    __shared__ unsigned long long s_best[4];
+    if ((t & 63) == 0) s_best[t >> 6] = k;
+    __syncthreads();
+    if (t == 0 && res) {
+        for (int w = 1; w < 4; ++w) k = s_best[w] > k ? s_best[w] : k;
+        if (k) atomicMax(&res->best, k);
+    }
 }
 
 // Marks the sketch buckets whose (global) sum reaches the best hot count: only cold pairs there

@@ -191,6 +191,9 @@ typedef struct {
     int64_t live_tokens;      /* sum over those calls of live corpus tokens (pair-scans) */
     int64_t compactions;      /* dead-slot compactions */
     int64_t exact_passes;     /* extra streaming passes for cold pairs whose sketch bucket could win */
+    int64_t step_timed;       /* streaming passes whose duration step_ms sums (the device loop times
+                                 every SPAN_EVERY-th iteration, all of its spans; select_ms covers
+                                 those same iterations) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

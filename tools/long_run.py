@@ -39,7 +39,7 @@ def main():
         done += len(got)
         print(json.dumps({
             'merges': done, 'wall_ms_per_merge': dt * 1e3 / max(1, len(got)),
-            'pass_ms': st['step_ms'] / max(1, st['step_launches']),
+            'pass_ms': st['step_ms'] / max(1, st['step_timed']),
             'launches': st['step_launches'], 'select_ms': st['select_ms'] / max(1, len(got)),
             'exact_passes': st['exact_passes'], 'tie_passes': st['tie_passes'],
             'compactions': st['compactions'], 'live': st['live_tokens'] / max(1, st['iterations']),

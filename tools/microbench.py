@@ -44,11 +44,11 @@ def main():
     live = rc['step_live'] / rc['step_launches']
     out = {
         'corpus_mib': mib, 'pre_merges': pre, 'ingest_s': ingest,
-        'recount_ms': rc['step_ms'] / rc['step_launches'],
-        'recount_GBps_alg': 4 * live / (rc['step_ms'] / rc['step_launches'] * 1e-3) / 1e9,
-        'merge_pass_ms': st['step_ms'] / max(1, st['step_launches']),
+        'recount_ms': rc['step_ms'] / max(1, rc['step_timed']),
+        'recount_GBps_alg': 4 * live / (rc['step_ms'] / max(1, rc['step_timed']) * 1e-3) / 1e9,
+        'merge_pass_ms': st['step_ms'] / max(1, st['step_timed']),
         'merge_pass_GBps_alg': 4 * st['step_live'] / max(1, st['step_launches']) /
-                               (st['step_ms'] / max(1, st['step_launches']) * 1e-3) / 1e9,
+                               (st['step_ms'] / max(1, st['step_timed']) * 1e-3) / 1e9,
         'select_ms_per_iter': st['select_ms'] / steps,
         'wall_ms_per_iter': dt * 1e3 / steps,
         'tie_passes': st['tie_passes'], 'exact_passes': st['exact_passes'], 'compactions': st['compactions'],
