@@ -634,8 +634,13 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
             int64_t *w) {
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
     int rc;
-    if ((rc = settle(c))) return rc;
-    if (c->n_live < 2) return BPE_NO_MERGE;
+    // with a maintained cold table the selection settles a pending merge from the Result it
+    // copies back anyway, so the host does not wait for the merge pass before enqueueing it
+    const bool deferred = c->pending && c->cold_exact && c->counts_valid;
+    if (!deferred) {
+        if ((rc = settle(c))) return rc;
+        if (c->n_live < 2) return BPE_NO_MERGE;
+    }
     if (!c->counts_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     c->opt_max_length = max_length;
@@ -1456,9 +1461,13 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     // rests for a few host iterations (backing off up to 16) before it is tried again.
     int64_t batch = LOOP_BATCH, rest = 0, backoff = 0;
     while (!max_iterations || n < max_iterations) {                      // core.ts:374-378
-        if ((rc = settle(c))) return rc;
-        if (c->n_live < 2) break;
-        if ((rc = maybe_compact(c))) return rc;
+        // (a maintained cold table: do_find settles the pending merge with its selection, and
+        // do_apply compacts)
+        if (!(c->pending && c->cold_exact)) {
+            if ((rc = settle(c))) return rc;
+            if (c->n_live < 2) break;
+            if ((rc = maybe_compact(c))) return rc;
+        }
         // batches on the device while the vocabulary has room (the host path reports the limit)
         int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)c->h_len16.size());
         if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
