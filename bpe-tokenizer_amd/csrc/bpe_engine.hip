@@ -89,7 +89,6 @@ struct bpe_ctx {
     RegionCarry *d_carry = nullptr;
     int64_t *d_outoff = nullptr;
     Result *d_res = nullptr, *h_res = nullptr;
-    uint32_t *h_cold_flags = nullptr;   // pinned copy of d_cold_flags
     int2 *d_cand = nullptr;
     ColdTable cold{};
     uint32_t *d_cold_flags = nullptr;   // [0] n_used, [1] overflow
@@ -515,26 +514,26 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     if (maintained) {
         // the maintained cold table holds every cold pair exactly (the sketch is not consulted):
         // best hot key, then the cold argmax and every pair sharing the best, one host round trip
-        if (table == c->d_hot && c->best_ready && c->best_ml == max_length)
+        if (table == c->d_hot && c->best_ready && c->best_ml == max_length) {
             HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, 2 * sizeof(unsigned), s));
-        else
+        } else {
             k_select<<<1, 1024, 0, s>>>(table, c->d_len16, max_length, c->d_res, c->d_cand,
                                        c->d_heavy);
+            HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
+        }
         c->best_ready = false;
-        HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
         k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
         k_collect<<<COLD_GRID, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
                                             c->d_cand);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_res, c->d_res, sizeof(Result), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand, MAX_CAND * sizeof(int2), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(c->h_cold_flags, c->d_cold_flags, 2 * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, s));
         if ((rc = span_end(c, e_sel, 1))) return rc;
         HIP_TRY(hipStreamSynchronize(s));
         if ((rc = settle_with(c, c->h_res->replaced))) return rc;
-        if (c->h_cold_flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
-        if ((uint64_t)c->h_cold_flags[0] * 4 > c->cold_cap * 3) {
+        const uint64_t flags = c->h_res->cold_flags;
+        if (flags >> 32) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+        if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3) {
             // too full to probe well: this selection still reads it, the next one rebuilds it
             c->cold_exact = false;
             c->exact_streak = 1;
@@ -1155,9 +1154,7 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = dev_alloc(&c->d_cold_flags, 4))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_cand, MAX_CAND * sizeof(int2), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
-    if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_cold_flags, 4 * sizeof(uint32_t), hipHostMallocDefault) !=
-            hipSuccess)
+    if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
     if ((rc = dev_alloc(&c->d_repl, REPLAY_BATCH))) return bail(rc);
@@ -1189,7 +1186,6 @@ int bpe_destroy(bpe_ctx *c) {
                     c->d_ctl, c->d_log, c->d_repl};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
-    if (c->h_cold_flags) (void)hipHostFree(c->h_cold_flags);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->h_log) (void)hipHostFree(c->h_log);

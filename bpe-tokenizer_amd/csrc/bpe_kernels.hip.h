@@ -105,7 +105,7 @@ struct Result {
     unsigned int n_heavy;                // sketch buckets that need exact cold counts
     unsigned long long last[MAX_CAND];   // R3: slot + 1 of the last counted occurrence
     unsigned long long replaced;         // apply: replacement count
-    unsigned long long pad1;
+    unsigned long long cold_flags;       // k_argmax_cold: (overflow << 32) | n_used of the cold table
 };
 
 // Device-resident mergeUntil loop (core.ts:367-384): the decision of each iteration stays in HBM and
@@ -1422,6 +1422,8 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
                               Result *res) {
     __shared__ unsigned long long s_best[4];
     const uint32_t n = *ct.n_used;
+    if (blockIdx.x == 0 && threadIdx.x == 0)   // (rides along with the Result's copy to the host)
+        res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n;
     unsigned long long best = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t n_ab = ct.dcounts[i];
