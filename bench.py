@@ -29,11 +29,23 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ALG_BYTES_PER_PAIR_SCAN = 4    # K1 reads each int32 token once
 
 
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
-    """The C restatement (oracle/, single thread) on a bounded sample of the same workload."""
+    """The multi-threaded CPU restatement (oracle/bpe_cpu_mt.cc: the same full recount per merge
+    as the reference and the GPU engine, pinned to the reference's fixtures) on a bounded sample
+    of the same workload, on all the host cores this process may use, then on one thread."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    from oracle import OracleState
+    from oracle import CpuMT
     pkg = importlib.import_module('bpe-tokenizer_amd')
     n = sample_mib << 20
     data = (pkg.synth_zipf(n, seed=12345) if corpus == 'zipf' else
@@ -43,24 +55,36 @@ def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
     for k, u in enumerate(uniq[np.argsort(idx)]):
         lut[u] = k
     nt = int((lut >= 0).sum())
-    st = OracleState(lut[data], np.arange(0, n + 1, 1 << 20, dtype=np.int64), [1] * nt, nt,
-                     extra=4096)
+    ids = lut[data]
     del data
-    scans = 0
-    iters = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or iters < 2:
-        live = int(st.off[-1])
-        m = st.find_next_merge(None, 2)
-        if m is None:
-            break
-        st.apply_merge(m[0], m[1])
-        scans += live
-        iters += 1
-    dt = time.perf_counter() - t0
-    return {'value': scans / dt, 'unit': 'pair-scans/s', 'cores': 1, 'kind': 'port',
-            'sample': '%d MiB of the same corpus stream (1 MiB samples), first %d merge '
-                      'iterations, oracle/bpe_oracle.c single-threaded, %.1f s' % (sample_mib, iters, dt)}
+    off = np.arange(0, n + 1, 1 << 20, dtype=np.int64)
+    threads = int(os.environ.get('OMP_NUM_THREADS') or 0) or len(os.sched_getaffinity(0))
+
+    def timed(T, budget):
+        st = CpuMT(ids, off, [1] * nt, nt, threads=T, extra=1 << 14)
+        scans = iters = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget or iters < 2:
+            m = st.merge_until(0, 2, 1)
+            if not m:
+                break
+            scans += st.last_scans
+            iters += 1
+        dt = time.perf_counter() - t0
+        used = st.threads
+        st.close()
+        return scans / dt, iters, dt, used
+
+    v_mt, it_mt, dt_mt, used = timed(threads, budget_s * 0.6)
+    v_1, it_1, dt_1, _ = timed(1, budget_s * 0.4)
+    return {'value': v_mt, 'unit': 'pair-scans/s', 'cores': used, 'kind': 'port',
+            'value_1_thread': v_1,
+            'host': {'cpu_model': cpu_model(), 'nproc': os.cpu_count(),
+                     'affinity': len(os.sched_getaffinity(0))},
+            'sample': '%d MiB of the same corpus stream (1 MiB samples), mergeUntil from the first '
+                      'merge: %d merges in %.1f s on %d threads, %d merges in %.1f s on 1 thread; '
+                      'oracle/bpe_cpu_mt.cc (full recount per merge, as the reference)'
+                      % (sample_mib, it_mt, dt_mt, used, it_1, dt_1)}
 
 
 def main():
@@ -72,8 +96,8 @@ def main():
     ap.add_argument('--alphabet', type=int, default=256)
     ap.add_argument('--corpus', choices=['uniform', 'zipf'], default='uniform',
                     help='uniform: the C3 byte stream; zipf: the skewed variant (Zipf 1.1 words)')
-    ap.add_argument('--cpu-sample-mib', type=int, default=64)
-    ap.add_argument('--cpu-budget-s', type=float, default=15.0)
+    ap.add_argument('--cpu-sample-mib', type=int, default=256)
+    ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 

@@ -51,7 +51,9 @@ class Stats(ctypes.Structure):
         ('select_ms', ctypes.c_double), ('tie_passes', ctypes.c_int64),
         ('iterations', ctypes.c_int64), ('live_tokens', ctypes.c_int64),
         ('compactions', ctypes.c_int64), ('exact_passes', ctypes.c_int64),
-        ('step_timed', ctypes.c_int64),
+        ('step_timed', ctypes.c_int64), ('tie_tail', ctypes.c_int64),
+        ('tie_lone', ctypes.c_int64), ('loop_host', ctypes.c_int64),
+        ('fused_passes', ctypes.c_int64),
     ]
 
     def as_dict(self):

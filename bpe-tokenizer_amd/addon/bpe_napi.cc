@@ -5,6 +5,7 @@
 #include <node_api.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -229,6 +230,77 @@ napi_value ApplyMerges(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// mergeUntil(h, maxLength, minWeight, maxIterations) -> Float64Array of (a, b, W) triples
+// (bpe_merge_until: the device-resident loop, core.ts:365-383; new ids follow bpe_num_tokens)
+napi_value MergeUntil(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv))
+        return throw_arg(env, "mergeUntil(h, maxLength, minWeight, maxIterations)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    int32_t nt = 0;
+    if (bpe_num_tokens(ctx, &nt) < 0) return throw_native(env, "bpe_num_tokens");
+    const int64_t max_it = get_i64(env, argv[3]);
+    // every merge adds a token below the vocabulary limit (bpe.h BPE_MAX_VOCAB)
+    int64_t cap = BPE_MAX_VOCAB - (int64_t)nt;
+    if (max_it > 0 && max_it < cap) cap = max_it;
+    if (cap < 1) cap = 1;
+    std::vector<int64_t> abw(3 * cap);
+    int64_t n = 0;
+    if (bpe_merge_until(ctx, get_i64(env, argv[1]), get_i64(env, argv[2]), max_it, abw.data(), cap,
+                        &n) < 0)
+        return throw_native(env, "bpe_merge_until");
+    if (n > cap) n = cap;
+    void *data = nullptr;
+    napi_value ab, out;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(1, 3 * n) * 8, &data, &ab);
+    double *d = static_cast<double *>(data);
+    for (int64_t i = 0; i < 3 * n; ++i) d[i] = (double)abw[i];
+    napi_create_typedarray(env, napi_float64_array, (size_t)(3 * n), ab, 0, &out);
+    return out;
+}
+
+// encodeMerges(Int32Array ids, Int32Array abc) -> Int32Array: one text through a run of merges
+// (a, b, c) on a scratch engine (bpe_apply_merges: encodeToCode's replay, core.ts:392-409)
+napi_value EncodeMerges(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_arg(env, "encodeMerges(Int32Array, Int32Array)");
+    napi_typedarray_type t1, t2;
+    size_t n1 = 0, n2 = 0, o1 = 0, o2 = 0;
+    void *ids = nullptr, *abc = nullptr;
+    napi_value ab1, ab2;
+    if (napi_get_typedarray_info(env, argv[0], &t1, &n1, &ids, &ab1, &o1) != napi_ok ||
+        t1 != napi_int32_array ||
+        napi_get_typedarray_info(env, argv[1], &t2, &n2, &abc, &ab2, &o2) != napi_ok ||
+        t2 != napi_int32_array || n2 % 3 != 0)
+        return throw_arg(env, "encodeMerges expects Int32Array ids and (a, b, c) triples");
+    const int32_t *m = static_cast<const int32_t *>(abc);
+    int32_t vocab = 0;
+    for (size_t i = 0; i < n1; ++i) vocab = std::max(vocab, static_cast<const int32_t *>(ids)[i] + 1);
+    for (size_t i = 0; i < n2; ++i) vocab = std::max(vocab, m[i] + 1);
+    bpe_ctx *ctx = nullptr;
+    if (bpe_create(&ctx, 0) != BPE_OK) return throw_native(env, "bpe_create");
+    struct Guard {
+        bpe_ctx *c;
+        ~Guard() { bpe_destroy(c); }
+    } guard{ctx};
+    // lengths only matter to the max_length filter of a find, which never runs here
+    for (int32_t i = 0; i < vocab; ++i)
+        if (bpe_set_token_len16(ctx, i, 1) < 0) return throw_native(env, "bpe_set_token_len16");
+    if (bpe_add_sample(ctx, static_cast<const int32_t *>(ids), (int64_t)n1) < 0 ||
+        bpe_apply_merges(ctx, m, (int64_t)(n2 / 3), nullptr, 0) < 0)
+        return throw_native(env, "bpe_apply_merges");
+    int64_t ns = 0, nt = 0;
+    if (bpe_corpus_size(ctx, &ns, &nt) < 0) return throw_native(env, "bpe_corpus_size");
+    void *out_data = nullptr;
+    napi_value out_ab, out;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(nt, 1) * 4, &out_data, &out_ab);
+    int64_t off[2];
+    if (bpe_read_corpus(ctx, static_cast<int32_t *>(out_data), std::max<int64_t>(nt, 1), off, 2) < 0)
+        return throw_native(env, "bpe_read_corpus");
+    napi_create_typedarray(env, napi_int32_array, (size_t)nt, out_ab, 0, &out);
+    return out;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     struct {
         const char *name;
@@ -239,7 +311,8 @@ napi_value Init(napi_env env, napi_value exports) {
         {"addLatin1", AddLatin1}, {"clearCorpus", ClearCorpus},
         {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},
         {"findNextMerge", FindNextMerge}, {"applyMerge", ApplyMerge},
-        {"applyMerges", ApplyMerges},
+        {"applyMerges", ApplyMerges}, {"mergeUntil", MergeUntil},
+        {"encodeMerges", EncodeMerges},
     };
     for (auto &f : fns) {
         napi_value fn;

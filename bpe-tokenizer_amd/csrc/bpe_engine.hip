@@ -99,6 +99,11 @@ struct bpe_ctx {
     int64_t pend_expect = -1;    // W the replacement count must equal (mergeUntil), -1 = any
     int2 *h_cand = nullptr;      // pinned: first MAX_CAND candidates come back with the Result
     bool counts_valid = false;   // d_hot + cold table describe the current corpus
+    // d_hot's sketch half is an upper bound of the cold pairs' counts.  A MODE_FUSED pass leaves
+    // it garbage (its LDS half holds the refresh hash there): every reader of the sketch recounts
+    // first (table_ok)
+    bool sketch_valid = false;
+    uint64_t cold_used = 0;      // n_used of the cold table last reported to the host
     // The cold table holds the exact count of EVERY cold pair and is kept so merge by merge
     // (cold_refresh) instead of being rebuilt by exact passes: entered after consecutive exact
     // passes (a corpus whose winners are pairs of merged tokens, e.g. Zipf words)
@@ -237,8 +242,9 @@ static_assert(COLD_GRID * 256 >= HOT_BINS, "k_collect covers the hot bins");
 // Empties the cold table: free slots, zero dense counts (the invariant past n_used), n_used = 0.
 int cold_clear(bpe_ctx *c) {
     HIP_TRY(hipMemsetAsync(c->cold.slots, 0xFF, c->cold_cap * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(c->cold.dcounts, 0, c->cold_cap * sizeof(uint32_t), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->cold.dcounts, 0, c->cold_cap * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, 2 * sizeof(uint32_t), c->stream));
+    c->cold_used = 0;
     return BPE_OK;
 }
 
@@ -410,8 +416,13 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     }
     c->counts_valid = true;
     c->carry_valid = true;
+    c->sketch_valid = !(merge && fused);
+    if (merge && fused && c->stats_on) c->stats.fused_passes += 1;
     return BPE_OK;
 }
+
+// d_hot holds this corpus's counts with a usable sketch (the hot bins and the sketch bound)
+bool table_ok(const bpe_ctx *c) { return c->counts_valid && c->sketch_valid; }
 
 // Host accounting of an applied merge once its replacement count R is known.
 int settle_with(bpe_ctx *c, unsigned long long Ru) {
@@ -458,9 +469,10 @@ int compact(bpe_ctx *c) {
     if ((int64_t)total != c->live_slots)
         return fail(BPE_ERR_STATE, "bpe native: compaction lost slots");
     std::swap(c->d_ids, c->d_tmp);
-    const bool counts = c->counts_valid, cold_exact = c->cold_exact;
+    const bool counts = c->counts_valid, cold_exact = c->cold_exact, sketch = c->sketch_valid;
     if ((rc = seal_packed(c))) return rc;
     c->counts_valid = counts;
+    c->sketch_valid = sketch;
     c->cold_exact = cold_exact;
     if (c->stats_on) c->stats.compactions += 1;
     return BPE_OK;
@@ -498,9 +510,13 @@ int exact_pass(bpe_ctx *c) {
     HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    c->cold_used = flags[0];
     if (c->stats_on) c->stats.exact_passes += 1;
     return BPE_OK;
 }
+
+// select_from_table: the maintained cold table overflowed, select again after a recount
+constexpr int SELECT_RETRY = 100;
 
 // Best hot pair + heavy sketch buckets for `table` (a [TABLE_BINS] u64 table on the device);
 // then, when some bucket is heavy, the exact pass; then every pair sharing the best key.
@@ -532,7 +548,16 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
         HIP_TRY(hipStreamSynchronize(s));
         if ((rc = settle_with(c, c->h_res->replaced))) return rc;
         const uint64_t flags = c->h_res->cold_flags;
-        if (flags >> 32) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+        c->cold_used = flags & 0xFFFFFFFFu;
+        if (flags >> 32) {
+            // a refresh claimed more slots than the table has: this selection cannot be
+            // trusted.  Leave the maintained state; the caller recounts and selects again (plain
+            // pass, then exact passes that rebuild the table)
+            c->cold_exact = false;
+            c->counts_valid = false;
+            c->exact_streak = 1;
+            return SELECT_RETRY;
+        }
         if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3) {
             // too full to probe well: this selection still reads it, the next one rebuilds it
             c->cold_exact = false;
@@ -640,12 +665,18 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
         if ((rc = settle(c))) return rc;
         if (c->n_live < 2) return BPE_NO_MERGE;
     }
-    if (!c->counts_valid)
+    // (the maintained cold table does not read the sketch; every other selection does)
+    if (!(c->cold_exact ? c->counts_valid : table_ok(c)))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     c->opt_max_length = max_length;
     hipEvent_t e_sel = span_begin(c);
     std::vector<int2> cand;
-    if ((rc = select_from_table(c, c->d_hot, max_length, true, cand, e_sel))) return rc;
+    rc = select_from_table(c, c->d_hot, max_length, true, cand, e_sel);
+    if (rc == SELECT_RETRY) {
+        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+        rc = select_from_table(c, c->d_hot, max_length, true, cand, nullptr);
+    }
+    if (rc) return rc;
     if (c->stats_on) {
         c->stats.iterations += 1;
         c->stats.live_tokens += c->n_live;
@@ -701,8 +732,16 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
         const int64_t na = c->h_count[a], nb = c->h_count[b];
         const uint64_t bound = (uint64_t)std::max<int64_t>(0, a == b ? na / 2 : std::min(na, nb));
         if ((rc = ensure_cold(c, bound))) return rc;
-        fused = c->cold_exact && c->cold_cap == cap0 && !getenv("BPE_DEBUG_NO_FUSED");
-        if (!fused) c->cold_exact = false;
+        // the refresh claims at most 2 * bound new slots (holes included): it must fit the
+        // table's 3/4 fill limit, which counts every claim made since the last rebuild
+        const uint64_t V = c->h_len16.size() + 1;
+        const bool room = c->cold_used + std::min<uint64_t>(2 * bound, V * V) + 64 <=
+                          c->cold_cap / 4 * 3;
+        fused = c->cold_exact && c->cold_cap == cap0 && room && !getenv("BPE_DEBUG_NO_FUSED");
+        if (!fused) {
+            c->cold_exact = false;
+            c->exact_streak = 1;   // (the next exact pass rebuilds the whole table)
+        }
     }
     if (fused) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
     if ((rc = run_pass(c, true, a, b, cc, replaced, fused))) return rc;
@@ -723,7 +762,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     c->cold_exact = false;   // (its merges do not refresh a maintained cold table)
     if ((rc = settle(c))) return rc;
     c->opt_max_length = max_length;
-    if (!c->counts_valid || !c->carry_valid)
+    if (!table_ok(c) || !c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     const int64_t base = (int64_t)c->h_len16.size();
     if ((rc = ensure_len16_cap(c, base + n))) return rc;
@@ -749,6 +788,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     h->next_id = (int32_t)base;
     h->w = -1;
     h->min_weight = min_weight;
+    h->max_id = BPE_MAX_VOCAB;
     HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
     TieArgs A;
     memset(&A, 0, sizeof A);
@@ -828,12 +868,17 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         out_abw[3 * i + 2] = W;
     }
     c->len16_lo = base + nd;   // k_decide wrote the new lengths on the device
-    if (c->stats_on) c->stats.tie_passes += h->n_tie;
+    if (c->stats_on) {
+        c->stats.tie_passes += h->n_tie;
+        c->stats.tie_tail += h->n_tail;
+        c->stats.tie_lone += h->n_lone;
+        c->stats.loop_host += h->n_host;
+    }
     c->last_replaced = nd ? c->h_log[LOG_WORDS * (nd - 1) + 2] : c->last_replaced;
     // every early-ended batch leaves the last reduce's best key in the Result
     c->best_ready = true;
     c->best_ml = max_length;
-    c->counts_valid = c->carry_valid = true;
+    c->counts_valid = c->carry_valid = c->sketch_valid = true;
     *n_done = nd;
     *status = h->status;
     return BPE_OK;
@@ -850,7 +895,7 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
     if ((rc = settle(c))) return rc;
     if ((rc = maybe_compact(c))) return rc;
     c->opt_max_length = max_length;
-    if (!c->counts_valid || !c->carry_valid)
+    if (!table_ok(c) || !c->carry_valid)
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     const int64_t base = (int64_t)c->h_len16.size();
     if ((rc = ensure_len16_cap(c, base + LOOP_BATCH))) return rc;
@@ -870,6 +915,7 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
     h->w = -1;
     h->min_weight = min_weight == 0 ? 2 : min_weight;                   // core.ts:256
     h->sharded = 1;
+    h->max_id = BPE_MAX_VOCAB;
     HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
     // this shard's table, to be summed over the ranks
     HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
@@ -994,8 +1040,13 @@ int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, in
         }
     }
     c->len16_lo = base + nd;
-    if (c->stats_on) c->stats.tie_passes += h->n_tie;
-    c->counts_valid = c->carry_valid = true;   // d_hot: this shard's table after the last merge
+    if (c->stats_on) {
+        c->stats.tie_passes += h->n_tie;
+        c->stats.tie_tail += h->n_tail;
+        c->stats.tie_lone += h->n_lone;
+        c->stats.loop_host += h->n_host;
+    }
+    c->counts_valid = c->carry_valid = c->sketch_valid = true;   // d_hot: this shard's table
     c->best_ready = false;
     *n_done = nd;
     *status = h->status;
@@ -1516,7 +1567,7 @@ int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
     int rc = set_device(c);
     if (rc) return rc;
     if ((rc = settle(c))) return rc;
-    if (!c->counts_valid)
+    if (!table_ok(c))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(uint64_t), hipMemcpyDeviceToDevice,
                            c->stream));

@@ -90,9 +90,11 @@ struct ColdTable {
     // the dense arrays, entry i = the i-th claimed index (claim order): every scan (argmax,
     // collect, invalidate, export) streams these coalesced, and the counts live here, so a scan
     // never gathers hashed slots.  A claim that loses its slot race leaves a hole (key EMPTY,
-    // count 0).  dcounts[i] == 0 for every i >= *n_used (zeroed with the table).
+    // count 0).  dcounts[i] == 0 for every i >= *n_used (zeroed with the table).  Counts are
+    // 64-bit: one pair of a 16 GiB shard can occur more than 2^32 times (JS numbers in the
+    // reference's Map are exact to 2^53, core.ts:280-292).
     uint32_t *dkeys;
-    uint32_t *dcounts;
+    unsigned long long *dcounts;
     uint32_t *n_used;
     uint32_t *overflow;  // set when a probe sequence wraps the table or the dense arrays fill up
     uint32_t mask;       // slots - 1 (= dense capacity - 1)
@@ -125,6 +127,10 @@ struct LoopCtl {
     // one rank of a sharded corpus: W is global (this shard's replacement count is logged, not
     // checked), ties take the full pass and their positions come from the all-reduced tie table
     int32_t sharded;
+    int32_t max_id;       // ids below it fit the vocabulary (BPE_MAX_VOCAB): at it the batch ends
+    int32_t n_tail;       // ties decided from the tail window alone (k_tie tail mode)
+    int32_t n_lone;       // ... of which by the lone candidate missing from the window
+    int32_t n_host;       // iterations handed to the host path (LOOP_HOST: 0 or 1 per batch)
 };
 
 // Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
@@ -182,7 +188,7 @@ __device__ __forceinline__ uint32_t pack_pair_s(int32_t x, int32_t y) {
 
 constexpr unsigned long long EMPTY64 = ~0ull;
 
-__device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, uint32_t inc) {
+__device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, unsigned long long inc) {
     uint32_t h = (key * 0x9E3779B1u) >> ct.shift;
     uint32_t mine = EMPTY;   // the dense index this call reserved (at its first free slot)
     for (uint32_t probes = 0; probes <= ct.mask; ++probes) {
@@ -272,7 +278,7 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
     if (n == 0 || MODE == MODE_NONE) return;
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) atomicAdd(&k.spill[table_index(x, y)], n);
     if (MODE != MODE_TABLE && exact_wanted<MODE>(k, x, y))
-        cold_add(k.ct, pair_key(x, y), (uint32_t)n);
+        cold_add(k.ct, pair_key(x, y), n);
 }
 
 // The LDS table: 16-bit counters, two per dword.
@@ -1426,8 +1432,8 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
         res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n;
     unsigned long long best = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t n_ab = ct.dcounts[i];
-        if (!n_ab || n_ab < (uint32_t)(best >> 17)) continue;   // (the key only when it can win)
+        const unsigned long long n_ab = ct.dcounts[i];
+        if (!n_ab || n_ab < (best >> 17)) continue;   // (the key only when it can win)
         const uint32_t key = ct.dkeys[i];
         const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
         if (!pair_ok(a, b, len16, max_length)) continue;
@@ -1547,12 +1553,20 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
             log[LOG_WORDS * (ctl->n_done - 1) + 3] = (long long)res->replaced;
         }
         ctl->w = -1;
+        // a heavy sketch bucket may hold a cold pair above the best hot one (even when no hot
+        // pair exists at all): only the host path's exact counts can tell
+        if (res->n_heavy) {
+            ctl->status = LOOP_HOST;
+            ctl->n_host += 1;
+            return;
+        }
         if (best == 0 || W < ctl->min_weight) {                   // core.ts:312-313
             ctl->status = LOOP_DONE;
             return;
         }
-        if (res->n_heavy || n == 0 || n > (unsigned)MAX_CAND) {
+        if (n == 0 || n > (unsigned)MAX_CAND || ctl->next_id >= ctl->max_id) {
             ctl->status = LOOP_HOST;
+            ctl->n_host += 1;
             return;
         }
         if (n > 1) {
@@ -1591,6 +1605,7 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
             if (missing > 1) {
                 // two or more occur only before the tail window: the host path's full pass
                 ctl->status = LOOP_HOST;
+                ctl->n_host += 1;
                 return;
             }
             // the only one missing occurs only earlier: its last occurrence is the earliest
@@ -1599,7 +1614,9 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
                     a = cand[j].x;
                     b = cand[j].y;
                 }
+            ctl->n_lone += 1;
         }
+        if (ctl->tie == 1) ctl->n_tail += 1;
         if (a < 0) {
             ctl->status = LOOP_ERROR;
             return;
@@ -1642,7 +1659,8 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
         if (pair_ok(a, b, len16, max_length) && pack_key(hot_counts[tid], a, b) == best)
             push_cand(res, cand, a, b);
     }
-    const uint32_t n = *ct.n_used, w = (uint32_t)(best >> 17);
+    const uint32_t n = *ct.n_used;
+    const unsigned long long w = best >> 17;
     for (uint32_t i = tid; i < n; i += gridDim.x * blockDim.x) {
         if (ct.dcounts[i] != w) continue;   // (dense view; the key only for count matches)
         const uint32_t key = ct.dkeys[i];

@@ -61,6 +61,10 @@ function replaceAll(s, from, to) {
   return s.split(from).join(to)
 }
 
+/** Texts at least this long, with at least this many merges, are encoded on the GPU. */
+const ENCODE_ON_DEVICE_CHARS = 1 << 16
+const ENCODE_ON_DEVICE_MERGES = 16
+
 /** JS `x || fallback` for numeric options, mapped onto the C ABI's int64 conventions. */
 function maxLengthArg(max_length) {
   // core.ts:255,272: falsy -> unlimited; otherwise `len <= max_length`
@@ -344,27 +348,86 @@ class BPETokenizer {
 
   /**
    * @description call `findNextMerge()` and `applyMerge()` in loop (core.ts:365-383).
+   * The loop runs on the device (bpe_merge_until: the merge decisions stay in HBM, one host round
+   * trip per batch of iterations); the merges it made are then entered into the tables exactly as
+   * findNextMerge + applyMerge would have, in order.
    */
   mergeUntil(options) {
     let max_iterations = options && options.max_iterations
-    for (let iteration = 1; !max_iterations || iteration <= max_iterations; iteration++) {
-      let merge = this.findNextMerge(options)
-      if (!merge) break
-      this.applyMerge(merge)
+    // core.ts:376: `!max_iterations || iteration <= max_iterations`
+    let it_arg = 0
+    if (max_iterations && max_iterations !== Infinity) {
+      if (!(max_iterations >= 1)) return
+      it_arg = Math.floor(max_iterations)
     }
+    if (!this._engine) return // an empty corpus: findNextMerge returns null (core.ts:312)
+    let engine = this.engine()
+    let max_length = options && options.max_length
+    let abw = loadNative().mergeUntil(engine, maxLengthArg(max_length), minWeightArg(options), it_arg)
+    let { code_to_token, token_table, merge_tokens, merge_codes } = this
+    for (let i = 0; i < abw.length; i += 3) {
+      let a = token_table[abw[i]]
+      let b = token_table[abw[i + 1]]
+      let weight = abw[i + 2]
+      let index = token_table.length
+      let c = {
+        chars: a.chars + b.chars,
+        weight: weight,
+        original_weight: weight,
+        code: String.fromCodePoint(index + 1),
+        index: index,
+      }
+      // applyMerge's bookkeeping (core.ts:345-354); the corpus is already rewritten
+      a.weight -= c.weight
+      b.weight -= c.weight
+      code_to_token[c.code] = c
+      token_table.push(c)
+      merge_tokens.push([a, b, c])
+      merge_codes.push([a.code + b.code, c.code])
+    }
+    if (abw.length) this.invalidateVectorIndex()
+    // the engine registered the UTF-16 length of every token it created (core.ts:318)
+    this._registered = token_table.length
   }
 
-  /** @description encode to binary string (core.ts:392-409). */
+  /**
+   * @description encode to binary string (core.ts:392-409).
+   * A long text with many merges is encoded on the GPU: the merges are replayed in order by
+   * apply-only passes over the text in HBM (bpe_apply_merges), one per merge, in place of one
+   * `replaceAll` per merge over a JS string.
+   */
   encodeToCode(content) {
     let { char_to_token } = this
 
     let content_in_code = ''
+    let ids = null
+    let long = content.length >= ENCODE_ON_DEVICE_CHARS && this.merge_tokens.length >= ENCODE_ON_DEVICE_MERGES
+    if (long) ids = []
     for (let char of content) {
       let token = char_to_token[char]
       if (!token) {
         throw new Error('unknown token, char: ' + JSON.stringify(char))
       }
-      content_in_code += token.code
+      if (long) ids.push(token.index)
+      else content_in_code += token.code
+    }
+
+    if (long) {
+      let abc = new Int32Array(3 * this.merge_tokens.length)
+      this.merge_tokens.forEach(([a, b, c], i) => {
+        abc[3 * i] = a.index
+        abc[3 * i + 1] = b.index
+        abc[3 * i + 2] = c.index
+      })
+      let out = loadNative().encodeMerges(Int32Array.from(ids), abc)
+      let parts = []
+      for (let i = 0; i < out.length; i += 8192) {
+        let part = []
+        let end = Math.min(out.length, i + 8192)
+        for (let j = i; j < end; j++) part.push(out[j] + 1)
+        parts.push(String.fromCodePoint.apply(null, part))
+      }
+      return parts.join('')
     }
 
     for (let [from_code, to_code] of this.merge_codes) {

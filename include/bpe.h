@@ -194,6 +194,12 @@ typedef struct {
     int64_t step_timed;       /* streaming passes whose duration step_ms sums (the device loop times
                                  every SPAN_EVERY-th iteration, all of its spans; select_ms covers
                                  those same iterations) */
+    int64_t tie_tail;         /* device loop: R3 ties decided from the corpus-tail window alone */
+    int64_t tie_lone;         /* ... of which the lone candidate missing from the window won */
+    int64_t loop_host;        /* device loop: iterations handed to the host path (heavy sketch
+                                 buckets, > BPE_MAX_CAND tied pairs, >= 2 tied pairs missing from
+                                 the tail window, the vocabulary limit) */
+    int64_t fused_passes;     /* merge passes that also refreshed the maintained cold-pair table */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

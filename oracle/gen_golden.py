@@ -92,7 +92,49 @@ function xorshiftCorpus(seed, A, base, nbytes) {
   }
   return codes
 }
-if (input.kind === 'cases') {
+// config-3 scale: the corpus is generated sample by sample (a 2^30-element JS array does not fit
+// V8's array limits), each sample flattened once added (the cons-string rope of core.ts:204
+// otherwise exhausts the heap); only the first merges run (each is a ~2 minute scan)
+function prefixRun(input) {
+  let { seed, A, base, total, sample, max_iterations, min_weight } = input
+  let x = seed >>> 0, t = new BPETokenizer(), t0 = Date.now()
+  for (let off = 0; off < total; off += sample) {
+    let n = Math.min(total, off + sample) - off, s = '', part = new Array(8192)
+    for (let i = 0; i < n; i += 8192) {
+      let k = Math.min(8192, n - i)
+      for (let j = 0; j < k; j++) {
+        x ^= x << 13; x >>>= 0; x ^= x >>> 17; x ^= x << 5; x >>>= 0
+        part[j] = base + Math.floor(x * A / 4294967296)
+      }
+      s += String.fromCharCode.apply(null, k === 8192 ? part : part.slice(0, k))
+    }
+    t.addToCorpus(s)
+    t.corpus_in_code[t.corpus_in_code.length - 1].charCodeAt(0)
+    if ((off / sample) % 64 == 0) console.error('sample', off / sample, (Date.now() - t0) / 1000, 's')
+  }
+  let ingest_s = (Date.now() - t0) / 1000, merges = [], merge_s = []
+  for (let it = 1; it <= max_iterations; it++) {
+    let t1 = Date.now()
+    let m = t.findNextMerge({ min_weight })
+    if (!m) break
+    merges.push([m[0].index, m[1].index, m[2].original_weight])
+    t.applyMerge(m)
+    merge_s.push((Date.now() - t1) / 1000)
+    console.error('merge', it, merges[merges.length - 1], merge_s[merge_s.length - 1], 's')
+  }
+  let corpus = t.corpus_in_code, live = 0
+  for (let s of corpus) for (let ch of s) live++
+  let sha = s => crypto.createHash('sha256').update(Buffer.from(new Int32Array(ids(s)).buffer)).digest('hex')
+  return {
+    seed, A, base, total, sample, max_iterations, min_weight, merges,
+    char_count: Object.keys(t.char_to_token).length, live_tokens_after: live,
+    first_sample_sha256: sha(corpus[0]), last_sample_sha256: sha(corpus[corpus.length - 1]),
+    ingest_seconds: ingest_s, merge_seconds: merge_s,
+  }
+}
+if (input.kind === 'prefix') {
+  fs.writeFileSync(process.argv[3], JSON.stringify(prefixRun(input)))
+} else if (input.kind === 'cases') {
   fs.writeFileSync(process.argv[3], JSON.stringify(input.cases.map(runCase)))
 } else if (input.kind === 'synthetic') {
   let { seed, A, base, total, sample, max_iterations, min_weight } = input
@@ -134,14 +176,15 @@ if (input.kind === 'cases') {
 """
 
 
-def run_node(payload, name):
+def run_node(payload, name, heap_mb=16000):
     inp = os.path.join(WORK, name + '.in.json')
     out = os.path.join(WORK, name + '.out.json')
     with open(inp, 'w') as f:
         json.dump(payload, f)
     with open(os.path.join(WORK, 'harness.js'), 'w') as f:
         f.write(HARNESS)
-    subprocess.check_call(['node', '--max-old-space-size=16000', 'harness.js', inp, out], cwd=WORK)
+    subprocess.check_call(['node', '--max-old-space-size=%d' % heap_mb, 'harness.js', inp, out],
+                          cwd=WORK)
     with open(out) as f:
         return json.load(f)
 
@@ -220,15 +263,30 @@ def gen_config2():
     print('wrote', path, len(out['merges']), 'merges in', out['node_seconds'], 's')
 
 
+def gen_config3_prefix():
+    """BASELINE config 3 (1 GiB, 256-char alphabet, 1 MiB samples): the reference's first merges
+    (SURVEY.md §8(c) golden item 5), with the live token count after them and the SHA-256 of the
+    first and last samples' ids."""
+    out = run_node({'kind': 'prefix', 'seed': 12345, 'A': 256, 'base': 0, 'total': 1 << 30,
+                    'sample': 1 << 20, 'max_iterations': 3, 'min_weight': 2}, 'config3', 55000)
+    path = os.path.join(GOLDEN, 'config3_prefix.json')
+    with open(path, 'w') as f:
+        json.dump(out, f, separators=(',', ':'))
+    print('wrote', path, out['merges'], 'ingest', out['ingest_seconds'], 's')
+
+
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--small', action='store_true')
     ap.add_argument('--config2', action='store_true')
+    ap.add_argument('--config3-prefix', action='store_true')
     args = ap.parse_args()
     if not os.path.exists(REF):
         sys.exit('reference not present: fixtures can only be (re)generated in the build container')
     erase_reference()
-    if args.small or not args.config2:
+    if args.small or not (args.config2 or args.config3_prefix):
         gen_small()
     if args.config2:
         gen_config2()
+    if args.config3_prefix:
+        gen_config3_prefix()

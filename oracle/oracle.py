@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'liboracle.so')
+LIB_PATH = os.environ.get('ORACLE_LIB') or os.path.join(HERE, 'liboracle.so')
 _lib = None
 
 
@@ -170,3 +170,108 @@ def xorshift_corpus(seed, A, base, n):
     out = np.empty(n, dtype=np.uint8)
     lib().oracle_xorshift_corpus(seed, A, base, out.ctypes.data, n)
     return out
+
+
+# ---- the multi-threaded restatement (oracle/bpe_cpu_mt.cc): larger parity cases + CPU baseline --
+LIB_MT_PATH = os.environ.get('ORACLE_MT_LIB') or os.path.join(HERE, 'liboracle_mt.so')
+_lib_mt = None
+
+
+def lib_mt():
+    global _lib_mt
+    if _lib_mt is None:
+        if not os.path.exists(LIB_MT_PATH):
+            build()
+        L = ctypes.CDLL(LIB_MT_PATH)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        vp = ctypes.c_void_p
+        L.cpu_create.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int32, ctypes.c_int64,
+                                 ctypes.c_int]
+        L.cpu_create.restype = vp
+        L.cpu_destroy.argtypes = [vp]
+        L.cpu_destroy.restype = None
+        L.cpu_live.argtypes = [vp]
+        L.cpu_live.restype = ctypes.c_int64
+        L.cpu_threads.argtypes = [vp]
+        L.cpu_threads.restype = ctypes.c_int
+        L.cpu_find_next_merge.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p]
+        L.cpu_find_next_merge.restype = ctypes.c_int
+        L.cpu_apply_merge.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+        L.cpu_apply_merge.restype = ctypes.c_int64
+        L.cpu_merge_until.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, i64p,
+                                      ctypes.c_int64, i64p]
+        L.cpu_merge_until.restype = ctypes.c_int64
+        L.cpu_read.argtypes = [vp, i32p, i64p]
+        L.cpu_read.restype = None
+        _lib_mt = L
+    return _lib_mt
+
+
+class CpuMT:
+    """The corpus held by the multi-threaded restatement (threads <= 0: all host cores)."""
+
+    def __init__(self, ids, off, len16, n_tokens, threads=0, extra=1 << 16):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        if ids.size == 0:
+            ids = np.zeros(1, np.int32)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        l16 = np.ascontiguousarray(np.asarray(len16, dtype=np.int32)[:n_tokens])
+        if l16.size == 0:
+            l16 = np.zeros(1, np.int32)
+        self.n_samples = len(off) - 1
+        self.n_tokens = n_tokens
+        self._h = lib_mt().cpu_create(_p(ids, ctypes.c_int32), _p(off, ctypes.c_int64),
+                                      self.n_samples, _p(l16, ctypes.c_int32), n_tokens, extra,
+                                      threads)
+
+    def close(self):
+        if self._h:
+            lib_mt().cpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def threads(self):
+        return lib_mt().cpu_threads(self._h)
+
+    def live(self):
+        return lib_mt().cpu_live(self._h)
+
+    def find_next_merge(self, max_length=None, min_weight=None):
+        a, b, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        rc = lib_mt().cpu_find_next_merge(self._h, js_truthy_int(max_length),
+                                          js_truthy_int(min_weight), ctypes.byref(a),
+                                          ctypes.byref(b), ctypes.byref(w))
+        return None if rc else (a.value, b.value, w.value)
+
+    def apply_merge(self, a, b, c=None):
+        if c is None:
+            c = self.n_tokens
+        self.n_tokens = max(self.n_tokens, c + 1)
+        return lib_mt().cpu_apply_merge(self._h, a, b, c)
+
+    def merge_until(self, max_length=None, min_weight=None, max_iterations=None, cap=1 << 16):
+        out = np.zeros(3 * cap, np.int64)
+        scans = ctypes.c_int64()
+        n = lib_mt().cpu_merge_until(self._h, js_truthy_int(max_length), js_truthy_int(min_weight),
+                                     js_truthy_int(max_iterations), _p(out, ctypes.c_int64), cap,
+                                     ctypes.byref(scans))
+        self.n_tokens += n
+        self.last_scans = scans.value
+        return [tuple(int(v) for v in out[3 * i:3 * i + 3]) for i in range(min(n, cap))]
+
+    def read(self):
+        ids = np.zeros(max(1, self.live()), np.int32)
+        off = np.zeros(self.n_samples + 1, np.int64)
+        lib_mt().cpu_read(self._h, _p(ids, ctypes.c_int32), _p(off, ctypes.c_int64))
+        return ids[:self.live()], off
+
+    def samples(self):
+        ids, off = self.read()
+        return [ids[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]

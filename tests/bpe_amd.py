@@ -8,14 +8,33 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 pkg = importlib.import_module('bpe-tokenizer_amd')
 
+# The two ways the engine runs the reference's merge loop (core.ts:365-383):
+#   'host' — findNextMerge / applyMerge one call each (bpe_find_next_merge + bpe_apply_merge:
+#            the host-driven selection with the full-pass R3 tie kernel);
+#   'loop' — mergeUntil (bpe_merge_until: the device-resident loop that the bench times, with
+#            k_select_multi / k_decide / the tail-window tie pass, handing iterations it cannot
+#            finish to the host path).
+MODES = ['host', 'loop']
 
-def run_engine(samples_ids, len16, opts, device=0):
-    """Drives the HIP engine exactly like the reference's merge loop (core.ts:374-381)."""
+
+def make_engine(samples_ids, len16, device=0):
     e = pkg.Engine(device)
     for i, l in enumerate(len16):
         e.set_token_len16(i, l)
     for s in samples_ids:
         e.add_sample(s)
+    return e
+
+
+def run_engine(samples_ids, len16, opts, device=0, mode='host', stats=False):
+    """Drives the HIP engine like the reference's merge loop (core.ts:374-381), in `mode`."""
+    e = make_engine(samples_ids, len16, device)
+    if stats:
+        e.stats_enable(True)
+    if mode == 'loop':
+        merges = e.merge_until(opts.get('max_length') or 0, opts.get('min_weight') or 0,
+                               opts.get('max_iterations') or 0)
+        return e, merges
     merges = []
     it = 1
     max_it = opts.get('max_iterations')

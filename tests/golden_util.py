@@ -59,3 +59,12 @@ def char_weights(samples_ids, n_chars):
         if len(s):
             w += np.bincount(np.asarray(s), minlength=n_chars)[:n_chars]
     return w.tolist()
+
+
+def load_config3_prefix():
+    """The reference's first merges on BASELINE config 3 (oracle/gen_golden.py --config3-prefix)."""
+    p = os.path.join(GOLDEN, 'config3_prefix.json')
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)

@@ -141,6 +141,60 @@ it('restoreToCorpus after fromJSON continues merging', () => {
   assert.deepStrictEqual(table(u), table(t))
 })
 
+it('mergeUntil on the device loop == findNextMerge + applyMerge one by one (core.ts:365-383)', () => {
+  let seed = 7
+  const rnd = () => { seed ^= seed << 13; seed >>>= 0; seed ^= seed >>> 17; seed ^= seed << 5; seed >>>= 0; return seed }
+  const alpha = 'abcdefghij klmnop'
+  const samples = []
+  for (let s = 0; s < 12; s++) {
+    let str = ''
+    const n = 2000 + (rnd() % 20000)
+    for (let i = 0; i < n; i++) str += (rnd() % 7 === 0 ? 'xx' : alpha[rnd() % alpha.length])
+    samples.push(str)
+  }
+  for (const opts of [{ max_iterations: 150 }, { max_iterations: 90, max_length: 3 }, { max_iterations: 2.5, min_weight: 3 }]) {
+    const t = new BPETokenizer(), u = new BPETokenizer()
+    for (const s of samples) { t.addToCorpus(s); u.addToCorpus(s) }
+    t.mergeUntil(opts)
+    for (let it = 1; !opts.max_iterations || it <= opts.max_iterations; it++) {
+      const m = u.findNextMerge(opts)
+      if (!m) break
+      u.applyMerge(m)
+    }
+    assert.deepStrictEqual(t.token_table, u.token_table)
+    assert.deepStrictEqual(t.merge_codes, u.merge_codes)
+    assert.deepStrictEqual(t.merge_tokens.map(m => m.map(x => x.index)), u.merge_tokens.map(m => m.map(x => x.index)))
+    assert.deepStrictEqual(t.corpus_in_code, u.corpus_in_code)
+    // and merging continues identically from both
+    t.mergeUntil({ max_iterations: 5 }); u.mergeUntil({ max_iterations: 5 })
+    assert.deepStrictEqual(t.token_table, u.token_table)
+  }
+  const e = new BPETokenizer()
+  e.mergeUntil({})                        // empty corpus: nothing to merge (core.ts:312)
+  e.addToCorpus('abab'); e.mergeUntil({ max_iterations: -1 })   // `iteration <= -1` never holds
+  assert.strictEqual(e.token_table.length, 2)
+})
+it('long texts are encoded on the device (encodeToCode, core.ts:392-409)', () => {
+  const t = new BPETokenizer()
+  const alpha = 'the quick brown fox jumps over a lazy dog'
+  let seed = 99, corpus = ''
+  const rnd = () => { seed ^= seed << 13; seed >>>= 0; seed ^= seed >>> 17; seed ^= seed << 5; seed >>>= 0; return seed }
+  for (let i = 0; i < 50000; i++) corpus += alpha[rnd() % alpha.length]
+  t.addToCorpus(corpus)
+  t.mergeUntil({ max_iterations: 200 })
+  assert(t.merge_tokens.length >= 100)
+  let text = ''
+  for (let i = 0; i < 200000; i++) text += alpha[rnd() % alpha.length]
+  // the reference's replay, on a JS string (core.ts:395-406)
+  let want = ''
+  for (const ch of text) want += t.char_to_token[ch].code
+  for (const [from_code, to_code] of t.merge_codes) want = want.split(from_code).join(to_code)
+  assert.strictEqual(t.encodeToCode(text), want)
+  const vec = t.encodeToVector(text)
+  assert.strictEqual(t.decodeVector(vec), text)
+  assert.throws(() => t.encodeToCode(text + '\u00e9'), e => e.message === 'unknown token, char: "\u00e9"')
+})
+
 // reference-generated golden cases through the whole JS surface
 const golden = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'small_cases.json')))
 let g = 0

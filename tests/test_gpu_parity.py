@@ -6,26 +6,28 @@ import random
 import numpy as np
 import pytest
 
-from bpe_amd import pkg, run_engine
-from golden_util import load_config2, load_small
-from oracle import Corpus, OracleState
+from bpe_amd import MODES, pkg, run_engine
+from golden_util import load_config2, load_config3_prefix, load_small
+from oracle import Corpus, CpuMT, OracleState
 
 pytestmark = pytest.mark.gpu
 
 
-def engine_case(case):
+def engine_case(case, mode='host'):
     c = Corpus()
     for s in case['samples']:
         c.add(s)
-    e, merges = run_engine(c.samples, c.len16, case['opts'])
+    e, merges = run_engine(c.samples, c.len16, case['opts'], mode=mode)
     return c, e, merges
 
 
-def test_small_golden_cases():
-    """All reference-generated small cases (spec inputs + 1500 seeded random corpora)."""
+@pytest.mark.parametrize('mode', MODES)
+def test_small_golden_cases(mode):
+    """All reference-generated small cases (spec inputs + 1500 seeded random corpora), through
+    findNextMerge/applyMerge and through mergeUntil's device-resident loop."""
     bad = []
     for case in load_small():
-        c, e, merges = engine_case(case)
+        c, e, merges = engine_case(case, mode)
         got = [list(m) for m in merges]
         if got != case['merges'] or e.samples() != case['final_ids']:
             bad.append((case['name'], got[:5], case['merges'][:5]))
@@ -35,11 +37,12 @@ def test_small_golden_cases():
     assert not bad, bad
 
 
-def test_config1_drop_in_numbers():
+@pytest.mark.parametrize('mode', MODES)
+def test_config1_drop_in_numbers(mode):
     """BASELINE config 1: 'aaabdaaabac', mergeUntil({min_weight:2})."""
     c = Corpus()
     c.add('aaabdaaabac')
-    e, merges = run_engine(c.samples, c.len16, {'min_weight': 2})
+    e, merges = run_engine(c.samples, c.len16, {'min_weight': 2}, mode=mode)
     assert merges == [(0, 0, 2), (0, 1, 2), (4, 5, 2)]
     assert e.samples() == [[6, 2, 6, 0, 3]]
 
@@ -61,8 +64,9 @@ def random_corpus(rng, n_tokens, alphabet, run_bias, n_samples):
     return out
 
 
+@pytest.mark.parametrize('mode', MODES)
 @pytest.mark.parametrize('seed', range(12))
-def test_random_vs_oracle(seed):
+def test_random_vs_oracle(seed, mode):
     rng = random.Random(seed)
     n_tokens = rng.choice([3000, 40000, 300000, 1500000])
     alphabet = rng.choice([2, 3, 5, 20, 95, 256, 300])
@@ -76,25 +80,46 @@ def test_random_vs_oracle(seed):
                      np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64),
                      len16, alphabet)
     want = st.merge_until(opts['max_length'], opts['min_weight'], opts['max_iterations'])
-    e, got = run_engine(samples, len16, opts)
+    e, got = run_engine(samples, len16, opts, mode=mode)
     assert got == want
     assert e.samples() == st.samples()
 
 
+@pytest.mark.parametrize('mode', MODES)
+@pytest.mark.parametrize('seed', range(3))
+def test_only_cold_pairs(seed, mode):
+    """A corpus of ids >= 256 only: no hot pair exists, so the best hot key is empty and every
+    candidate hides in the cold sketch.  The device loop must hand such iterations to the exact
+    counts instead of stopping (core.ts:312 returns null only when no pair exists at all)."""
+    rng = random.Random(300 + seed)
+    V = 256 + rng.choice([3, 20, 60])
+    samples = [np.array([rng.randrange(256, V) for _ in range(rng.randint(0, 4000))], np.int32)
+               for _ in range(rng.choice([1, 7]))]
+    len16 = [1] * V
+    ids, off = np.concatenate(samples), np.concatenate([[0], np.cumsum([len(s) for s in samples])])
+    st = OracleState(ids, off.astype(np.int64), len16, V)
+    want = st.merge_until(0, 2, 12)
+    e, got = run_engine(samples, len16, {'max_iterations': 12}, mode=mode)
+    assert got == want
+    assert e.samples() == st.samples()
+
+
+@pytest.mark.parametrize('mode', MODES)
 @pytest.mark.parametrize('n', [9, 10, 1023, 1024, 65536 * 3 + 7, 3_000_001])
-def test_long_runs_cross_chunks_and_regions(n):
+def test_long_runs_cross_chunks_and_regions(n, mode):
     """'x' * n (+ a breaker) — runs far longer than a chunk and than a region."""
     samples = [np.zeros(n, np.int32), np.array([0, 0, 1, 0, 0, 0], np.int32),
                np.concatenate([np.zeros(n // 3, np.int32), [1], np.zeros(n // 2, np.int32)]).astype(np.int32)]
     st = OracleState(np.concatenate(samples), np.array([0, n, n + 6, n + 6 + len(samples[2])],
                                                        np.int64), [1, 1], 2)
     want = st.merge_until(0, 0, 0)
-    e, got = run_engine(samples, [1, 1], {})
+    e, got = run_engine(samples, [1, 1], {}, mode=mode)
     assert got == want
     assert e.samples() == st.samples()
 
 
-def test_ties_need_r3():
+@pytest.mark.parametrize('mode', MODES)
+def test_ties_need_r3(mode):
     """Many pairs with equal W and equal a+b: the earliest W-th occurrence must win (R3)."""
     rng = random.Random(5)
     for trial in range(20):
@@ -114,7 +139,7 @@ def test_ties_need_r3():
         len16 = [1] * V
         st = OracleState(samples[0], np.array([0, len(seq)], np.int64), len16, V)
         want = st.merge_until(0, -1, 30)
-        e, got = run_engine(samples, len16, {'min_weight': -1, 'max_iterations': 30})
+        e, got = run_engine(samples, len16, {'min_weight': -1, 'max_iterations': 30}, mode=mode)
         assert got == want, trial
         assert e.samples() == st.samples()
 
@@ -168,6 +193,9 @@ def test_config3_prefix_vs_oracle():
     off = np.arange(0, n + 1, 1 << 20, dtype=np.int64)
     st = OracleState(ids, off, [1] * nt, nt, extra=64)
     del ids
+    g = load_config3_prefix()
+    if g is not None:   # the reference's own first merges (tests/golden/config3_prefix.json)
+        assert nt == g['char_count']
     for _ in range(3):
         want = st.find_next_merge(0, 2)
         got = e.find_next_merge(0, 2)
@@ -175,7 +203,11 @@ def test_config3_prefix_vs_oracle():
         c = st.n_tokens
         st.apply_merge(want[0], want[1])
         assert e.apply_merge(got[0], got[1], c) == got[2]
+        if g is not None:
+            assert list(got) == g['merges'][_]
     assert e.corpus_size()[1] == st.off[-1]
+    if g is not None:
+        assert e.corpus_size()[1] == g['live_tokens_after']
 
 
 def test_restore_style_apply_and_append_after_merges():
@@ -217,22 +249,24 @@ def test_restore_style_apply_and_append_after_merges():
     assert e.samples() == st2.samples()
 
 
-def test_compaction_under_heavy_merging():
+@pytest.mark.parametrize('mode', MODES)
+def test_compaction_under_heavy_merging(mode):
     """'ab' * 1.5M: the first merge halves the corpus, which triggers the dead-slot compaction."""
     n = 3_000_000
     sample = np.tile(np.array([0, 1], np.int32), n // 2)
     st = OracleState(sample, np.array([0, n], np.int64), [1, 1], 2, extra=64)
     want = st.merge_until(0, 2, 0)
-    e, got = run_engine([sample], [1, 1], {})
+    e, got = run_engine([sample], [1, 1], {}, mode=mode, stats=True)
     assert got == want
     assert e.samples() == st.samples()
 
 
+@pytest.mark.parametrize('mode', MODES)
 @pytest.mark.parametrize('early', [1, 2, 3])
-def test_ties_resolved_from_the_corpus_tail(early):
-    """R3 ties in a corpus larger than the device loop's tail window (8192 chunks): `early` of the
-    tied pairs occur only in the first quarter.  One such pair wins from the window alone; two or
-    more need the full pass (the loop hands the iteration to the host path)."""
+def test_ties_of_cold_pairs_in_a_large_corpus(early, mode):
+    """R3 ties of cold pairs (ids >= 256) in a corpus larger than the device loop's tail window:
+    `early` of the tied pairs occur only in the first quarter.  Their sketch buckets are heavy, so
+    the device loop hands these iterations to the host path (exact pass + full tie pass)."""
     rng = np.random.default_rng(early)
     n, V = 4_000_000, 3000
     seq = rng.integers(0, V, n, dtype=np.int32)      # filler: every filler pair is rare
@@ -251,9 +285,68 @@ def test_ties_resolved_from_the_corpus_tail(early):
     len16 = [1] * n_tok
     st = OracleState(seq, np.array([0, n], np.int64), len16, n_tok)
     want = st.merge_until(0, 2, 8)
-    e, got = run_engine([seq], len16, {'min_weight': 2, 'max_iterations': 8})
+    e, got = run_engine([seq], len16, {'min_weight': 2, 'max_iterations': 8}, mode=mode)
     assert got == want
     assert e.samples() == st.samples()
+
+
+def tail_tie_corpus(early, n=4_000_000, W=200, seed=0):
+    """Six hot pairs (a, b) with a + b = 11 and count W each (R3 ties: equal W, equal c_index),
+    in a filler of hot ids 12..239 whose pairs stay far below W.  The first `early` tied pairs
+    occur only in the first quarter of the corpus, before the device loop's tail window (the last
+    ~2M slots); the others occur all over, once in the last chunks.  Breakers drawn from 240..255
+    around every inserted pair keep the pairs of merged tokens (cold ids) rare, so no sketch
+    bucket turns heavy and the device loop decides every tie itself."""
+    rng = np.random.default_rng(seed + early)
+    seq = rng.integers(12, 240, n, dtype=np.int32)
+    pairs = [(k, 11 - k) for k in range(6)]
+    grid = np.arange(4, n - 200, 7)
+    perm = rng.permutation(len(grid))
+    early_grid = perm[grid[perm] < n // 4]
+    late_grid = perm[grid[perm] >= n // 4]
+    used_e = used_l = 0
+    for k, (a, b) in enumerate(pairs):
+        if k < early:
+            pos = grid[early_grid[used_e:used_e + W]]
+            used_e += W
+        else:
+            pos = grid[late_grid[used_l:used_l + W]]
+            used_l += W
+            pos[0] = n - 14 - 7 * k                    # one occurrence in the last chunks
+        for p in pos:
+            seq[p - 1] = 240 + rng.integers(0, 16)
+            seq[p], seq[p + 1] = a, b
+            seq[p + 2] = 240 + rng.integers(0, 16)
+    return seq
+
+
+@pytest.mark.parametrize('mode', MODES)
+@pytest.mark.parametrize('early', [0, 1, 2, 3])
+def test_ties_resolved_from_the_corpus_tail(early, mode):
+    """The device loop's R3 tail window (k_tie tail mode + k_decide phase 1,
+    csrc/bpe_kernels.hip.h) against the oracle, with each of its branches asserted through the
+    engine's counters: every tied pair in the window (decided there), the lone pair missing from
+    it (it wins: its last occurrence is earlier than every window occurrence), and two or more
+    missing (the iteration goes to the host path's full tie pass).  Reference: core.ts:294-305."""
+    seq = tail_tie_corpus(early)
+    n = len(seq)
+    len16 = [1] * 256
+    st = OracleState(seq, np.array([0, n], np.int64), len16, 256)
+    want = st.merge_until(0, 2, 8)
+    e, got = run_engine([seq], len16, {'min_weight': 2, 'max_iterations': 8}, mode=mode,
+                        stats=True)
+    assert got == want
+    assert [m[2] for m in got[:6]] == [200] * 6 and sorted(m[0] + m[1] for m in got[:6]) == [11] * 6
+    assert e.samples() == st.samples()
+    s = e.stats()
+    if mode == 'loop':
+        assert s['exact_passes'] == 0, s
+        if early == 0:      # every tie decided from the window
+            assert s['tie_tail'] >= 5 and s['tie_lone'] == 0 and s['loop_host'] == 0, s
+        elif early == 1:    # the lone missing pair wins, then the window decides the rest
+            assert s['tie_lone'] == 1 and s['tie_tail'] >= 5 and s['loop_host'] == 0, s
+        else:               # two or more missing: handed to the host path's full pass
+            assert s['loop_host'] >= 1, s
 
 
 def _flat(samples):
@@ -320,7 +413,8 @@ def test_encode_samples_with_a_trained_merge_list():
     assert got == st.samples()
 
 
-def test_runs_across_region_boundaries_from_a_fast_chunk():
+@pytest.mark.parametrize('mode', MODES)
+def test_runs_across_region_boundaries_from_a_fast_chunk(mode):
     """x x | x y at every region boundary (two chunks per region): the trailing run of each
     region has even length, which only the exact path of the region's last chunk works out
     (RegionSum.trail_odd -> k_runs).  A wrong parity counts one (x, x) too many per boundary."""
@@ -333,7 +427,7 @@ def test_runs_across_region_boundaries_from_a_fast_chunk():
         seq[p - 3:p + 2] = [3002, x, x, x, y]
     st = OracleState(seq, np.array([0, n], np.int64), [1] * 3003, 3003)
     want = st.merge_until(0, 2, 3)
-    e, got = run_engine([seq], [1] * 3003, {'min_weight': 2, 'max_iterations': 3})
+    e, got = run_engine([seq], [1] * 3003, {'min_weight': 2, 'max_iterations': 3}, mode=mode)
     assert got == want
     assert e.samples() == st.samples()
 
@@ -360,3 +454,57 @@ def test_zipf_words_vs_oracle(mib, n, max_length):
     assert eoff.tolist() == st.off.tolist()
     assert np.array_equal(flat, st.ids[:st.off[-1]])
     assert e.stats()['exact_passes'] <= 10
+
+
+@pytest.mark.slow
+def test_cold_pair_count_beyond_2_32():
+    """A cold pair whose count exceeds 2^32 (the reference's Map counts are JS numbers, exact to
+    2^53, core.ts:280-292): 'x' * (2^33 + 2) ingested as token id 300, so (300, 300) occurs
+    2^32 + 1 times (leftmost non-overlapping, core.ts:285-290).  Its sketch bucket is heavy, so
+    the exact cold-pair table counts it (64-bit counts), and the run crosses every region (k_runs
+    adds the pairs the waves could not see).  mergeUntil must give W = 2^32 + 1, 2^31, 2^30, 2^29."""
+    n = (1 << 33) + 2
+    data = np.full(n, ord('x'), np.uint8)
+    e = pkg.Engine(0)
+    for i in range(301):
+        e.set_token_len16(i, 1)
+    cmap = np.full(256, -1, np.int32)
+    cmap[ord('x')] = 300
+    _, nt, hist = e.add_latin1(data, sample_bytes=0, char_to_id=cmap, n_tokens=301)
+    del data
+    assert nt == 301 and hist[ord('x')] == n
+    got = e.merge_until(0, 2, 4)
+    assert got == [(300, 300, (1 << 32) + 1), (301, 301, 1 << 31), (302, 302, 1 << 30),
+                   (303, 303, 1 << 29)]
+    assert e.corpus_size() == (1, n - sum(m[2] for m in got))
+    e.close()
+
+
+@pytest.mark.slow
+def test_c3_dynamics_through_the_device_loop():
+    """The bench's timed path (bpe_merge_until: k_step_loop, k_select_multi, k_decide, the
+    tail-window tie pass, the dead-slot compaction) over the dynamics of BASELINE config 3, scaled
+    down: a 32 MiB uniform 256-char corpus (xorshift32 seed 12345, 1 MiB samples), 3000 merges.
+    Each merge removes ~W/N = 1/65536 of the stream, so the run crosses the 3 % compaction, and
+    about one iteration in ten is an R3 tie.  Checked against the multi-threaded CPU restatement
+    (itself pinned to the reference's fixtures): every merge and the final corpus."""
+    n = 32 << 20
+    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    e = pkg.Engine(0)
+    e.stats_enable(True)
+    cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    ids = cmap[data]
+    del data
+    off = np.arange(0, n + 1, 1 << 20, dtype=np.int64)
+    cpu = CpuMT(ids, off, [1] * nt, nt, threads=16, extra=4096)
+    del ids
+    want = cpu.merge_until(0, 2, 3000)
+    got = e.merge_until(0, 2, 3000)
+    s = e.stats()
+    assert got == want
+    flat, eoff = e.read_corpus()
+    cflat, coff = cpu.read()
+    assert np.array_equal(eoff, coff) and np.array_equal(flat, cflat)
+    assert s['compactions'] >= 1, s
+    assert s['tie_tail'] >= 10, s
+    assert s['tie_passes'] >= s['tie_tail'], s

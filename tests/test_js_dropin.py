@@ -31,7 +31,8 @@ def test_addon_builds_and_exports():
                                    "console.log(Object.keys(a).sort().join(','))",
                                    os.path.join(ADDON_DIR, 'bpe_napi.node')], text=True)
     assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEngine,'
-                           'deviceCount,findNextMerge,readCorpus,setTokenLen16')
+                           'deviceCount,encodeMerges,findNextMerge,mergeUntil,readCorpus,'
+                           'setTokenLen16')
 
 
 def test_host_logic_against_golden():
