@@ -27,6 +27,7 @@ MAX_VOCAB = 55296
 # Every symbol include/bpe.h and include/bpe_tools.h declare (checked by tests/test_capi.py).
 C_API = [
     'bpe_version', 'bpe_last_error', 'bpe_device_count', 'bpe_create', 'bpe_destroy',
+    'bpe_create_multi', 'bpe_shard_count',
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_apply_merges', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
@@ -37,6 +38,8 @@ C_API = [
 HOT_BINS = 65536
 TABLE_BINS = 81920
 MAX_CAND = 16       # BPE_MAX_CAND
+REDUCE_RCCL = 0     # BPE_REDUCE_RCCL
+REDUCE_HOST = 1     # BPE_REDUCE_HOST
 LOOP_BATCH = 64     # BPE_LOOP_BATCH
 
 
@@ -86,6 +89,9 @@ def lib():
         'bpe_device_count': ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'bpe_create': ([ctypes.POINTER(vp), ctypes.c_int], ctypes.c_int),
         'bpe_destroy': ([vp], ctypes.c_int),
+        'bpe_create_multi': ([ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                              ctypes.c_int], ctypes.c_int),
+        'bpe_shard_count': ([vp, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'bpe_set_token_len16': ([vp, ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
         'bpe_num_tokens': ([vp, i32p], ctypes.c_int),
         'bpe_add_sample': ([vp, i32p, ctypes.c_int64], ctypes.c_int),
@@ -171,11 +177,23 @@ def _i32(a):
 
 
 class Engine:
-    """One corpus shard on one HIP device (a `bpe_ctx`)."""
+    """One corpus shard on one HIP device (a `bpe_ctx`); with `devices`, one corpus sharded over
+    several (bpe_create_multi: RCCL all-reduces, or host copies when reduce='host')."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None, reduce='rccl'):
         self._ctx = ctypes.c_void_p()
-        _check(lib().bpe_create(ctypes.byref(self._ctx), device), 'bpe_create')
+        if devices is None:
+            _check(lib().bpe_create(ctypes.byref(self._ctx), device), 'bpe_create')
+        else:
+            dv = (ctypes.c_int * len(devices))(*devices)
+            _check(lib().bpe_create_multi(ctypes.byref(self._ctx), len(devices), dv,
+                                          REDUCE_HOST if reduce == 'host' else REDUCE_RCCL),
+                   'bpe_create_multi')
+
+    def shard_count(self):
+        n = ctypes.c_int()
+        _check(lib().bpe_shard_count(self._ctx, ctypes.byref(n)), 'bpe_shard_count')
+        return n.value
 
     def close(self):
         if self._ctx:

@@ -55,15 +55,32 @@ napi_value num(napi_env env, double x) {
     return v;
 }
 
-// createEngine(device) -> external handle (bpe_create, core.ts:77 `new BPETokenizer()`)
+// createEngine(device[, Int32Array devices, reduce]) -> external handle (bpe_create, core.ts:77
+// `new BPETokenizer()`); with a device list, one corpus sharded over those devices
+// (bpe_create_multi, reduce = BPE_REDUCE_RCCL 0 / BPE_REDUCE_HOST 1)
 napi_value CreateEngine(napi_env env, napi_callback_info info) {
-    napi_value argv[1];
+    napi_value argv[3];
     int device = 0;
-    size_t argc = 1;
+    size_t argc = 3;
     napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
     if (argc >= 1) device = (int)get_i64(env, argv[0]);
     bpe_ctx *ctx = nullptr;
-    if (bpe_create(&ctx, device) != BPE_OK) return throw_native(env, "bpe_create");
+    napi_valuetype t = napi_undefined;
+    if (argc >= 2) napi_typeof(env, argv[1], &t);
+    if (argc >= 2 && t == napi_object) {
+        napi_typedarray_type type;
+        size_t n = 0, off = 0;
+        void *data = nullptr;
+        napi_value ab;
+        if (napi_get_typedarray_info(env, argv[1], &type, &n, &data, &ab, &off) != napi_ok ||
+            type != napi_int32_array || n == 0)
+            return throw_arg(env, "createEngine expects an Int32Array of device indices");
+        const int reduce = argc >= 3 ? (int)get_i64(env, argv[2]) : BPE_REDUCE_RCCL;
+        if (bpe_create_multi(&ctx, (int)n, static_cast<const int *>(data), reduce) != BPE_OK)
+            return throw_native(env, "bpe_create_multi");
+    } else if (bpe_create(&ctx, device) != BPE_OK) {
+        return throw_native(env, "bpe_create");
+    }
     napi_value ext;
     napi_create_external(env, ctx, finalize_ctx, nullptr, &ext);
     return ext;

@@ -10,6 +10,7 @@
 // so a mergeUntil iteration streams the corpus exactly once.
 #include "bpe_kernels.hip.h"
 #include "bpe.h"
+#include "bpe_multi.h"
 #include "bpe_tools.h"
 
 #include <algorithm>
@@ -64,6 +65,9 @@ int dev_alloc(T **p, size_t n) {
 }  // namespace
 
 struct bpe_ctx {
+    // a corpus sharded over several devices (bpe_create_multi): every entry point forwards to
+    // csrc/bpe_multi.cpp, which drives one single-device context per shard
+    bpe_multi *multi = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     // corpus: n_chunks left-packed chunks + one all-SEP spare chunk
@@ -1153,6 +1157,16 @@ int append_begin(bpe_ctx *c, int64_t extra_slots) {
 
 }  // namespace
 
+int bpe_fail(int code, const char *msg) { return fail(code, msg); }
+
+// a multi-device context forwards the call; per-shard entry points refuse it
+#define MULTI(call) \
+    if (c && c->multi) return multi_##call
+#define NOT_MULTI                                                                          \
+    if (c && c->multi)                                                                     \
+        return fail(BPE_ERR_STATE, "bpe native: a per-shard entry point on a multi-device " \
+                                   "context (drive its shards through bpe_create instead)")
+
 // ================================================================================================
 // C ABI
 // ================================================================================================
@@ -1227,8 +1241,32 @@ int bpe_create(bpe_ctx **out, int device) {
     return BPE_OK;
 }
 
+int bpe_create_multi(bpe_ctx **out, int n_shards, const int *devices, int reduce) {
+    if (!out) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    *out = nullptr;
+    bpe_multi *m = nullptr;
+    int rc = multi_create(&m, n_shards, devices, reduce);
+    if (rc) return rc;
+    bpe_ctx *c = new bpe_ctx();
+    c->multi = m;
+    *out = c;
+    return BPE_OK;
+}
+
+int bpe_shard_count(bpe_ctx *c, int *n) {
+    if (!c || !n) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    MULTI(shard_count(c->multi, n));
+    *n = 1;
+    return BPE_OK;
+}
+
 int bpe_destroy(bpe_ctx *c) {
     if (!c) return BPE_OK;
+    if (c->multi) {
+        multi_destroy(c->multi);
+        delete c;
+        return BPE_OK;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
@@ -1250,6 +1288,7 @@ int bpe_destroy(bpe_ctx *c) {
 }
 
 int bpe_set_token_len16(bpe_ctx *c, int32_t id, int32_t len16) {
+    MULTI(set_token_len16(c->multi, id, len16));
     if (!c || id < 0 || len16 < 0) return fail(BPE_ERR_ARG, "bpe native: bad token registration");
     if (id >= BPE_MAX_VOCAB)
         return fail(BPE_ERR_VOCAB, "bpe native: vocab is limited to 55295 tokens (UTF-16 surrogates)");
@@ -1264,12 +1303,14 @@ int bpe_set_token_len16(bpe_ctx *c, int32_t id, int32_t len16) {
 }
 
 int bpe_num_tokens(bpe_ctx *c, int32_t *n) {
+    if (c && n) MULTI(num_tokens(c->multi, n));
     if (!c || !n) return fail(BPE_ERR_ARG, "bpe native: null argument");
     *n = (int32_t)c->h_len16.size();
     return BPE_OK;
 }
 
 int bpe_add_sample(bpe_ctx *c, const int32_t *ids, int64_t n) {
+    if (n >= 0 && (n == 0 || ids)) MULTI(add_sample(c->multi, ids, n));
     if (!c || n < 0 || (n > 0 && !ids)) return fail(BPE_ERR_ARG, "bpe native: bad sample");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1298,6 +1339,7 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
                    int32_t char_to_id[256], int32_t *n_tokens_io, int64_t char_hist[256]) {
     if (!c || n < 0 || (n > 0 && !bytes) || !char_to_id || !n_tokens_io || sample_bytes < 0)
         return fail(BPE_ERR_ARG, "bpe native: bad latin1 ingest arguments");
+    MULTI(add_latin1(c->multi, bytes, n, sample_bytes, char_to_id, n_tokens_io, char_hist));
     int rc = set_device(c);
     if (rc) return rc;
     if (n == 0) {
@@ -1386,6 +1428,7 @@ int bpe_add_latin1(bpe_ctx *c, const uint8_t *bytes, int64_t n, int64_t sample_b
 }
 
 int bpe_clear_corpus(bpe_ctx *c) {
+    MULTI(clear_corpus(c->multi));
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1398,6 +1441,7 @@ int bpe_clear_corpus(bpe_ctx *c) {
 }
 
 int bpe_corpus_size(bpe_ctx *c, int64_t *n_samples, int64_t *n_tokens) {
+    MULTI(corpus_size(c->multi, n_samples, n_tokens));
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1410,6 +1454,7 @@ int bpe_corpus_size(bpe_ctx *c, int64_t *n_samples, int64_t *n_tokens) {
 int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
                     int64_t off_cap) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    MULTI(read_corpus(c->multi, ids_out, ids_cap, sample_off, off_cap));
     if (ids_cap < c->n_live || off_cap < c->n_samples + 1 || (c->n_live && !ids_out) || !sample_off)
         return fail(BPE_ERR_ARG, "bpe native: read_corpus buffers too small");
     int rc = set_device(c);
@@ -1439,6 +1484,7 @@ int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *samp
 
 int bpe_find_next_merge(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a,
                         int32_t *b, int64_t *w) {
+    if (a && b && w) MULTI(find_next_merge(c->multi, max_length, min_weight, a, b, w));
     if (!c || !a || !b || !w) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1446,6 +1492,7 @@ int bpe_find_next_merge(bpe_ctx *c, int64_t max_length, int64_t min_weight, int3
 }
 
 int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
+    MULTI(apply_merge(c->multi, a, b, cc, replaced));
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1454,6 +1501,7 @@ int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *repla
 
 int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint64_t *table,
                         uint64_t *tie, int rank) {
+    NOT_MULTI;
     if (!c || !table || !tie || rank < 0) return fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1462,24 +1510,28 @@ int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint
 }
 
 int bpe_rank_loop_select(bpe_ctx *c) {
+    NOT_MULTI;
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     return rc ? rc : rank_loop_select(c);
 }
 
 int bpe_rank_loop_decide(bpe_ctx *c) {
+    NOT_MULTI;
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     return rc ? rc : rank_loop_decide(c);
 }
 
 int bpe_rank_loop_count(bpe_ctx *c) {
+    NOT_MULTI;
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     return rc ? rc : rank_loop_count(c);
 }
 
 int bpe_rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status) {
+    NOT_MULTI;
     if (!c || !n_merges || !status || (cap > 0 && !out_abw))
         return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
@@ -1487,6 +1539,7 @@ int bpe_rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_merg
 }
 
 int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, int count_after) {
+    if (n >= 0 && (n == 0 || abc)) MULTI(apply_merges(c->multi, abc, n, replaced, count_after));
     if (!c || n < 0 || (n > 0 && !abc)) return fail(BPE_ERR_ARG, "bpe native: bad apply_merges arguments");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1495,6 +1548,7 @@ int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replace
 
 int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
                     int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    if (n_merges && (cap <= 0 || out_abw)) MULTI(merge_until(c->multi, max_length, min_weight, max_iterations, out_abw, cap, n_merges));
     if (!c || !n_merges || (cap > 0 && !out_abw))
         return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
@@ -1563,6 +1617,7 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
 }
 
 int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
+    NOT_MULTI;
     if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1577,6 +1632,7 @@ int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
 
 int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint32_t *cold_keys,
                      uint64_t *cold_counts, int64_t cap, int64_t *n_cold) {
+    NOT_MULTI;
     if (!c || !table || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1611,6 +1667,7 @@ int bpe_select_counts(bpe_ctx *c, const uint64_t *table, const uint32_t *cold_ke
                       const uint64_t *cold_counts, int64_t n_cold, int64_t max_length,
                       int64_t min_weight, int32_t *cand, int64_t cap, int64_t *n_cand,
                       int64_t *w) {
+    NOT_MULTI;
     const uint64_t *hot = table;
     if (!c || !hot || !n_cand || !w || n_cold < 0 || (n_cold && (!cold_keys || !cold_counts)) ||
         (cap > 0 && !cand))
@@ -1652,6 +1709,7 @@ int bpe_select_counts(bpe_ctx *c, const uint64_t *table, const uint32_t *cold_ke
 }
 
 int bpe_tie_positions(bpe_ctx *c, const int32_t *cand, int64_t n, uint64_t *last) {
+    NOT_MULTI;
     if (!c || n < 0 || (n > 0 && (!cand || !last)))
         return fail(BPE_ERR_ARG, "bpe native: bad tie arguments");
     int rc = set_device(c);
@@ -1666,12 +1724,14 @@ int bpe_tie_positions(bpe_ctx *c, const int32_t *cand, int64_t n, uint64_t *last
 }
 
 int bpe_stats_enable(bpe_ctx *c, int on) {
+    MULTI(stats_enable(c->multi, on));
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     c->stats_on = on != 0;
     return BPE_OK;
 }
 
 int bpe_get_stats(bpe_ctx *c, bpe_stats *out) {
+    if (out) MULTI(get_stats(c->multi, out));
     if (!c || !out) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = flush_spans(c);
     if (rc) return rc;
@@ -1680,6 +1740,7 @@ int bpe_get_stats(bpe_ctx *c, bpe_stats *out) {
 }
 
 int bpe_reset_stats(bpe_ctx *c) {
+    MULTI(reset_stats(c->multi));
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = flush_spans(c);
     if (rc) return rc;
@@ -1688,6 +1749,7 @@ int bpe_reset_stats(bpe_ctx *c) {
 }
 
 int bpe_recount(bpe_ctx *c) {
+    NOT_MULTI;
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1696,6 +1758,7 @@ int bpe_recount(bpe_ctx *c) {
 }
 
 int bpe_get_stream(bpe_ctx *c, void **stream) {
+    if (stream) MULTI(get_stream(c->multi, stream));
     if (!c || !stream) return fail(BPE_ERR_ARG, "bpe native: null argument");
     *stream = (void *)c->stream;
     return BPE_OK;

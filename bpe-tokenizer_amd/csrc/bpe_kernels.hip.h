@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace bpe {
 
 constexpr int32_t SEP = -1;                 // sample separator (live slot, never in a pair)
@@ -42,6 +44,24 @@ constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x 
 #define BPE_WAVES 16
 #endif
 constexpr int WAVES_PER_WG = BPE_WAVES;
+// Register ring of the streaming passes: RING chunks per wave (k_step: loads issued RING - 3
+// chunks ahead, k_tie: RING - 2).  Depth 2 already streams at 5.8 TB/s and 12 at 6.06
+// (tools/probe/stream_probe.hip); 7, 9 and 11 time alike in k_step.
+#ifndef BPE_RING
+#define BPE_RING 7
+#endif
+constexpr int RING = BPE_RING;
+static_assert(RING >= 5, "ring depth");
+
+// f(integral_constant<I>) for I = 0 .. N-1, unrolled in the source (the ring's slot indices must be
+// compile-time constants, or the ring is moved to scratch memory)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
 constexpr int WG = WAVES_PER_WG * 64;       // one workgroup per CU (LDS-bound)
 constexpr int MAX_WG = 256;                 // one per CU on MI355X
 constexpr int MAX_REGIONS = MAX_WG * WAVES_PER_WG;
@@ -708,27 +728,48 @@ __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, 
     inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
 }
 
+// The LDS adds of a fast-path chunk; their returned words go to o (the overflow screen runs a
+// stage later, check_deferred, so no wave waits on its LDS atomics' return).
 template <bool FUSED = false>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
-                                          const Sink &k) {
-    uint32_t o[4];
+                                          const Sink &k, uint32_t (&o)[4]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t addr, inc;
         pair_slot<FUSED>(x[e], y[e], addr, inc);
         o[e] = atomicAdd(lds_word(k, addr), inc);
     }
-    // conservative screen: only a counter at >= 0x4000 can be at 0x7FFF
-    if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
+}
+
+// A fast-path count whose overflow screen is still due: the words its LDS adds returned.  The
+// screen runs one stage later (the chunk and its right-hand neighbour are still in the ring), so
+// the adds' return latency hides behind the next chunk's work.  The delay is safe: a counter
+// that reached 0x8000 takes at most two stages of the workgroup's adds (16 waves x 512 pairs)
+// before its 0x8000 is moved to the spill, far below the 32K of headroom under 0xFFFF.
+struct Defer {
+    uint32_t o[4];
+    int pend;   // o holds the returns of a fast-path chunk (wave-uniform)
+};
+
+// The deferred overflow screen of the chunk w counted at the previous stage (nxt = the first
+// post-merge token after it).  Conservative: only a counter at >= 0x4000 can be at 0x7FFF; then
+// the chunk's pairs are recomputed (rare) and each lane that saw 0x7FFF spills.
+template <bool FUSED>
+__device__ __forceinline__ void check_deferred(const Chunk &w, int32_t nxt, const Defer &d,
+                                               const Sink &k) {
+    if (!d.pend) return;
+    if (__ballot(((d.o[0] | d.o[1] | d.o[2] | d.o[3]) & 0x40004000u) != 0u) == 0ull) return;
+    int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
+    asm volatile("" : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3));
+    const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
+    const int32_t x3 = sel(lane_in(P63), w.last, t3);
+    const int32_t r3 = from_next(t0, nxt);
+    const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            // recomputed here (rare) rather than kept live across the adds
-            int32_t xx = x[e], yy = y[e];
-            asm volatile("" : "+v"(xx), "+v"(yy));
-            uint32_t addr, inc;
-            pair_slot<FUSED>(xx, yy, addr, inc);
-            if (inc) lds_fix(k, addr, inc, (uint32_t)table_index(xx, yy), o[e]);
-        }
+    for (int e = 0; e < 4; ++e) {
+        uint32_t addr, inc;
+        pair_slot<FUSED>(x[e], y[e], addr, inc);
+        if (inc) lds_fix(k, addr, inc, (uint32_t)table_index(x[e], y[e]), d.o[e]);
     }
 }
 
@@ -771,9 +812,12 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
 // TAIL: the region's last chunk (nxt = NONE).  It always takes the exact path: the parity of its
 // last token's run offset feeds RegionSum::trail_odd, which k_runs needs whenever that run goes on
 // in the next region, and the fast path does not work that parity out.
+// Fast-path counts of MODE_TABLE / MODE_FUSED leave their overflow screen in `df` (check_deferred
+// at the next stage); every other path finishes here.  (Screening before the next chunk's adds
+// instead, so that it waits on nothing newer, timed 2.4 % slower.)
 template <int MODE, bool TAIL = false>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
-                                            const Sink &k) {
+                                            const Sink &k, Defer &df) {
     const int len = w.len;
     if (MODE == MODE_NONE && !TAIL) {
         // apply-only passes keep only the region sums: the chunk needs work only in the region's
@@ -818,23 +862,17 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 cold = __ballot(mx >= (uint32_t)HOT);
             }
             if (cold == 0ull) {
-                uint32_t o[4];
+                // (the deferred screen recomputes these as pair_slot, which equals the hot form
+                // for valid hot pairs)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
-                if (__ballot(((o[0] | o[1] | o[2] | o[3]) & 0x40004000u) != 0u) != 0ull) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        int32_t xx = x[e], yy = y[e];
-                        asm volatile("" : "+v"(xx), "+v"(yy));
-                        lds_fix(k, hot_addr(xx, yy), hot_inc(xx), hot_bin((uint32_t)xx, (uint32_t)yy), o[e]);
-                    }
-                }
+                    df.o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
             } else {
                 // mixed planes (partial chunks hold merged tokens: the steady state)
-                add_pairs<MODE == MODE_FUSED>(x, y, k);
+                add_pairs<MODE == MODE_FUSED>(x, y, k, df.o);
                 if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
             }
+            df.pend = 1;
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -1078,7 +1116,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             ids + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
         const int lo = lane * 16;
-        auto load = [&](Chunk &q, int c) {
+        auto load = [&](Chunk &q, int c) __attribute__((always_inline)) {
             const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
             q.t[0] = (int)x[0];
             q.t[1] = (int)x[1];
@@ -1101,11 +1139,15 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             return v;
         };
         const uint32_t key = pack_pair_s(ma, mb);
-        // Ring of seven: stage c applies chunk c (cur), counts chunk c-1 (prv) and loads chunk
-        // c+5 into the slot of chunk c-2 (fre), which the previous stage freed, so the load can
-        // issue at once without its registers overlapping a chunk still in use.
-        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c) {
-            load(fre, c + 5);
+        // Ring of RING slots: stage c applies chunk c (cur), counts chunk c-1 (prv), runs the
+        // deferred overflow screen of chunk c-2 (chk, counted at stage c-1) and loads chunk
+        // c+RING-3 into the slot of chunk c-3 (fre), which the previous stage freed, so the load
+        // can issue at once without its registers overlapping a chunk still in use.
+        Defer dq;
+        dq.pend = 0;
+        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, const Chunk &chk,
+                         Chunk &fre, int c) __attribute__((always_inline)) {
+            load(fre, c + RING - 3);
             if (c < nc) {
                 finish_load(cur);
             } else {
@@ -1118,39 +1160,41 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             if (MERGE && cur.len)
                 apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, key,
                                    rs, c, lane, ap);
+            Defer dn;
+            dn.pend = 0;
             if (cur.len) {
-                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k);
+                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, dn);
             } else {
                 cur = prv;   // rare: hand the pending chunk on
             }
+            // (chk was counted at the previous stage against prv's first token, both unchanged)
+            check_deferred<MODE == MODE_FUSED>(chk, prv.first, dq, k);
+            dq = dn;
         };
         if (nc > 0) {
-            Chunk S0, S1, S2, S3, S4, S5, S6;
-            load(S0, 0);
-            load(S1, 1);
-            load(S2, 2);
-            load(S3, 3);
-            load(S4, 4);
-            S6.len = 0;
+            Chunk S[RING];   // (constant indices only: the ring stays in registers)
+            static_for<0, RING - 3>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
+            S[RING - 1].len = 0;
             if (MERGE) {
                 // does the token before the region match the region's first live token?
-                const int32_t f = live_from(0, bcast(S0.t[0], 0));
+                const int32_t f = live_from(0, bcast(S[0].t[0], 0));
                 // (integer arithmetic: a short-circuit && here makes the flag a vector value)
                 ap.match = (((uint32_t)(ap.prev ^ ma) | (uint32_t)(f ^ mb)) == 0u) &
                            ((MERGE == MERGE_XY) | (ap.par == 0));
             }
-            // whole rounds of seven stages; stages past the region see empty chunks, so the
-            // pending chunk always ends in S6
-            for (int c = 0; c < nc; c += 7) {
-                stage(S0, S1, S6, S5, c);
-                stage(S1, S2, S0, S6, c + 1);
-                stage(S2, S3, S1, S0, c + 2);
-                stage(S3, S4, S2, S1, c + 3);
-                stage(S4, S5, S3, S2, c + 4);
-                stage(S5, S6, S4, S3, c + 5);
-                stage(S6, S0, S5, S4, c + 6);
+            // whole rounds of RING stages; stages past the region see empty chunks, so the
+            // pending chunk always ends in the last slot
+            for (int c = 0; c < nc; c += RING) {
+                static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
+                    constexpr int i = decltype(I)::value;
+                    stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
+                          S[(i + RING - 2) % RING], S[(i + RING - 3) % RING], c + i);
+                });
             }
-            if (S6.len) count_chunk<MODE, true>(S6, NONE, lane, s, k);
+            check_deferred<MODE == MODE_FUSED>(S[RING - 2], S[RING - 1].first, dq, k);
+            Defer dt;
+            dt.pend = 0;
+            if (S[RING - 1].len) count_chunk<MODE, true>(S[RING - 1], NONE, lane, s, k, dt);
         }
         if (lane == 0) {
             RegionSum o;
@@ -1923,7 +1967,7 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<int32_t *>(A.ids) + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
     const int lo = lane * 16;
-    auto load = [&](Chunk &q, int c) {
+    auto load = [&](Chunk &q, int c) __attribute__((always_inline)) {
         const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
         q.t[0] = (int)x[0];
         q.t[1] = (int)x[1];
@@ -1931,9 +1975,9 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         q.t[3] = (int)x[3];
     };
     int pc = 0;   // chunk index of the pending chunk
-    // ring of seven, as in k_step: chunk c+5 loads into the slot chunk c-2 freed
-    auto stage = [&](Chunk &cur, Chunk &prv, Chunk &fre, int c) {
-        load(fre, c + 5);
+    // the ring of k_step: chunk c+RING-2 loads into the slot chunk c-2 freed
+    auto stage = [&](Chunk &cur, Chunk &prv, Chunk &fre, int c) __attribute__((always_inline)) {
+        load(fre, c + RING - 2);
         if (c < nc) {
             finish_load(cur);
         } else {
@@ -1948,23 +1992,16 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
             cur = prv;   // rare: hand the pending chunk on
         }
     };
-    Chunk S0, S1, S2, S3, S4, S5, S6;
-    load(S0, 0);
-    load(S1, 1);
-    load(S2, 2);
-    load(S3, 3);
-    load(S4, 4);
-    S6.len = 0;
-    for (int c = 0; c < nc; c += 7) {
-        stage(S0, S6, S5, c);
-        stage(S1, S0, S6, c + 1);
-        stage(S2, S1, S0, c + 2);
-        stage(S3, S2, S1, c + 3);
-        stage(S4, S3, S2, c + 4);
-        stage(S5, S4, S3, c + 5);
-        stage(S6, S5, S4, c + 6);
+    Chunk S[RING];
+    static_for<0, RING - 2>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
+    S[RING - 1].len = 0;
+    for (int c = 0; c < nc; c += RING) {
+        static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
+            constexpr int i = decltype(I)::value;
+            stage(S[i], S[(i + RING - 1) % RING], S[(i + RING - 2) % RING], c + i);
+        });
     }
-    if (S6.len) tie_chunk(S6, rc.next_tok, pc, lane, ts);
+    if (S[RING - 1].len) tie_chunk(S[RING - 1], rc.next_tok, pc, lane, ts);
     if (lane == 0) {
 #pragma unroll
         for (int j = 0; j < MAX_CAND; ++j)

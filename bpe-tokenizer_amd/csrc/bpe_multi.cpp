@@ -1,0 +1,569 @@
+// bpe_multi.cpp — one corpus sharded over several HIP devices behind ONE bpe_ctx
+// (bpe_create_multi, include/bpe.h): the drop-in's BPE_NUM_GPUS, so that `new BPETokenizer()`
+// (core.ts:77) and every corpus-touching method keep their surface while the corpus spans the
+// GPUs of the node.
+//
+// Layout.  Shard r is an ordinary single-device context holding a contiguous run of whole
+// samples, in corpus order: pairs never cross samples (core.ts:265-267), so each shard counts
+// and rewrites its samples alone, and rule R3's "earliest last occurrence" compares
+// (shard, shard-local position) lexicographically.  Samples added before the first pass over the
+// corpus are staged on the host and then cut into n runs of about equal token counts; samples
+// added later go to the last shard (corpus order is kept).
+//
+// Exchange per merge iteration (the device-resident rank loop of every shard, bpe_rank_loop_*):
+//   all-reduce(SUM) of the 81920-bin pair table -> selection on every shard from the same global
+//   table -> all-reduce(MAX) of the tied candidates' (shard << 40 | last position) -> decision ->
+//   the fused apply + count pass of every shard.
+// The all-reduces run over RCCL (one communicator per device, ncclCommInitAll, grouped calls on
+// the shards' streams) or, for shards sharing a device (tests), as host copies.  An iteration the
+// rank loop cannot finish (heavy sketch buckets, many tied pairs) takes the host protocol: global
+// table, exact counts of the heavy cold pairs on every shard, global selection, tie positions.
+#include "bpe_multi.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int64_t RANK_SHIFT = 40;   // as sharded.py / k_tie_export: rank << 40 | position
+
+struct Rccl {
+    void *so = nullptr;
+    ncclResult_t (*init_all)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t,
+                               ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+}  // namespace
+
+struct bpe_multi {
+    int n = 0;
+    int reduce = BPE_REDUCE_HOST;
+    std::vector<int> dev;
+    std::vector<bpe_ctx *> sh;
+    std::vector<hipStream_t> st;
+    std::vector<unsigned long long *> d_table, d_tie;   // per shard, on its device
+    std::vector<uint32_t *> d_keys;                      // per shard: exact cold-pair lists
+    std::vector<unsigned long long *> d_counts;
+    int64_t cold_cap = 0;
+    unsigned long long *h_buf = nullptr, *h_sum = nullptr;   // pinned, BPE_TABLE_BINS each
+    std::vector<std::vector<int32_t>> staged;            // samples not yet on a device
+    bool distributed = false;
+    std::vector<ncclComm_t> comms;
+    Rccl rccl;
+};
+
+namespace {
+
+#define MHIP(expr)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return bpe_fail(e_ == hipErrorOutOfMemory ? BPE_ERR_OOM : BPE_ERR_HIP,        \
+                            (std::string("bpe native: ") + #expr + ": " +                 \
+                             hipGetErrorString(e_)).c_str());                              \
+    } while (0)
+
+#define MTRY(expr)                 \
+    do {                           \
+        int rc_ = (expr);          \
+        if (rc_ < 0) return rc_;   \
+    } while (0)
+
+int load_rccl(Rccl &r) {
+    const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char *nm : names)
+        if ((r.so = dlopen(nm, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!r.so) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL (librccl.so) not found");
+    r.init_all = (decltype(r.init_all))dlsym(r.so, "ncclCommInitAll");
+    r.all_reduce = (decltype(r.all_reduce))dlsym(r.so, "ncclAllReduce");
+    r.group_start = (decltype(r.group_start))dlsym(r.so, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(r.so, "ncclGroupEnd");
+    r.destroy = (decltype(r.destroy))dlsym(r.so, "ncclCommDestroy");
+    r.error_string = (decltype(r.error_string))dlsym(r.so, "ncclGetErrorString");
+    if (!r.init_all || !r.all_reduce || !r.group_start || !r.group_end || !r.destroy)
+        return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
+    return BPE_OK;
+}
+
+int nccl_check(bpe_multi *m, ncclResult_t r, const char *what) {
+    if (r == ncclSuccess) return BPE_OK;
+    std::string msg = std::string("bpe native: ") + what + ": " +
+                      (m->rccl.error_string ? m->rccl.error_string(r) : "RCCL error");
+    return bpe_fail(BPE_ERR_HIP, msg.c_str());
+}
+
+// In-place all-reduce of count u64 per shard (SUM or MAX), ordered on the shards' streams.
+int all_reduce(bpe_multi *m, std::vector<unsigned long long *> &buf, size_t count, bool max) {
+    if (m->n == 1) return BPE_OK;
+    if (m->reduce == BPE_REDUCE_RCCL) {
+        MTRY(nccl_check(m, m->rccl.group_start(), "ncclGroupStart"));
+        for (int r = 0; r < m->n; ++r) {
+            ncclResult_t e = m->rccl.all_reduce(buf[r], buf[r], count, ncclUint64,
+                                                max ? ncclMax : ncclSum, m->comms[r], m->st[r]);
+            if (e != ncclSuccess) {
+                m->rccl.group_end();
+                return nccl_check(m, e, "ncclAllReduce");
+            }
+        }
+        return nccl_check(m, m->rccl.group_end(), "ncclGroupEnd");
+    }
+    // host copies (shards sharing a device): after each shard's stream has produced its part
+    for (int r = 0; r < m->n; ++r) {
+        MHIP(hipSetDevice(m->dev[r]));
+        MHIP(hipMemcpyAsync(m->h_buf, buf[r], count * 8, hipMemcpyDeviceToHost, m->st[r]));
+        MHIP(hipStreamSynchronize(m->st[r]));
+        if (r == 0) {
+            std::memcpy(m->h_sum, m->h_buf, count * 8);
+        } else if (max) {
+            for (size_t i = 0; i < count; ++i) m->h_sum[i] = std::max(m->h_sum[i], m->h_buf[i]);
+        } else {
+            for (size_t i = 0; i < count; ++i) m->h_sum[i] += m->h_buf[i];
+        }
+    }
+    for (int r = 0; r < m->n; ++r) {
+        MHIP(hipSetDevice(m->dev[r]));
+        MHIP(hipMemcpyAsync(buf[r], m->h_sum, count * 8, hipMemcpyHostToDevice, m->st[r]));
+        MHIP(hipStreamSynchronize(m->st[r]));   // (h_sum is reused by the next reduction)
+    }
+    return BPE_OK;
+}
+
+// The staged samples, cut into n contiguous runs of about equal token counts.
+int distribute(bpe_multi *m) {
+    if (m->distributed) return BPE_OK;
+    m->distributed = true;
+    int64_t total = 0;
+    for (auto &s : m->staged) total += (int64_t)s.size();
+    int64_t acc = 0;
+    for (auto &s : m->staged) {
+        const int64_t len = (int64_t)s.size();
+        int r = total ? (int)std::min<int64_t>(m->n - 1, (acc + len / 2) * m->n / total) : 0;
+        MTRY(bpe_add_sample(m->sh[r], s.data(), len));
+        acc += len;
+        std::vector<int32_t>().swap(s);
+    }
+    m->staged.clear();
+    return BPE_OK;
+}
+
+int ensure_cold_bufs(bpe_multi *m, int64_t need) {
+    if (need <= m->cold_cap) return BPE_OK;
+    int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1 << 16, 2 * m->cold_cap));
+    for (int r = 0; r < m->n; ++r) {
+        MHIP(hipSetDevice(m->dev[r]));
+        if (m->d_keys[r]) (void)hipFree(m->d_keys[r]);
+        if (m->d_counts[r]) (void)hipFree(m->d_counts[r]);
+        m->d_keys[r] = nullptr;
+        m->d_counts[r] = nullptr;
+        MHIP(hipMalloc((void **)&m->d_keys[r], cap * sizeof(uint32_t)));
+        MHIP(hipMalloc((void **)&m->d_counts[r], cap * sizeof(unsigned long long)));
+    }
+    m->cold_cap = cap;
+    return BPE_OK;
+}
+
+}  // namespace
+
+// ---- lifecycle -----------------------------------------------------------------------------------
+int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
+    *out = nullptr;
+    if (n < 1 || (reduce != BPE_REDUCE_RCCL && reduce != BPE_REDUCE_HOST))
+        return bpe_fail(BPE_ERR_ARG, "bpe native: bad multi-device arguments");
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev == 0)
+        return bpe_fail(BPE_ERR_HIP, "bpe native: no HIP device available (MI355X required)");
+    bpe_multi *m = new bpe_multi();
+    m->n = n;
+    m->reduce = reduce;
+    for (int r = 0; r < n; ++r) m->dev.push_back(devices ? devices[r] : r);
+    auto bail = [&](int rc) {
+        multi_destroy(m);
+        return rc;
+    };
+    for (int r = 0; r < n; ++r) {
+        if (m->dev[r] < 0 || m->dev[r] >= n_dev)
+            return bail(bpe_fail(BPE_ERR_ARG, "bpe native: bad device index"));
+        for (int q = 0; q < r; ++q)
+            if (m->dev[q] == m->dev[r] && reduce == BPE_REDUCE_RCCL)
+                return bail(bpe_fail(BPE_ERR_ARG, "bpe native: RCCL needs one shard per device "
+                                                  "(use BPE_REDUCE_HOST for shared devices)"));
+    }
+    m->sh.assign(n, nullptr);
+    m->st.assign(n, nullptr);
+    m->d_table.assign(n, nullptr);
+    m->d_tie.assign(n, nullptr);
+    m->d_keys.assign(n, nullptr);
+    m->d_counts.assign(n, nullptr);
+    for (int r = 0; r < n; ++r) {
+        int rc = bpe_create(&m->sh[r], m->dev[r]);
+        if (rc) return bail(rc);
+        void *s = nullptr;
+        bpe_get_stream(m->sh[r], &s);
+        m->st[r] = (hipStream_t)s;
+        if (hipSetDevice(m->dev[r]) != hipSuccess ||
+            hipMalloc((void **)&m->d_table[r], BPE_TABLE_BINS * 8) != hipSuccess ||
+            hipMalloc((void **)&m->d_tie[r], BPE_MAX_CAND * 8) != hipSuccess)
+            return bail(bpe_fail(BPE_ERR_OOM, "bpe native: multi-device buffers"));
+    }
+    if (hipHostMalloc((void **)&m->h_buf, BPE_TABLE_BINS * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&m->h_sum, BPE_TABLE_BINS * 8, hipHostMallocDefault) != hipSuccess)
+        return bail(bpe_fail(BPE_ERR_OOM, "bpe native: pinned host buffers"));
+    if (reduce == BPE_REDUCE_RCCL && n > 1) {
+        int rc = load_rccl(m->rccl);
+        if (rc) return bail(rc);
+        m->comms.assign(n, nullptr);
+        rc = nccl_check(m, m->rccl.init_all(m->comms.data(), n, m->dev.data()), "ncclCommInitAll");
+        if (rc) {
+            m->comms.clear();
+            return bail(rc);
+        }
+    }
+    *out = m;
+    return BPE_OK;
+}
+
+int multi_destroy(bpe_multi *m) {
+    if (!m) return BPE_OK;
+    for (auto c : m->comms)
+        if (c && m->rccl.destroy) m->rccl.destroy(c);
+    for (int r = 0; r < (int)m->sh.size(); ++r) {
+        (void)hipSetDevice(m->dev[r]);
+        if (m->sh[r]) bpe_destroy(m->sh[r]);
+        void *ptrs[] = {m->d_table[r], m->d_tie[r], m->d_keys[r], m->d_counts[r]};
+        for (void *p : ptrs)
+            if (p) (void)hipFree(p);
+    }
+    if (m->h_buf) (void)hipHostFree(m->h_buf);
+    if (m->h_sum) (void)hipHostFree(m->h_sum);
+    if (m->rccl.so) dlclose(m->rccl.so);
+    delete m;
+    return BPE_OK;
+}
+
+int multi_shard_count(bpe_multi *m, int *n) {
+    *n = m->n;
+    return BPE_OK;
+}
+
+// ---- vocabulary and corpus ------------------------------------------------------------------------
+int multi_set_token_len16(bpe_multi *m, int32_t id, int32_t len16) {
+    for (auto s : m->sh) MTRY(bpe_set_token_len16(s, id, len16));
+    return BPE_OK;
+}
+
+int multi_num_tokens(bpe_multi *m, int32_t *n) { return bpe_num_tokens(m->sh[0], n); }
+
+int multi_add_sample(bpe_multi *m, const int32_t *ids, int64_t n) {
+    if (m->distributed) return bpe_add_sample(m->sh.back(), ids, n);   // (corpus order kept)
+    for (int64_t i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= BPE_MAX_VOCAB)
+            return bpe_fail(BPE_ERR_ARG, "bpe native: token id out of range in sample");
+    int32_t mx = -1;
+    for (int64_t i = 0; i < n; ++i) mx = std::max(mx, ids[i]);
+    int32_t nt = 0;
+    MTRY(bpe_num_tokens(m->sh[0], &nt));
+    for (int32_t id = nt; id <= mx; ++id) MTRY(multi_set_token_len16(m, id, 1));
+    m->staged.emplace_back(ids, ids + n);
+    return BPE_OK;
+}
+
+int multi_add_latin1(bpe_multi *m, const uint8_t *bytes, int64_t n, int64_t sample_bytes,
+                     int32_t char_to_id[256], int32_t *n_tokens_io, int64_t char_hist[256]) {
+    const int32_t nt0 = *n_tokens_io;
+    if (m->distributed || !m->staged.empty() || n == 0) {
+        // after other samples: all of it to the end of the corpus
+        MTRY(distribute(m));
+        MTRY(bpe_add_latin1(m->sh.back(), bytes, n, sample_bytes, char_to_id, n_tokens_io,
+                            char_hist));
+    } else {
+        // a fresh corpus: whole samples cut into n contiguous parts, in order (the char map is
+        // threaded through the parts, so ids follow the corpus-wide first appearance)
+        if (sample_bytes == 0 || sample_bytes > n) sample_bytes = n;
+        const int64_t n_smp = (n + sample_bytes - 1) / sample_bytes;
+        int64_t hist[256] = {0}, part[256];
+        int64_t s0 = 0;
+        for (int r = 0; r < m->n; ++r) {
+            const int64_t s1 = r == m->n - 1 ? n_smp : n_smp * (r + 1) / m->n;
+            const int64_t b0 = s0 * sample_bytes, b1 = std::min(n, s1 * sample_bytes);
+            if (b1 > b0) {
+                MTRY(bpe_add_latin1(m->sh[r], bytes + b0, b1 - b0, sample_bytes, char_to_id,
+                                    n_tokens_io, part));
+                for (int ch = 0; ch < 256; ++ch) hist[ch] += part[ch];
+            }
+            s0 = s1;
+        }
+        m->distributed = true;
+        if (char_hist) std::memcpy(char_hist, hist, sizeof hist);
+    }
+    // every shard knows every token (new ids are numbered by the vocabulary size)
+    for (int32_t id = nt0; id < *n_tokens_io; ++id) MTRY(multi_set_token_len16(m, id, 1));
+    return BPE_OK;
+}
+
+int multi_clear_corpus(bpe_multi *m) {
+    m->staged.clear();
+    m->distributed = false;
+    for (auto s : m->sh) MTRY(bpe_clear_corpus(s));
+    return BPE_OK;
+}
+
+int multi_corpus_size(bpe_multi *m, int64_t *n_samples, int64_t *n_tokens) {
+    int64_t ns = 0, nt = 0;
+    for (auto s : m->sh) {
+        int64_t a = 0, b = 0;
+        MTRY(bpe_corpus_size(s, &a, &b));
+        ns += a;
+        nt += b;
+    }
+    for (auto &s : m->staged) {
+        ns += 1;
+        nt += (int64_t)s.size();
+    }
+    if (n_samples) *n_samples = ns;
+    if (n_tokens) *n_tokens = nt;
+    return BPE_OK;
+}
+
+int multi_read_corpus(bpe_multi *m, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
+                      int64_t off_cap) {
+    MTRY(distribute(m));
+    int64_t ns = 0, nt = 0;
+    MTRY(multi_corpus_size(m, &ns, &nt));
+    if (ids_cap < nt || off_cap < ns + 1 || (nt && !ids_out) || !sample_off)
+        return bpe_fail(BPE_ERR_ARG, "bpe native: read_corpus buffers too small");
+    int64_t o = 0, k = 0;
+    sample_off[0] = 0;
+    for (auto s : m->sh) {
+        int64_t a = 0, b = 0;
+        MTRY(bpe_corpus_size(s, &a, &b));
+        std::vector<int64_t> off(a + 1);
+        MTRY(bpe_read_corpus(s, ids_out ? ids_out + o : nullptr, b, off.data(), a + 1));
+        for (int64_t i = 1; i <= a; ++i) sample_off[++k] = o + off[i];
+        o += b;
+    }
+    return BPE_OK;
+}
+
+// ---- the hot path -----------------------------------------------------------------------------------
+// findNextMerge over the shards (core.ts:247-326): the host protocol (sharded.py
+// exchange_and_select, in C++).
+int multi_find_next_merge(bpe_multi *m, int64_t max_length, int64_t min_weight, int32_t *a,
+                          int32_t *b, int64_t *w) {
+    MTRY(distribute(m));
+    for (int r = 0; r < m->n; ++r) MTRY(bpe_export_counts(m->sh[r], (uint64_t *)m->d_table[r]));
+    MTRY(all_reduce(m, m->d_table, BPE_TABLE_BINS, false));
+    // exact counts of the cold pairs whose global sketch bucket could still win (every shard
+    // decides alike whether any bucket qualifies)
+    std::map<uint32_t, uint64_t> cold;
+    bool heavy = false;
+    for (int r = 0; r < m->n; ++r) {
+        int64_t nc = 0;
+        int rc = bpe_heavy_counts(m->sh[r], (uint64_t *)m->d_table[r], max_length, m->d_keys[r],
+                                  (uint64_t *)m->d_counts[r], m->cold_cap, &nc);
+        if (rc < 0 && nc > m->cold_cap) {
+            MTRY(ensure_cold_bufs(m, nc));
+            rc = bpe_heavy_counts(m->sh[r], (uint64_t *)m->d_table[r], max_length, m->d_keys[r],
+                                  (uint64_t *)m->d_counts[r], m->cold_cap, &nc);
+        }
+        if (rc < 0) return rc;
+        if (nc < 0) continue;
+        heavy = true;
+        if (nc == 0) continue;
+        std::vector<uint32_t> k(nc);
+        std::vector<uint64_t> v(nc);
+        MHIP(hipSetDevice(m->dev[r]));
+        MHIP(hipMemcpy(k.data(), m->d_keys[r], nc * 4, hipMemcpyDeviceToHost));
+        MHIP(hipMemcpy(v.data(), m->d_counts[r], nc * 8, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < nc; ++i)
+            if (v[i]) cold[k[i]] += v[i];   // (holes: count 0)
+    }
+    int64_t n_cold = 0;
+    if (heavy && !cold.empty()) {
+        MTRY(ensure_cold_bufs(m, (int64_t)cold.size()));
+        std::vector<uint32_t> k;
+        std::vector<uint64_t> v;
+        for (auto &kv : cold) {
+            k.push_back(kv.first);
+            v.push_back(kv.second);
+        }
+        n_cold = (int64_t)k.size();
+        MHIP(hipSetDevice(m->dev[0]));
+        MHIP(hipMemcpy(m->d_keys[0], k.data(), n_cold * 4, hipMemcpyHostToDevice));
+        MHIP(hipMemcpy(m->d_counts[0], v.data(), n_cold * 8, hipMemcpyHostToDevice));
+    }
+    constexpr int64_t CAP = 4096;
+    std::vector<int32_t> cand(2 * CAP);
+    int64_t n_cand = 0, W = 0;
+    int rc = bpe_select_counts(m->sh[0], (uint64_t *)m->d_table[0], m->d_keys[0],
+                               (uint64_t *)m->d_counts[0], n_cold, max_length, min_weight,
+                               cand.data(), CAP, &n_cand, &W);
+    if (rc) return rc;   // BPE_NO_MERGE or an error
+    if (n_cand > CAP) return bpe_fail(BPE_ERR_STATE, "bpe native: more than 4096 tied pairs");
+    int64_t best = 0;
+    if (n_cand > 1) {
+        // R3: the candidate whose last counted occurrence is earliest in corpus order
+        std::vector<uint64_t> glob(n_cand, 0), last(n_cand);
+        for (int r = 0; r < m->n; ++r) {
+            MTRY(bpe_tie_positions(m->sh[r], cand.data(), n_cand, last.data()));
+            for (int64_t j = 0; j < n_cand; ++j)
+                if (last[j]) glob[j] = std::max<uint64_t>(glob[j], ((uint64_t)r << RANK_SHIFT) | last[j]);
+        }
+        uint64_t bp = ~0ull;
+        best = -1;
+        for (int64_t j = 0; j < n_cand; ++j)
+            if (glob[j] && glob[j] < bp) {
+                bp = glob[j];
+                best = j;
+            }
+        if (best < 0) return bpe_fail(BPE_ERR_STATE, "bpe native: tie pass found no occurrence");
+    }
+    *a = cand[2 * best];
+    *b = cand[2 * best + 1];
+    *w = W;
+    return BPE_OK;
+}
+
+int multi_apply_merge(bpe_multi *m, int32_t a, int32_t b, int32_t c, int64_t *replaced) {
+    MTRY(distribute(m));
+    int64_t tot = 0;
+    for (auto s : m->sh) {
+        int64_t r = 0;
+        MTRY(bpe_apply_merge(s, a, b, c, &r));
+        tot += r;
+    }
+    if (replaced) *replaced = tot;
+    return BPE_OK;
+}
+
+int multi_apply_merges(bpe_multi *m, const int32_t *abc, int64_t n, int64_t *replaced,
+                       int count_after) {
+    MTRY(distribute(m));
+    std::vector<int64_t> rep(std::max<int64_t>(n, 1));
+    if (replaced) std::fill(replaced, replaced + n, 0);
+    for (auto s : m->sh) {
+        MTRY(bpe_apply_merges(s, abc, n, rep.data(), count_after));
+        if (replaced)
+            for (int64_t i = 0; i < n; ++i) replaced[i] += rep[i];
+    }
+    return BPE_OK;
+}
+
+// mergeUntil (core.ts:365-383) over the shards: batches of the device-resident rank loop, the
+// host protocol for the iterations it hands back.
+int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
+                      int64_t max_iterations, int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    MTRY(distribute(m));
+    int64_t n = 0, batch = BPE_LOOP_BATCH;
+    std::vector<std::vector<int64_t>> abw(m->n, std::vector<int64_t>(3 * BPE_LOOP_BATCH));
+    auto put = [&](int32_t a, int32_t b, int64_t w) {
+        if (n < cap) {
+            out_abw[3 * n] = a;
+            out_abw[3 * n + 1] = b;
+            out_abw[3 * n + 2] = w;
+        }
+        ++n;
+    };
+    while (!max_iterations || n < max_iterations) {
+        int32_t nt = 0;
+        MTRY(bpe_num_tokens(m->sh[0], &nt));
+        int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)nt);
+        if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
+        int status = 2;
+        if (want > 0) {
+            for (int r = 0; r < m->n; ++r)
+                MTRY(bpe_rank_loop_begin(m->sh[r], max_length, min_weight,
+                                         (uint64_t *)m->d_table[r], (uint64_t *)m->d_tie[r], r));
+            for (int64_t i = 0; i < want; ++i) {
+                MTRY(all_reduce(m, m->d_table, BPE_TABLE_BINS, false));
+                for (auto s : m->sh) MTRY(bpe_rank_loop_select(s));
+                MTRY(all_reduce(m, m->d_tie, BPE_MAX_CAND, true));
+                for (auto s : m->sh) MTRY(bpe_rank_loop_decide(s));
+                for (auto s : m->sh) MTRY(bpe_rank_loop_count(s));
+            }
+            int64_t nd = -1;
+            for (int r = 0; r < m->n; ++r) {
+                int64_t k = 0;
+                int st = 0;
+                MTRY(bpe_rank_loop_end(m->sh[r], abw[r].data(), BPE_LOOP_BATCH, &k, &st));
+                if ((nd >= 0 && (k != nd || st != status)) ||
+                    (r > 0 && !std::equal(abw[r].begin(), abw[r].begin() + 3 * k, abw[0].begin())))
+                    return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the merges");
+                nd = k;
+                status = st;
+            }
+            for (int64_t i = 0; i < nd; ++i) put((int32_t)abw[0][3 * i], (int32_t)abw[0][3 * i + 1], abw[0][3 * i + 2]);
+            if (status == 1) break;                                        // no pair qualifies
+            if (status == 0) {
+                batch = std::min<int64_t>(BPE_LOOP_BATCH, 2 * batch);
+                continue;
+            }
+            batch = std::max<int64_t>(1, std::min<int64_t>(BPE_LOOP_BATCH, 2 * nd));
+            if (max_iterations && n >= max_iterations) break;
+        }
+        // the host protocol for this iteration (or the vocabulary limit, reported by the apply)
+        int32_t a, b;
+        int64_t w;
+        int rc = multi_find_next_merge(m, max_length, min_weight, &a, &b, &w);
+        if (rc == BPE_NO_MERGE) break;
+        if (rc) return rc;
+        MTRY(bpe_num_tokens(m->sh[0], &nt));
+        int64_t rep = 0;
+        MTRY(multi_apply_merge(m, a, b, nt, &rep));
+        if (rep != w) return bpe_fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+        put(a, b, w);
+    }
+    *n_merges = n;
+    return BPE_OK;
+}
+
+// ---- measurement -------------------------------------------------------------------------------------
+int multi_stats_enable(bpe_multi *m, int on) {
+    for (auto s : m->sh) MTRY(bpe_stats_enable(s, on));
+    return BPE_OK;
+}
+
+int multi_get_stats(bpe_multi *m, bpe_stats *out) {
+    // counters summed over the shards; times: the slowest shard's
+    bpe_stats acc;
+    std::memset(&acc, 0, sizeof acc);
+    for (auto s : m->sh) {
+        bpe_stats x;
+        MTRY(bpe_get_stats(s, &x));
+        acc.step_ms = std::max(acc.step_ms, x.step_ms);
+        acc.select_ms = std::max(acc.select_ms, x.select_ms);
+        acc.step_launches += x.step_launches;
+        acc.step_slots += x.step_slots;
+        acc.step_live += x.step_live;
+        acc.tie_passes += x.tie_passes;
+        acc.iterations = std::max(acc.iterations, x.iterations);
+        acc.live_tokens += x.live_tokens;
+        acc.compactions += x.compactions;
+        acc.exact_passes += x.exact_passes;
+        acc.step_timed = std::max(acc.step_timed, x.step_timed);
+        acc.tie_tail += x.tie_tail;
+        acc.tie_lone += x.tie_lone;
+        acc.loop_host = std::max(acc.loop_host, x.loop_host);
+        acc.fused_passes += x.fused_passes;
+    }
+    *out = acc;
+    return BPE_OK;
+}
+
+int multi_reset_stats(bpe_multi *m) {
+    for (auto s : m->sh) MTRY(bpe_reset_stats(s));
+    return BPE_OK;
+}
+
+int multi_get_stream(bpe_multi *m, void **stream) { return bpe_get_stream(m->sh[0], stream); }

@@ -106,10 +106,23 @@ class BPETokenizer {
     Object.defineProperty(this, '_pending', { value: [], writable: true, enumerable: false })
   }
 
-  /** @description the HIP engine holding the corpus (created on first use) */
+  /**
+   * @description the HIP engine holding the corpus (created on first use).  The corpus spans
+   * several GPUs when BPE_NUM_GPUS > 1 (devices 0..n-1) or BPE_DEVICES lists device indices
+   * ("0,1,2,3"); BPE_REDUCE=host exchanges the pair counts through host copies instead of RCCL
+   * (any placement, e.g. two shards on one device).  The class surface does not change.
+   */
   engine() {
     if (!this._engine) {
-      this._engine = loadNative().createEngine(0)
+      let n = loadNative()
+      let devices = null
+      if (process.env.BPE_DEVICES) devices = process.env.BPE_DEVICES.split(',').map(Number)
+      else if (+process.env.BPE_NUM_GPUS > 1) {
+        devices = []
+        for (let i = 0; i < +process.env.BPE_NUM_GPUS; i++) devices.push(i)
+      }
+      let reduce = process.env.BPE_REDUCE === 'host' ? 1 : 0
+      this._engine = devices && devices.length > 1 ? n.createEngine(0, Int32Array.from(devices), reduce) : n.createEngine(0)
       this._registered = 0
     }
     this.flushMerges()

@@ -54,6 +54,22 @@ int bpe_device_count(int *n);
 int bpe_create(bpe_ctx **out, int device);
 int bpe_destroy(bpe_ctx *ctx);
 
+/* One corpus sharded over n_shards HIP devices behind one context (the drop-in's BPE_NUM_GPUS;
+ * SURVEY.md §5, §8(e)).  devices: n_shards device indices (NULL: 0 .. n_shards-1).  Every entry
+ * point below works on it as on a single-device context, with identical results: the shards hold
+ * contiguous runs of whole samples (pairs never cross samples, core.ts:265-267), samples added
+ * before the first pass are cut into runs of about equal size, later ones go to the last shard.
+ * Per merge iteration the shards all-reduce their pair tables and tie positions:
+ *   BPE_REDUCE_RCCL — RCCL communicators over the devices (ncclCommInitAll, grouped calls on the
+ *                     shards' streams; one shard per device);
+ *   BPE_REDUCE_HOST — host copies (any placement, e.g. several shards on one device: tests).
+ * The per-shard entry points (bpe_export_counts ... bpe_rank_loop_*, bpe_recount) refuse a
+ * multi-device context. */
+#define BPE_REDUCE_RCCL 0
+#define BPE_REDUCE_HOST 1
+int bpe_create_multi(bpe_ctx **out, int n_shards, const int *devices, int reduce);
+int bpe_shard_count(bpe_ctx *ctx, int *n_shards);
+
 /* ---- vocabulary ------------------------------------------------------------------------------
  * Registers token `id` with the UTF-16 length of its chars (`token.chars.length`, used by the
  * max_length filter, core.ts:270-273).  Grows the table when id >= current size.  Called by the

@@ -18,9 +18,10 @@ def build_addon():
     subprocess.check_call(['make', '-s', '-C', ADDON_DIR])
 
 
-def run_node(script, *flags, timeout=600):
+def run_node(script, *flags, timeout=600, env=None):
     out = subprocess.run([NODE, *flags, os.path.join(ROOT, 'tests', 'js', script)],
-                         capture_output=True, text=True, timeout=timeout)
+                         capture_output=True, text=True, timeout=timeout,
+                         env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     return out.stdout
 
@@ -44,4 +45,14 @@ def test_host_logic_against_golden():
 def test_reference_spec_and_golden_through_js():
     build_addon()
     out = run_node('spec_gpu.js', '--expose-gc')
+    assert 'spec_gpu ok' in out
+
+
+@pytest.mark.gpu
+def test_reference_spec_and_golden_through_js_on_two_shards():
+    """The same spec + golden run with the corpus sharded over two shards (BPE_DEVICES=0,0 on the
+    one-GPU box, pair counts exchanged through host copies): the class surface and every result
+    are unchanged."""
+    build_addon()
+    out = run_node('spec_gpu.js', '--expose-gc', env={'BPE_DEVICES': '0,0', 'BPE_REDUCE': 'host'})
     assert 'spec_gpu ok' in out

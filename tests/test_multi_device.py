@@ -1,0 +1,138 @@
+"""One corpus sharded over several shards behind ONE context (bpe_create_multi, include/bpe.h):
+the drop-in's BPE_NUM_GPUS path.  On the one-GPU test box the shards share device 0 and exchange
+their tables through host copies (BPE_REDUCE_HOST); the RCCL exchange (one shard per device) runs
+only where several devices exist.  Every result must equal the oracle's on the whole corpus."""
+import random
+
+import numpy as np
+import pytest
+
+from bpe_amd import MODES, pkg
+from golden_util import load_small
+from oracle import Corpus, OracleState
+from test_gpu_parity import random_corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def multi_engine(samples, len16, n_shards, mode_devices=None):
+    e = pkg.Engine(devices=mode_devices or [0] * n_shards, reduce='host')
+    for i, l in enumerate(len16):
+        e.set_token_len16(i, l)
+    for s in samples:
+        e.add_sample(s)
+    return e
+
+
+def run(e, opts, mode, n_tokens):
+    if mode == 'loop':
+        return e.merge_until(opts.get('max_length') or 0, opts.get('min_weight') or 0,
+                             opts.get('max_iterations') or 0)
+    out = []
+    it = 1
+    while not opts.get('max_iterations') or it <= opts['max_iterations']:
+        m = e.find_next_merge(opts.get('max_length') or 0, opts.get('min_weight') or 0)
+        if m is None:
+            break
+        assert e.apply_merge(m[0], m[1], n_tokens) == m[2]
+        n_tokens += 1
+        out.append(m)
+        it += 1
+    return out
+
+
+@pytest.mark.parametrize('mode', MODES)
+@pytest.mark.parametrize('seed', range(8))
+def test_sharded_context_vs_oracle(seed, mode):
+    """Random corpora (runs, cold ids >= 256, ties, max_length / min_weight) over 2-4 shards:
+    merges and final corpus equal the oracle's on the unsharded corpus."""
+    rng = random.Random(500 + seed)
+    alphabet = rng.choice([3, 20, 256, 300])
+    samples = random_corpus(rng, rng.choice([20000, 400000]), alphabet, rng.choice([0.0, 0.3]),
+                            rng.choice([5, 17, 60]))
+    len16 = [rng.choice([1, 1, 2]) for _ in range(alphabet)]
+    opts = {'max_iterations': rng.choice([25, 60]), 'max_length': rng.choice([0, 0, 4]),
+            'min_weight': rng.choice([0, 2, 3])}
+    ids = np.concatenate(samples)
+    off = np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64)
+    st = OracleState(ids, off, len16, alphabet)
+    want = st.merge_until(opts['max_length'], opts['min_weight'], opts['max_iterations'])
+    e = multi_engine(samples, len16, rng.choice([2, 3, 4]))
+    got = run(e, opts, mode, alphabet)
+    assert got == want
+    assert e.samples() == st.samples()
+    e.close()
+
+
+def test_golden_cases_over_two_shards():
+    """The reference-generated golden cases (tests/golden/small_cases.json) through a 2-shard
+    context: merges and final corpus."""
+    bad = []
+    for case in load_small()[::3]:
+        c = Corpus()
+        for s in case['samples']:
+            c.add(s)
+        e = multi_engine(c.samples, c.len16, 2)
+        o = case['opts']
+        got = run(e, o, 'loop', len(c.chars))
+        if [list(m) for m in got] != case['merges'] or e.samples() != case['final_ids']:
+            bad.append(case['name'])
+        e.close()
+    assert not bad, bad[:10]
+
+
+def test_latin1_ingest_is_split_in_corpus_order():
+    """Bulk ingest over 3 shards: whole samples in order, corpus-wide first-appearance ids, the
+    same merges as one context."""
+    data = pkg.synth_latin1(6 << 20, seed=7, A=200, base=40)
+    one = pkg.Engine(0)
+    cm1, nt1, h1 = one.add_latin1(data, sample_bytes=1 << 20)
+    multi = pkg.Engine(devices=[0, 0, 0], reduce='host')
+    assert multi.shard_count() == 3
+    cm3, nt3, h3 = multi.add_latin1(data, sample_bytes=1 << 20)
+    assert nt1 == nt3 and np.array_equal(cm1, cm3) and np.array_equal(h1, h3)
+    assert multi.corpus_size() == one.corpus_size()
+    a, oa = one.read_corpus()
+    b, ob = multi.read_corpus()
+    assert np.array_equal(a, b) and np.array_equal(oa, ob)
+    assert multi.merge_until(0, 2, 150) == one.merge_until(0, 2, 150)
+    a, _ = one.read_corpus()
+    b, _ = multi.read_corpus()
+    assert np.array_equal(a, b)
+
+
+def test_samples_added_after_merging_go_to_the_last_shard():
+    rng = random.Random(9)
+    V = 30
+    first = [np.array([rng.randrange(V) for _ in range(rng.randint(0, 4000))], np.int32)
+             for _ in range(7)]
+    later = [np.array([rng.randrange(V) for _ in range(3000)], np.int32) for _ in range(2)]
+    e = multi_engine(first, [1] * V, 3)
+    m1 = e.merge_until(0, 2, 10)
+    for s in later:
+        e.add_sample(s)
+    m2 = e.merge_until(0, 2, 10)
+    st = OracleState(np.concatenate(first), np.concatenate([[0], np.cumsum([len(s) for s in first])]),
+                     [1] * V, V)
+    assert m1 == st.merge_until(0, 2, 10)
+    ids = np.concatenate([st.ids] + later)
+    off = np.concatenate([st.off, st.off[-1] + np.cumsum([len(s) for s in later])])
+    st2 = OracleState(ids, off, list(st.len16[:st.n_tokens]), st.n_tokens)
+    assert m2 == st2.merge_until(0, 2, 10)
+    assert e.samples() == st2.samples()
+
+
+def test_per_shard_entry_points_refuse_a_multi_context():
+    e = pkg.Engine(devices=[0, 0], reduce='host')
+    with pytest.raises(pkg.BpeError, match='multi-device'):
+        e.recount()
+
+
+@pytest.mark.skipif(pkg.device_count() < 2, reason='RCCL exchange needs two devices')
+def test_rccl_exchange_over_two_devices():
+    data = pkg.synth_latin1(8 << 20, seed=12345, A=256)
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    two = pkg.Engine(devices=[0, 1], reduce='rccl')
+    two.add_latin1(data, sample_bytes=1 << 20)
+    assert two.merge_until(0, 2, 300) == one.merge_until(0, 2, 300)
