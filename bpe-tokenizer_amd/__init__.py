@@ -131,6 +131,8 @@ def lib():
                               ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
+        if not hasattr(L, name):   # (an older experimental build: BPE_LIB)
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

@@ -134,6 +134,8 @@ struct bpe_ctx {
     std::vector<hipEvent_t> ev_pool;
     // device-resident mergeUntil loop: control block + merge log (pinned host mirrors)
     LoopCtl *d_ctl = nullptr, *h_ctl = nullptr;
+    long long *d_count = nullptr;   // per-token occurrence counts (maintained-table loop)
+    int64_t count_cap = 0;
     long long *d_log = nullptr, *h_log = nullptr;
     // apply-only replay: per-merge replacement counts
     unsigned long long *d_repl = nullptr, *h_repl = nullptr;
@@ -252,7 +254,7 @@ int cold_clear(bpe_ctx *c) {
     return BPE_OK;
 }
 
-int ensure_cold(bpe_ctx *c, uint64_t extra) {
+int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     uint64_t s = extra;
     for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
     uint64_t need = 2 * s + 16;
@@ -260,7 +262,7 @@ int ensure_cold(bpe_ctx *c, uint64_t extra) {
     need = std::min<uint64_t>(need, V * V);
     need = std::min<uint64_t>(need, (uint64_t)c->n_live + 16);
     uint64_t cap = 1024;
-    while (cap < 2 * need) cap <<= 1;
+    while (cap < 2 * need || cap < min_cap) cap <<= 1;
     if (cap <= c->cold_cap) return BPE_OK;
     if (cap > (1ull << 31)) return fail(BPE_ERR_OOM, "bpe native: cold pair table too large");
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -503,17 +505,24 @@ int exact_pass(bpe_ctx *c) {
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     geometry(c);
     hipStream_t s = c->stream;
-    if ((rc = cold_clear(c))) return rc;
-    k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
-        c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
-        c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
-    k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy, nullptr);
-    HIP_TRY(hipGetLastError());
     uint32_t flags[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    for (int attempt = 0;; ++attempt) {
+        if ((rc = cold_clear(c))) return rc;
+        k_step<NO_MERGE, MODE_EXACT><<<c->G, WG, 0, s>>>(
+            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials,
+            c->d_spill, c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+        k_runs<MODE_EXACT><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                              c->d_spill, c->cold, c->d_heavy,
+                                                              nullptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!flags[1]) break;
+        // the distinct pairs fit by construction; claims that lost a race (holes) did not:
+        // a table twice as large, and the pass again
+        if (attempt == 2) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+        if ((rc = ensure_cold(c, 0, 2 * c->cold_cap))) return rc;
+    }
     c->cold_used = flags[0];
     if (c->stats_on) c->stats.exact_passes += 1;
     return BPE_OK;
@@ -542,6 +551,7 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
             HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
         }
         c->best_ready = false;
+        HIP_TRY(hipMemsetAsync(&c->d_res->cold_dead, 0, sizeof(unsigned long long), s));
         k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res);
         k_collect<<<COLD_GRID, 256, 0, s>>>(table, c->cold, c->d_len16, max_length, c->d_res,
                                             c->d_cand);
@@ -562,8 +572,10 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
             c->exact_streak = 1;
             return SELECT_RETRY;
         }
-        if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3) {
-            // too full to probe well: this selection still reads it, the next one rebuilds it
+        if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3 ||
+            2 * c->h_res->cold_dead > (flags & 0xFFFFFFFFu) + 65536) {
+            // too full to probe well, or mostly claims whose pair is gone (every scan streams
+            // them): this selection still reads it, the next one rebuilds it
             c->cold_exact = false;
             c->exact_streak = 1;
         }
@@ -755,6 +767,9 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
 // Up to n mergeUntil iterations with the decisions kept on the device (core.ts:367-384): per
 // iteration k_select_multi, k_decide, [k_tie, k_decide] and the pass (k_step_loop, k_runs,
 // k_reduce_table), every kernel reading the merge from the LoopCtl, and one host sync at the end.
+// With a maintained cold table (skewed corpora) the selection is k_argmax_cold + k_collect over
+// that table and the pass is the fused one (k_cold_invalidate, k_step_loop<MODE_FUSED>,
+// k_runs<MODE_FUSED>), as in the host path.
 // The merges go to out_abw[3 * i ...]; *status is the LoopStatus the batch ended with (LOOP_RUN:
 // all n done; LOOP_HOST: the next iteration needs the host path).  The host tables are brought up
 // to date from the log.
@@ -763,13 +778,27 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     int rc;
     *n_done = 0;
     *status = LOOP_DONE;
-    c->cold_exact = false;   // (its merges do not refresh a maintained cold table)
     if ((rc = settle(c))) return rc;
     c->opt_max_length = max_length;
-    if (!table_ok(c) || !c->carry_valid)
+    const bool maint = c->cold_exact && c->counts_valid && c->carry_valid &&
+                       !getenv("BPE_DEBUG_NO_FUSED");
+    if (!maint) c->cold_exact = false;
+    if (!maint && (!table_ok(c) || !c->carry_valid))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     const int64_t base = (int64_t)c->h_len16.size();
     if ((rc = ensure_len16_cap(c, base + n))) return rc;
+    if (maint) {
+        // this corpus's token counts, for the refresh fit check of each decision
+        if (c->count_cap < c->cap_vocab) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            dfree(c->d_count);
+            c->d_count = nullptr;
+            if ((rc = dev_alloc(&c->d_count, c->cap_vocab))) return rc;
+            c->count_cap = c->cap_vocab;
+        }
+        HIP_TRY(hipMemcpyAsync(c->d_count, c->h_count.data(), base * sizeof(long long),
+                               hipMemcpyHostToDevice, c->stream));
+    }
     // the device table must be exact below `base`: k_decide extends it
     if (c->len16_lo < base) {
         HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
@@ -793,6 +822,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     h->w = -1;
     h->min_weight = min_weight;
     h->max_id = BPE_MAX_VOCAB;
+    h->maintained = maint ? 1 : 0;
+    h->cold_cap = c->cold_cap;
     HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
     TieArgs A;
     memset(&A, 0, sizeof A);
@@ -809,23 +840,47 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         // a few microseconds, about 3% of an iteration with all six
         c->span_mute = (c->span_tick++ % SPAN_EVERY) != 0;
         hipEvent_t e_sel = span_begin(c);
-        k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res,
-                                                        c->d_cand, c->d_heavy, c->d_ctl);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
+        long long *cnt = maint ? c->d_count : nullptr;
+        if (maint) {
+            k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res,
+                                                    c->d_ctl);
+            k_collect<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length,
+                                                c->d_res, c->d_cand, c->d_ctl);
+        } else {
+            k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length,
+                                                            c->d_res, c->d_cand, c->d_heavy,
+                                                            c->d_ctl);
+        }
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr,
+                                  cnt);
         k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr,
+                                  cnt);
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
-        k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
-                                        c->d_partials, c->d_spill, c->cold, c->d_sums,
-                                        &c->d_res->replaced);
+        if (maint) {
+            k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, c->d_ctl);
+            k_step_loop<MODE_FUSED><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                        c->d_carry, c->d_ctl, c->d_partials,
+                                                        c->d_spill, c->cold, c->d_sums,
+                                                        &c->d_res->replaced);
+        } else {
+            k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
+                                            c->d_ctl, c->d_partials, c->d_spill, c->cold,
+                                            c->d_sums, &c->d_res->replaced);
+        }
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_step, 0))) return rc;
         hipEvent_t e_red = span_begin(c);
-        k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
-                                                              c->d_spill, c->cold, c->d_heavy,
-                                                              c->d_ctl);
+        if (maint)
+            k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                  c->d_spill, c->cold, c->d_heavy,
+                                                                  c->d_ctl);
+        else
+            k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                  c->d_spill, c->cold, c->d_heavy,
+                                                                  c->d_ctl);
         k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
             c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, max_length, c->d_res, c->d_ctl);
         HIP_TRY(hipGetLastError());
@@ -872,6 +927,11 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         out_abw[3 * i + 2] = W;
     }
     c->len16_lo = base + nd;   // k_decide wrote the new lengths on the device
+    if (maint) {
+        c->cold_used = c->h_res->cold_flags & 0xFFFFFFFFu;   // (as of the last selection)
+        if (nd) c->sketch_valid = false;                     // (fused passes)
+        if (c->stats_on) c->stats.fused_passes += nd;
+    }
     if (c->stats_on) {
         c->stats.tie_passes += h->n_tie;
         c->stats.tie_tail += h->n_tail;
@@ -882,7 +942,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     // every early-ended batch leaves the last reduce's best key in the Result
     c->best_ready = true;
     c->best_ml = max_length;
-    c->counts_valid = c->carry_valid = c->sketch_valid = true;
+    c->counts_valid = c->carry_valid = true;
+    if (!maint) c->sketch_valid = true;
     *n_done = nd;
     *status = h->status;
     return BPE_OK;
@@ -1272,7 +1333,7 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
-                    c->d_ctl, c->d_log, c->d_repl};
+                    c->d_ctl, c->d_log, c->d_repl, c->d_count};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
@@ -1576,7 +1637,6 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             --rest;
             want = 0;
         }
-        if (c->cold_exact) want = 0;   // (the maintained cold table is refreshed by the host path)
         if (want > 0) {
             int64_t nd = 0;
             int st = LOOP_DONE;

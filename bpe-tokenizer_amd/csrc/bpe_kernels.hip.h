@@ -128,6 +128,7 @@ struct Result {
     unsigned long long last[MAX_CAND];   // R3: slot + 1 of the last counted occurrence
     unsigned long long replaced;         // apply: replacement count
     unsigned long long cold_flags;       // k_argmax_cold: (overflow << 32) | n_used of the cold table
+    unsigned long long cold_dead;        // k_argmax_cold: claims whose pair is gone (count 0, key set)
 };
 
 // Device-resident mergeUntil loop (core.ts:367-384): the decision of each iteration stays in HBM and
@@ -151,6 +152,11 @@ struct LoopCtl {
     int32_t n_tail;       // ties decided from the tail window alone (k_tie tail mode)
     int32_t n_lone;       // ... of which by the lone candidate missing from the window
     int32_t n_host;       // iterations handed to the host path (LOOP_HOST: 0 or 1 per batch)
+    // the maintained cold-pair table (skewed corpora): selection reads it instead of the sketch,
+    // each merge pass refreshes it (MODE_FUSED); cold_cap = its capacity (for the fill limits)
+    int32_t maintained;
+    int32_t pad_;
+    unsigned long long cold_cap;
 };
 
 // Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
@@ -239,6 +245,9 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, unsi
     atomicOr(ct.overflow, 1u);
 }
 
+// entries per thread and sweep of the cold-table scans (their loads in flight together)
+constexpr int COLD_ILP = 8;
+
 __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
     return ((uint32_t)x << 16) | (uint32_t)y;
 }
@@ -270,7 +279,8 @@ __device__ __forceinline__ int table_index(int32_t x, int32_t y) {
 // Where a pass's pair occurrences go.  MODE_TABLE: the per-workgroup LDS table (exact hot bins +
 // cold sketch buckets, 16-bit counters) with a global u64 spill.  MODE_EXACT: exact counts of the
 // cold pairs whose sketch bucket is marked heavy, into the sparse table; the rest is ignored.
-// MODE_FUSED: the table (sketch folded) plus the cold pairs with a side in {ma, mb, mc}.
+// MODE_FUSED: the hot bins (no sketch: the maintained cold table counts the cold pairs) plus the
+// cold pairs with a side in {ma, mb, mc}.
 struct Sink {
     uint32_t *hist;                  // LDS table (MODE_TABLE)
     unsigned long long *spill;       // global u64 [TABLE_BINS]
@@ -328,15 +338,9 @@ __device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | (
 
 // The same from the pair, as two instructions (the compiler otherwise re-associates the mask and
 // the shift into three, for lack of a second literal operand)
-template <bool FUSED = false>
 __device__ __forceinline__ uint32_t cold_addr_of(int32_t x, int32_t y) {
     uint32_t b, a;
-    // MODE_FUSED folds the sketch into its lower half (the maintained cold table makes the sketch
-    // unused; the upper half holds the refresh's LDS hash)
-    if (FUSED)
-        asm("v_bfe_u32 %0, %1, 0, 12" : "=v"(b) : "v"(sketch_hash(x, y)));
-    else
-        asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
+    asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
     asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(a) : "v"(b), "s"(HOT_BYTES));
     return a;
 }
@@ -383,11 +387,12 @@ __device__ __forceinline__ void lds_cold_add(const Sink &k, uint32_t key, uint32
     cold_add(k.ct, key, inc);
 }
 
-// MODE_FUSED's LDS hash: the upper half of the sketch dwords, (key, count) x 2048.
-constexpr int FH_BITS = 11;
+// MODE_FUSED's LDS hash: all of the sketch dwords (the sketch is not kept while the cold table is
+// maintained), (key, count) x 4096.
+constexpr int FH_BITS = 12;
 constexpr int FH_SLOTS = 1 << FH_BITS;
-constexpr int FH_BASE = HOT_BINS / 2 + 2 * FH_SLOTS;   // dword index of the first key
-static_assert(FH_BASE + 2 * FH_SLOTS == HIST_WORDS, "fused LDS hash = upper half of the sketch");
+constexpr int FH_BASE = HOT_BINS / 2;   // dword index of the first key
+static_assert(FH_BASE + 2 * FH_SLOTS == HIST_WORDS, "fused LDS hash = the sketch's dwords");
 
 __device__ __forceinline__ void lds_fused_add(const Sink &k, uint32_t key, uint32_t inc) {
     uint32_t *keys = k.hist + FH_BASE;
@@ -411,16 +416,18 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) 
     if (MODE == MODE_NONE) return;
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         uint32_t addr, inc, bin;
-        if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) {
+        const bool hot = ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT;
+        if (hot) {
             addr = hot_addr(x, y);
             inc = hot_inc(x);
             bin = hot_bin((uint32_t)x, (uint32_t)y);
         } else {
-            addr = cold_addr(MODE == MODE_FUSED ? sketch_hash(x, y) & 0xFFFu : sketch_hash(x, y));
+            addr = cold_addr(sketch_hash(x, y));
             inc = hot_inc(x);
             bin = HOT_BINS + sketch_bucket(x, y);
         }
-        lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
+        // (MODE_FUSED keeps no sketch: its cold pairs go to the maintained table only)
+        if (MODE == MODE_TABLE || hot) lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
         if (MODE == MODE_FUSED && exact_wanted<MODE>(k, x, y)) lds_fused_add(k, pair_key(x, y), 1u);
     } else if (exact_wanted<MODE>(k, x, y)) {
         lds_cold_add(k, pair_key(x, y), 1u);
@@ -719,13 +726,20 @@ struct Tally {
 // opaque to the compiler so both uses below read it as is), the class select (two), and the
 // increment (three): hot_inc(x) for a valid pair, 0 when a side is negative (SEP, dead), with the
 // validity bit (u's sign) as the value shifted.  Pairs with a cold side go to their sketch bucket.
+// FUSED (the maintained cold table counts the cold pairs): a cold pair adds 0 to a hot dword (its
+// address masked into the hot table) instead of going to the sketch.
 template <bool FUSED = false>
 __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, uint32_t &inc) {
     uint32_t u = ~((uint32_t)x | (uint32_t)y);
     asm("" : "+v"(u));
     const uint32_t hot = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
-    addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of<FUSED>(x, y));   // both ids < 256
-    inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
+    if (FUSED) {
+        addr = hot & (HOT_BYTES - 4);
+        inc = (uint32_t)(u >= 0xFFFFFF00u) << (((uint32_t)x << 4) & 31u);   // both ids < 256
+    } else {
+        addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of(x, y));   // both ids < 256
+        inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
+    }
 }
 
 // The LDS adds of a fast-path chunk; their returned words go to o (the overflow screen runs a
@@ -1214,13 +1228,17 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         const uint4 *h4 = reinterpret_cast<const uint4 *>(hist);
         for (int i = threadIdx.x; i < HIST_WORDS / 4; i += WG) out[i] = h4[i];
         if (MODE == MODE_FUSED)   // (the slab's sketch dwords are then garbage: unused)
-            for (int i = threadIdx.x; i < FH_SLOTS; i += WG) {
+            for (int j = threadIdx.x; j < FH_SLOTS; j += WG) {
+                // (each workgroup starts its flush elsewhere: workgroups adding one new key at
+                // the same moment each reserve a dense index, and all but one become holes)
+                const int i = (j + (int)blockIdx.x * 97 * 64) & (FH_SLOTS - 1);
                 const uint32_t key = hist[FH_BASE + i];
                 if (key != EMPTY) cold_add(ct, key, hist[FH_BASE + FH_SLOTS + i]);
             }
     } else if (MODE == MODE_EXACT) {
         __syncthreads();
-        for (int i = threadIdx.x; i < LH_SLOTS; i += WG) {
+        for (int j = threadIdx.x; j < LH_SLOTS; j += WG) {
+            const int i = (j + (int)blockIdx.x * 97 * 64) & (LH_SLOTS - 1);   // (as above)
             const uint32_t key = hist[HEAVY_WORDS + i];
             if (key != EMPTY) cold_add(ct, key, hist[HEAVY_WORDS + LH_SLOTS + i]);
         }
@@ -1252,6 +1270,8 @@ k_apply(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
 }
 
 // The device loop's pass: the merge to apply is the one k_decide left in the LoopCtl.
+// MODE_FUSED: the maintained cold table's refresh rides along (k_cold_invalidate ran before).
+template <int MODE = MODE_TABLE>
 __global__ void __launch_bounds__(WG)
 k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             const RegionCarry *__restrict__ carry, const LoopCtl *__restrict__ ctl,
@@ -1261,11 +1281,11 @@ k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     if (ctl->status != LOOP_RUN) return;
     const int32_t ma = ctl->a, mb = ctl->b, mc = ctl->c;
     if (ma == mb)
-        step_body<MERGE_XX, MODE_TABLE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
-                                        spill, ct, nullptr, sums, replaced);
+        step_body<MERGE_XX, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
+                                  ct, nullptr, sums, replaced);
     else
-        step_body<MERGE_XY, MODE_TABLE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
-                                        spill, ct, nullptr, sums, replaced);
+        step_body<MERGE_XY, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
+                                  ct, nullptr, sums, replaced);
 }
 
 __device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
@@ -1292,6 +1312,11 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
                        int32_t mb = -1, int32_t mc = -1) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R || loop_off(ctl)) return;
+    if (MODE == MODE_FUSED && ctl) {   // (device loop: the merge this pass applied)
+        ma = ctl->a;
+        mb = ctl->b;
+        mc = ctl->c;
+    }
     Sink k;
     k.hist = nullptr;
     k.spill = spill;
@@ -1468,29 +1493,53 @@ __global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
 }
 
 // argmax over the claimed cold slots (dense view, coalesced).
+// Also counts the claims whose pair is gone (res->cold_dead, zero on entry: a real key whose count a
+// merge zeroed and no pass counted again): they stay in the dense view, and every scan streams
+// them, until the table is rebuilt.  (Holes, key EMPTY, are claims that lost a race.)
 __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, int64_t max_length,
-                              Result *res) {
+                              Result *res, const LoopCtl *ctl = nullptr) {
     __shared__ unsigned long long s_best[4];
+    __shared__ unsigned s_live;
+    if (loop_off(ctl)) return;
     const uint32_t n = *ct.n_used;
     if (blockIdx.x == 0 && threadIdx.x == 0)   // (rides along with the Result's copy to the host)
         res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n;
+    if (threadIdx.x == 0) s_live = 0;
+    __syncthreads();
     unsigned long long best = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const unsigned long long n_ab = ct.dcounts[i];
-        if (!n_ab || n_ab < (best >> 17)) continue;   // (the key only when it can win)
-        const uint32_t key = ct.dkeys[i];
-        const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        if (!pair_ok(a, b, len16, max_length)) continue;
-        const unsigned long long k = pack_key(n_ab, a, b);
-        best = k > best ? k : best;
+    unsigned dead = 0;
+    // COLD_ILP entries per thread and sweep, their loads issued together (one dependent load per
+    // thread at a time left the scan latency-bound at about a third of the stream rate)
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += COLD_ILP * stride) {
+        unsigned long long v[COLD_ILP];
+        uint32_t kk[COLD_ILP];
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const uint32_t i = i0 + q * stride;
+            v[q] = i < n ? ct.dcounts[i] : 0ull;
+            kk[q] = i < n ? ct.dkeys[i] : EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const unsigned long long n_ab = v[q];
+            dead += (n_ab == 0) & (kk[q] != EMPTY);
+            const int32_t a = (int32_t)(kk[q] >> 16), b = (int32_t)(kk[q] & 0xFFFFu);
+            if (n_ab && pair_ok(a, b, len16, max_length)) {
+                const unsigned long long k = pack_key(n_ab, a, b);
+                best = k > best ? k : best;
+            }
+        }
     }
     // one atomic per workgroup (a wave each would queue thousands on one address)
     best = wave_max_u64(best);
     if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+    if (dead) atomicAdd(&s_live, dead);
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = s_best[w] > best ? s_best[w] : best;
         if (best) atomicMax(&res->best, best);
+        if (s_live) atomicAdd(&res->cold_dead, (unsigned long long)s_live);
     }
 }
 
@@ -1580,13 +1629,32 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
 // candidates), or decides.  phase 1, after k_tie: the candidate whose last counted occurrence is
 // earliest (rule R3).  A decision logs (a, b, W), registers the new token's UTF-16 length
 // (core.ts:318) and clears the Result for the next pass.  One thread.
+//
+// With a maintained cold table (ctl->maintained) the selection read that table, not the sketch:
+// the batch hands over to the host when the table overflowed, is 3/4 full, is more than half dead
+// claims (it is then rebuilt), or when the refresh of the chosen merge might not fit (2 claims
+// per replacement at most).  count: this corpus's per-token occurrence counts, kept up to date
+// here with W (the host reads them back at the batch end).
 __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
-                         long long *log, int phase, const unsigned long long *__restrict__ tie_pos) {
+                         long long *log, int phase, const unsigned long long *__restrict__ tie_pos,
+                         long long *__restrict__ count = nullptr) {
     if (threadIdx.x != 0 || ctl->status != LOOP_RUN) return;
     const unsigned long long best = res->best;
     const long long W = (long long)(best >> 17);
     const unsigned n = res->n_cand;
     int32_t a = -1, b = -1;
+    auto to_host = [&]() {
+        ctl->status = LOOP_HOST;
+        ctl->n_host += 1;
+    };
+    // room in the maintained table for the refresh of the merge: every pair the merge creates
+    // has the new token c as a side, and c occurs W times, so it claims at most 2 W new slots
+    auto room = [&]() -> bool {
+        if (!ctl->maintained) return true;
+        const unsigned long long V = (unsigned long long)ctl->next_id + 1;
+        const unsigned long long claims = 2 * (unsigned long long)W < V * V ? 2 * W : V * V;
+        return (res->cold_flags & 0xFFFFFFFFull) + claims + 64 <= ctl->cold_cap / 4 * 3;
+    };
     if (phase == 0) {
         if (ctl->w >= 0) {
             // the previous merge's replacement count: == W on the whole corpus, logged per shard
@@ -1597,11 +1665,17 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
             log[LOG_WORDS * (ctl->n_done - 1) + 3] = (long long)res->replaced;
         }
         ctl->w = -1;
-        // a heavy sketch bucket may hold a cold pair above the best hot one (even when no hot
-        // pair exists at all): only the host path's exact counts can tell
-        if (res->n_heavy) {
-            ctl->status = LOOP_HOST;
-            ctl->n_host += 1;
+        if (ctl->maintained) {
+            const unsigned long long used = res->cold_flags & 0xFFFFFFFFull;
+            if ((res->cold_flags >> 32) || used * 4 > ctl->cold_cap * 3 ||
+                2 * res->cold_dead > used + 65536) {
+                to_host();
+                return;
+            }
+        } else if (res->n_heavy) {
+            // a heavy sketch bucket may hold a cold pair above the best hot one (even when no
+            // hot pair exists at all): only the host path's exact counts can tell
+            to_host();
             return;
         }
         if (best == 0 || W < ctl->min_weight) {                   // core.ts:312-313
@@ -1632,6 +1706,10 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
         }
         a = cand[0].x;
         b = cand[0].y;
+        if (!room()) {
+            to_host();
+            return;
+        }
     } else {
         if (!ctl->tie) return;
         unsigned long long bp = ~0ull;
@@ -1665,6 +1743,10 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
             ctl->status = LOOP_ERROR;
             return;
         }
+        if (!room()) {
+            to_host();
+            return;
+        }
         ctl->tie = 0;
     }
     const int32_t c = ctl->next_id;
@@ -1680,10 +1762,16 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
     ctl->w = W;
     ctl->next_id = c + 1;
     ctl->n_done = i + 1;
+    if (count) {   // (replacements == W exactly on one corpus)
+        count[a] -= W;
+        count[b] -= W;
+        count[c] = W;
+    }
     res->best = 0;
     res->n_cand = 0;
     res->n_heavy = 0;
     res->replaced = 0;
+    res->cold_dead = 0;
 }
 
 __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, int32_t b) {
@@ -1694,7 +1782,8 @@ __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, in
 // Collects every pair whose packed key equals the best (same W and same a+b).
 __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, ColdTable ct,
                           const int32_t *__restrict__ len16, int64_t max_length, Result *res,
-                          int2 *cand) {
+                          int2 *cand, const LoopCtl *ctl = nullptr) {
+    if (loop_off(ctl)) return;
     const unsigned long long best = res->best;
     if (best == 0) return;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1705,12 +1794,22 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
     }
     const uint32_t n = *ct.n_used;
     const unsigned long long w = best >> 17;
-    for (uint32_t i = tid; i < n; i += gridDim.x * blockDim.x) {
-        if (ct.dcounts[i] != w) continue;   // (dense view; the key only for count matches)
-        const uint32_t key = ct.dkeys[i];
-        const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
-        if (pair_ok(a, b, len16, max_length) && pack_key(w, a, b) == best)
-            push_cand(res, cand, a, b);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = tid; i0 < n; i0 += COLD_ILP * stride) {
+        unsigned long long v[COLD_ILP];   // (loads issued together, as in k_argmax_cold)
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const uint32_t i = i0 + q * stride;
+            v[q] = i < n ? ct.dcounts[i] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            if (v[q] != w) continue;   // (dense view; the key only for count matches)
+            const uint32_t key = ct.dkeys[i0 + q * stride];
+            const int32_t a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFFu);
+            if (pair_ok(a, b, len16, max_length) && pack_key(w, a, b) == best)
+                push_cand(res, cand, a, b);
+        }
     }
 }
 
@@ -1763,12 +1862,28 @@ __global__ void k_collect_list(const unsigned long long *__restrict__ hot,
 // The maintained cold table before its refresh after the merge (a, b) -> c: the pairs with a side
 // a or b lose their count (the refresh pass counts them again on the merged corpus; every other
 // pair's count is unchanged by the merge).
-__global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b) {
+// (device loop: the merge the next pass applies, from the LoopCtl)
+__global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b, const LoopCtl *ctl = nullptr) {
+    if (loop_off(ctl)) return;
+    if (ctl) {
+        a = ctl->a;
+        b = ctl->b;
+    }
     const uint32_t n = *ct.n_used;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t key = ct.dkeys[i];
-        const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-        if ((x == a) | (x == b) | (y == a) | (y == b)) ct.dcounts[i] = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += COLD_ILP * stride) {
+        uint32_t kk[COLD_ILP];   // (loads issued together, as in k_argmax_cold)
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const uint32_t i = i0 + q * stride;
+            kk[q] = i < n ? ct.dkeys[i] : EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const int32_t x = (int32_t)(kk[q] >> 16), y = (int32_t)(kk[q] & 0xFFFFu);
+            if ((kk[q] != EMPTY) & ((x == a) | (x == b) | (y == a) | (y == b)))
+                ct.dcounts[i0 + q * stride] = 0;
+        }
     }
 }
 

@@ -50,3 +50,5 @@ if has js; then
   timeout -k 10 300 python3 tools/loop_bench.py 64 1000 5 > "$OUT/bench_py64.json"
   cat "$OUT/bench_py64.json"
 fi
+# keep the merged-back output small (the raw per-dispatch CSVs are tens of MB)
+find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete

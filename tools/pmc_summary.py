@@ -17,7 +17,7 @@ import sys
 
 # the merge pass, the dominant kernel of the bench: the device loop's pass, or (host-driven
 # iterations) k_step<MERGE_XY>
-KERNELS = ('bpe::k_step_loop', 'k_step<1, 0>')
+KERNELS = ('k_step_loop<0>', 'bpe::k_step_loop', 'k_step<1, 0>')
 
 
 def per_launch(path, counter):
@@ -33,7 +33,8 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     fetch, n_f = per_launch(os.path.join(src, 'fetch'), 'FETCH_SIZE')
     write, n_w = per_launch(os.path.join(src, 'write'), 'WRITE_SIZE')
-    KERNEL = next((k for k in KERNELS if k in fetch), KERNELS[0])
+    want = (sys.argv[3],) if len(sys.argv) > 3 else KERNELS   # (a kernel named on the command line)
+    KERNEL = next((k for k in want if k in fetch), want[0])
     out = {'source': src, 'kernel': KERNEL}
     if KERNEL in fetch:
         out['fetch_bytes_per_launch'] = 2 * fetch[KERNEL] * 1024      # KiB, x2 (gfx950 wide reads)
