@@ -113,6 +113,10 @@ struct bpe_ctx {
     // passes (a corpus whose winners are pairs of merged tokens, e.g. Zipf words)
     bool cold_exact = false;
     int exact_streak = 0;
+    // with the cold table maintained, merge passes count incrementally (MODE_INCR: the hot bins are
+    // maintained too, and a pass counts only the pairs the merge can change); BPE_FUSED=1 keeps
+    // the full hot recount with the cold refresh riding along (MODE_FUSED) instead
+    bool use_incr = true;
     bool carry_valid = false;    // d_sums / d_carry describe the current corpus and geometry
     int64_t cpr = 0;
     int R = 0, G = 0;
@@ -366,7 +370,18 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     hipEvent_t e_step = span_begin(c);
-    if (merge && fused && a == b)
+    const bool incr = merge && fused && c->use_incr;
+    if (incr) {
+        k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, a, b);
+        if (a == b)
+            k_step<MERGE_XX, MODE_INCR><<<c->G, WG, 0, s>>>(
+                c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials,
+                c->d_spill, c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced, c->d_hot);
+        else
+            k_step<MERGE_XY, MODE_INCR><<<c->G, WG, 0, s>>>(
+                c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials,
+                c->d_spill, c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced, c->d_hot);
+    } else if (merge && fused && a == b)
         k_step<MERGE_XX, MODE_FUSED><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
@@ -389,15 +404,26 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     HIP_TRY(hipGetLastError());
     if ((rc = span_end(c, e_step, 0))) return rc;
     hipEvent_t e_red = span_begin(c);
-    if (merge && fused)
-        k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(
-            c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr, a, b, cc);
-    else
-        k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(
-            c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr);
-    k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
-        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res,
-        nullptr);
+    if (incr) {
+        // the touched pairs into the maintained tables, then the best hot key
+        k_runs<MODE_INCR><<<(c->R + 255) / 256, 256, 0, s>>>(
+            c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr, a, b, cc,
+            c->d_hot);
+        k_reduce_rows<<<4 * INCR_RLIM / 2 / RR_COLS, 256, 0, s>>>(
+            c->d_partials, c->G, c->d_spill, c->d_hot, c->cold, a, b, cc);
+        k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, c->opt_max_length,
+                                                    c->d_res);
+    } else {
+        if (merge && fused)
+            k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(
+                c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr, a, b, cc);
+        else
+            k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(
+                c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr);
+        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+            c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res,
+            nullptr);
+    }
     HIP_TRY(hipGetLastError());
     if ((rc = span_end(c, e_red, 1))) return rc;
     c->best_ready = true;
@@ -759,7 +785,7 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
             c->exact_streak = 1;   // (the next exact pass rebuilds the whole table)
         }
     }
-    if (fused) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
+    if (fused && !c->use_incr) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
     if ((rc = run_pass(c, true, a, b, cc, replaced, fused))) return rc;
     return BPE_OK;
 }
@@ -859,7 +885,13 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
-        if (maint) {
+        if (maint && c->use_incr) {
+            k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl);
+            k_step_loop<MODE_INCR><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                       c->d_carry, c->d_ctl, c->d_partials,
+                                                       c->d_spill, c->cold, c->d_sums,
+                                                       &c->d_res->replaced, c->d_hot);
+        } else if (maint) {
             k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, c->d_ctl);
             k_step_loop<MODE_FUSED><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
                                                         c->d_carry, c->d_ctl, c->d_partials,
@@ -873,16 +905,27 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_step, 0))) return rc;
         hipEvent_t e_red = span_begin(c);
-        if (maint)
-            k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
-                                                                  c->d_spill, c->cold, c->d_heavy,
-                                                                  c->d_ctl);
-        else
-            k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
-                                                                  c->d_spill, c->cold, c->d_heavy,
-                                                                  c->d_ctl);
-        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
-            c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, max_length, c->d_res, c->d_ctl);
+        if (maint && c->use_incr) {
+            k_runs<MODE_INCR><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                 c->d_spill, c->cold, c->d_heavy,
+                                                                 c->d_ctl, -1, -1, -1, c->d_hot);
+            k_reduce_rows<<<4 * INCR_RLIM / 2 / RR_COLS, 256, 0, s>>>(
+                c->d_partials, c->G, c->d_spill, c->d_hot, c->cold, -1, -1, -1, c->d_ctl);
+            k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res,
+                                                        c->d_ctl);
+        } else {
+            if (maint)
+                k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                      c->d_spill, c->cold,
+                                                                      c->d_heavy, c->d_ctl);
+            else
+                k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                                      c->d_spill, c->cold,
+                                                                      c->d_heavy, c->d_ctl);
+            k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+                c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, max_length, c->d_res,
+                c->d_ctl);
+        }
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_red, 1))) return rc;
     }
@@ -1258,6 +1301,7 @@ int bpe_create(bpe_ctx **out, int device) {
     if (device < 0 || device >= n) return fail(BPE_ERR_ARG, "bpe native: bad device index");
     bpe_ctx *c = new bpe_ctx();
     c->device = device;
+    c->use_incr = !getenv("BPE_FUSED");
     int rc;
     auto bail = [&](int code) {
         bpe_destroy(c);

@@ -80,7 +80,11 @@ constexpr int HEAVY_WORDS = SKETCH_BINS / 32;        // bitmap of sketch buckets
 // pairs in heavy sketch buckets, or nothing (apply-only replay: restoreMerge, batch encoding).
 // MODE_FUSED: a merge pass that also refreshes the maintained cold table (the table counts plus
 // MODE_EXACT's refresh of the pairs with a side in {ma, mb, mc}, in one stream of the corpus)
-enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1, MODE_NONE = 2, MODE_FUSED = 3 };
+// MODE_INCR: incremental counts.  Both tables are maintained: the merge
+// (ma, mb) -> mc changes only the counts of the pairs with a side in {ma, mb, mc} (every other pair
+// keeps its occurrences and its run parity), so those are zeroed before the pass and the pass
+// counts only them, into dense per-token LDS rows (no 128 KiB histogram of every pair).
+enum CountMode { MODE_TABLE = 0, MODE_EXACT = 1, MODE_NONE = 2, MODE_FUSED = 3, MODE_INCR = 4 };
 constexpr int MAX_CAND = 16;                // candidates resolved per tie pass
 constexpr int CAND_CAP = 65536;             // candidates collected per iteration
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -289,6 +293,10 @@ struct Sink {
     // MODE_FUSED (ma >= 0): the maintained cold table's refresh after the merge (ma, mb) -> mc,
     // every cold pair with a side in {ma, mb, mc}, whatever its bucket (heavy is then unused)
     int32_t ma, mb, mc;
+    // MODE_INCR: the maintained hot table (global u64 [HOT_BINS]) and the rows' spill
+    // (global u64 [4 * INCR_RLIM])
+    unsigned long long *hot;
+    unsigned long long *rspill;
 };
 
 template <int MODE>
@@ -301,11 +309,30 @@ __device__ __forceinline__ bool exact_wanted(const Sink &k, int32_t x, int32_t y
     return (k.heavy[b >> 5] >> (b & 31)) & 1u;
 }
 
+// MODE_INCR: is (x, y) a valid pair with a side in {ma, mb, mc}?
+__device__ __forceinline__ bool incr_touched(const Sink &k, int32_t x, int32_t y) {
+    return ((x | y) >= 0) & ((x == k.ma) | (x == k.mb) | (x == k.mc) | (y == k.ma) | (y == k.mb) |
+                             (y == k.mc));
+}
+
+// MODE_INCR: n occurrences of a touched pair straight into the maintained tables.
+__device__ __forceinline__ void incr_global_add(const Sink &k, int32_t x, int32_t y,
+                                                unsigned long long n) {
+    if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT)
+        atomicAdd(&k.hot[hot_bin((uint32_t)x, (uint32_t)y)], n);
+    else
+        cold_add(k.ct, ((uint32_t)x << 16) | (uint32_t)y, n);
+}
+
 // Adds n occurrences of (x, y) from outside the LDS table (boundary pairs, resolved runs).
 template <int MODE>
 __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32_t y,
                                                  unsigned long long n) {
     if (n == 0 || MODE == MODE_NONE) return;
+    if (MODE == MODE_INCR) {
+        if (incr_touched(k, x, y)) incr_global_add(k, x, y, n);
+        return;
+    }
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) atomicAdd(&k.spill[table_index(x, y)], n);
     if (MODE != MODE_TABLE && exact_wanted<MODE>(k, x, y))
         cold_add(k.ct, pair_key(x, y), n);
@@ -410,10 +437,78 @@ __device__ __forceinline__ void lds_fused_add(const Sink &k, uint32_t key, uint3
     cold_add(k.ct, key, inc);
 }
 
+// MODE_INCR's LDS: four rows of 16-bit counters indexed by the pair's other token, for the pairs
+// (ma, y), (mb, y), (x, ma), (x, mb) in this order of precedence (each pair counts once), the
+// other token below INCR_RLIM; then a hash of (key, count) dwords for everything else touched
+// (the pairs of mc, and other tokens >= INCR_RLIM).  A counter reaching 0x8000 spills 0x8000 to the
+// global rspill row (one lane sees each transition, as in the hot table).
+constexpr int INCR_RLIM = 18432;                       // counters per row
+constexpr int IH_SLOTS = 2048;
+constexpr int IH_BASE = 4 * INCR_RLIM / 2;             // dword index of the hash keys
+static_assert(IH_BASE + 2 * IH_SLOTS == HIST_WORDS, "MODE_INCR LDS layout");
+
+// counters of a row in use: other tokens below the vocabulary size after the merge (mc + 1)
+__device__ __forceinline__ int incr_vlim(int32_t mc) {
+    const int v = (mc + 2) & ~1;
+    return v < INCR_RLIM ? v : INCR_RLIM;
+}
+
+__device__ __forceinline__ void incr_hash_add(const Sink &k, uint32_t key, uint32_t inc) {
+    uint32_t *keys = k.hist + IH_BASE;
+    uint32_t *cnt = keys + IH_SLOTS;
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - 11);
+    for (int p = 0; p < LH_PROBES; ++p) {
+        uint32_t kk = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kk == EMPTY) kk = atomicCAS(&keys[h], EMPTY, key);
+        if (kk == EMPTY || kk == key) {
+            atomicAdd(&cnt[h], inc);
+            return;
+        }
+        h = (h + 1) & (IH_SLOTS - 1);
+    }
+    incr_global_add(k, (int32_t)(key >> 16), (int32_t)(key & 0xFFFFu), inc);
+}
+
+// One occurrence of a pair touched by the merge (incr_touched) into MODE_INCR's LDS.
+__device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y) {
+    int row, idx;
+    if (x == k.ma) {
+        row = 0;
+        idx = y;
+    } else if (x == k.mb) {
+        row = 1;
+        idx = y;
+    } else if (y == k.ma) {
+        row = 2;
+        idx = x;
+    } else if (y == k.mb) {
+        row = 3;
+        idx = x;
+    } else {
+        row = 4;
+        idx = INCR_RLIM;
+    }
+    if (idx >= INCR_RLIM) {
+        incr_hash_add(k, ((uint32_t)x << 16) | (uint32_t)y, 1u);
+        return;
+    }
+    const uint32_t c = (uint32_t)(row * INCR_RLIM + idx);
+    const uint32_t sh = (c & 1u) << 4;
+    const uint32_t old = atomicAdd(&k.hist[c >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+        atomicSub(&k.hist[c >> 1], 0x8000u << sh);
+        atomicAdd(&k.rspill[c], 0x8000ull);
+    }
+}
+
 // One counted occurrence of (x, y) (outside the streaming fast paths).
 template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
     if (MODE == MODE_NONE) return;
+    if (MODE == MODE_INCR) {
+        if (incr_touched(k, x, y)) incr_add(k, x, y);
+        return;
+    }
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         uint32_t addr, inc, bin;
         const bool hot = ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT;
@@ -891,6 +986,57 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
 #pragma unroll
             for (int e = 0; e < 4; ++e)
                 if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
+        } else if (MODE == MODE_INCR) {
+            // only the pairs with a side in {ma, mb, mc}: membership masks per slot (compares into
+            // lane masks, combined on the scalar unit), the LDS only for chunks that hold one
+            const int32_t ma = k.ma, mb = k.mb, mc = k.mc;
+            const unsigned long long M0 = __ballot((t0 == ma) | (t0 == mb) | (t0 == mc)),
+                                     M1 = __ballot((t1 == ma) | (t1 == mb) | (t1 == mc)),
+                                     M2 = __ballot((t2 == ma) | (t2 == mb) | (t2 == mc)),
+                                     M3 = __ballot((x3 == ma) | (x3 == mb) | (x3 == mc)),
+                                     M4 = __ballot((r3 == ma) | (r3 == mb) | (r3 == mc));
+            const unsigned long long Wm[4] = {M0 | M1, M1 | M2, M2 | M3, M3 | M4};
+            if ((Wm[0] | Wm[1] | Wm[2] | Wm[3]) != 0ull) {
+                // branch-free on the common route (a row counter): every lane adds, 0 when its
+                // pair is not touched (to a counter of its own: no two lanes on one address);
+                // pairs of mc, and other tokens past the rows, take the hash (rare)
+                uint32_t o[4], dw[4], sh[4];
+                unsigned long long hsh = 0, rok = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int32_t xx = x[e], yy = y[e];
+                    const bool act = lane_in(Wm[e]) & ((xx | yy) >= 0);
+                    const bool xa = xx == ma, xb = xx == mb, ya = yy == ma, yb = yy == mb;
+                    const int row = xa ? 0 : xb ? 1 : ya ? 2 : 3;
+                    const int idx = (xa | xb) ? yy : xx;
+                    const bool inrow = act & (xa | xb | ya | yb) & (idx < INCR_RLIM);
+                    const uint32_t cc = (uint32_t)(row * INCR_RLIM + idx);
+                    sh[e] = (cc & 1u) << 4;
+                    dw[e] = inrow ? (cc >> 1) : (uint32_t)lane;
+                    o[e] = atomicAdd(&k.hist[dw[e]], (uint32_t)inrow << sh[e]);
+                    rok |= (unsigned long long)inrow << e;   // (per lane: bit e)
+                    hsh |= (unsigned long long)(act & !inrow) << e;
+                }
+                // a counter that reached 0x8000: exactly one lane saw 0x7FFF (rare)
+                bool spill = false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    spill |= ((rok >> e) & 1ull) && ((o[e] >> sh[e]) & 0xFFFFu) == 0x7FFFu;
+                if (__ballot(spill) != 0ull) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (((rok >> e) & 1ull) && ((o[e] >> sh[e]) & 0xFFFFu) == 0x7FFFu) {
+                            atomicSub(&k.hist[dw[e]], 0x8000u << sh[e]);
+                            atomicAdd(&k.rspill[2 * dw[e] + (sh[e] >> 4)], 0x8000ull);
+                        }
+                }
+                if (__ballot(hsh != 0ull) != 0ull) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if ((hsh >> e) & 1ull)
+                            incr_hash_add(k, ((uint32_t)x[e] << 16) | (uint32_t)y[e], 1u);
+                }
+            }
         }
         // the last token starts its run here (a run continuing into the next chunk would be a run
         // of three, or a partial chunk's X X end), so its offset parity is 0
@@ -1080,7 +1226,10 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                                           unsigned long long *__restrict__ spill, ColdTable ct,
                                           const uint32_t *__restrict__ heavy_g,
                                           RegionSum *__restrict__ sums,
-                                          unsigned long long *__restrict__ replaced) {
+                                          unsigned long long *__restrict__ replaced,
+                                          unsigned long long *__restrict__ hot_g = nullptr) {
+    // (MODE_INCR: `spill` holds the rows' spill, 4 * INCR_RLIM u64; hot_g the maintained table)
+    unsigned long long *rspill = spill;
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         // (MODE_FUSED: the LDS hash's keys start EMPTY; one store per dword, so no two threads
         // write the same dword before the barrier)
@@ -1096,6 +1245,15 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             hist[HEAVY_WORDS + i] = EMPTY;
             hist[HEAVY_WORDS + LH_SLOTS + i] = 0;
         }
+    } else if (MODE == MODE_INCR) {
+        // the rows' used part (other tokens < min(vocabulary, INCR_RLIM)) and the hash
+        const int vl = incr_vlim(mc);
+        for (int r = 0; r < 4; ++r)
+            for (int i = threadIdx.x; i < vl / 2; i += WG) hist[r * (INCR_RLIM / 2) + i] = 0;
+        for (int i = threadIdx.x; i < IH_SLOTS; i += WG) {
+            hist[IH_BASE + i] = EMPTY;
+            hist[IH_BASE + IH_SLOTS + i] = 0;
+        }
     }
     if (MODE != MODE_NONE) __syncthreads();
     Sink k;
@@ -1103,9 +1261,11 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.spill = spill;
     k.ct = ct;
     k.heavy = hist;
-    k.ma = MODE == MODE_FUSED ? ma : -1;
+    k.ma = MODE == MODE_FUSED || MODE == MODE_INCR ? ma : -1;
     k.mb = mb;
     k.mc = mc;
+    k.hot = hot_g;
+    k.rspill = rspill;
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6)));
     if (r < R) {
@@ -1235,6 +1395,22 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 const uint32_t key = hist[FH_BASE + i];
                 if (key != EMPTY) cold_add(ct, key, hist[FH_BASE + FH_SLOTS + i]);
             }
+    } else if (MODE == MODE_INCR) {
+        // the rows' used part to this workgroup's slab (k_reduce_rows sums the slabs), the hash's
+        // keys straight into the maintained tables
+        __syncthreads();
+        const int vl = incr_vlim(mc);
+        uint32_t *out = partials + (size_t)blockIdx.x * HIST_WORDS;
+        for (int r = 0; r < 4; ++r)
+            for (int i = threadIdx.x; i < vl / 2; i += WG)
+                out[r * (INCR_RLIM / 2) + i] = hist[r * (INCR_RLIM / 2) + i];
+        for (int j = threadIdx.x; j < IH_SLOTS; j += WG) {
+            const int i = (j + (int)blockIdx.x * 97 * 64) & (IH_SLOTS - 1);
+            const uint32_t key = hist[IH_BASE + i];
+            if (key != EMPTY)
+                incr_global_add(k, (int32_t)(key >> 16), (int32_t)(key & 0xFFFFu),
+                                hist[IH_BASE + IH_SLOTS + i]);
+        }
     } else if (MODE == MODE_EXACT) {
         __syncthreads();
         for (int j = threadIdx.x; j < LH_SLOTS; j += WG) {
@@ -1251,10 +1427,10 @@ k_step(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
        const RegionCarry *__restrict__ carry, int32_t ma, int32_t mb, int32_t mc,
        uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
        const uint32_t *__restrict__ heavy_g, RegionSum *__restrict__ sums,
-       unsigned long long *__restrict__ replaced) {
+       unsigned long long *__restrict__ replaced, unsigned long long *__restrict__ hot_g = nullptr) {
     __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
     step_body<MERGE, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill, ct,
-                           heavy_g, sums, replaced);
+                           heavy_g, sums, replaced, hot_g);
 }
 
 // Apply-only pass (restoreMerge replay, batch encoding, core.ts:477-494 / 392-409): the merge is
@@ -1276,16 +1452,17 @@ __global__ void __launch_bounds__(WG)
 k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             const RegionCarry *__restrict__ carry, const LoopCtl *__restrict__ ctl,
             uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
-            RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced) {
+            RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced,
+            unsigned long long *__restrict__ hot_g = nullptr) {
     __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
     if (ctl->status != LOOP_RUN) return;
     const int32_t ma = ctl->a, mb = ctl->b, mc = ctl->c;
     if (ma == mb)
         step_body<MERGE_XX, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
-                                  ct, nullptr, sums, replaced);
+                                  ct, nullptr, sums, replaced, hot_g);
     else
         step_body<MERGE_XY, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
-                                  ct, nullptr, sums, replaced);
+                                  ct, nullptr, sums, replaced, hot_g);
 }
 
 __device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
@@ -1309,10 +1486,10 @@ template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
                        unsigned long long *__restrict__ spill, ColdTable ct,
                        const uint32_t *__restrict__ heavy, const LoopCtl *ctl, int32_t ma = -1,
-                       int32_t mb = -1, int32_t mc = -1) {
+                       int32_t mb = -1, int32_t mc = -1, unsigned long long *hot = nullptr) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R || loop_off(ctl)) return;
-    if (MODE == MODE_FUSED && ctl) {   // (device loop: the merge this pass applied)
+    if ((MODE == MODE_FUSED || MODE == MODE_INCR) && ctl) {   // (device loop: the merge applied)
         ma = ctl->a;
         mb = ctl->b;
         mc = ctl->c;
@@ -1322,9 +1499,11 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.spill = spill;
     k.ct = ct;
     k.heavy = heavy;
-    k.ma = MODE == MODE_FUSED ? ma : -1;
+    k.ma = MODE == MODE_FUSED || MODE == MODE_INCR ? ma : -1;
     k.mb = mb;
     k.mc = mc;
+    k.hot = hot;
+    k.rspill = nullptr;
     const int p = prev_nonempty(s, r - 1);
     const int nx = next_nonempty(s, r + 1, R);
     RegionCarry rc;
@@ -1479,17 +1658,27 @@ __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len
     return !max_length || (int64_t)len16[a] + len16[b] <= max_length;
 }
 
-// argmax over the dense hot table: best = max packed key.
-__global__ void k_argmax_hot(const unsigned long long *__restrict__ hot_counts,
-                             const int32_t *__restrict__ len16, int64_t max_length, Result *res,
-                             const LoopCtl *ctl = nullptr) {
+// argmax over the dense hot table: best = max packed key.  One atomic per block of 256 (an atomic
+// per wave queued a thousand on one address: 12 us per launch).
+__global__ void __launch_bounds__(256)
+k_argmax_hot(const unsigned long long *__restrict__ hot_counts, const int32_t *__restrict__ len16,
+             int64_t max_length, Result *res, const LoopCtl *ctl = nullptr) {
+    __shared__ unsigned long long s_best[4];
     if (loop_off(ctl)) return;
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long k = 0;
-    if (bin < HOT_BINS && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
-        k = pack_key(hot_counts[bin], bin_a(bin), bin_b(bin));
+    for (int bin = blockIdx.x * blockDim.x + threadIdx.x; bin < HOT_BINS;
+         bin += gridDim.x * blockDim.x)
+        if (pair_ok(bin_a(bin), bin_b(bin), len16, max_length)) {
+            const unsigned long long v = pack_key(hot_counts[bin], bin_a(bin), bin_b(bin));
+            k = v > k ? v : k;
+        }
     k = wave_max_u64(k);
-    if ((threadIdx.x & 63) == 0 && k) atomicMax(&res->best, k);
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) k = s_best[w] > k ? s_best[w] : k;
+        if (k) atomicMax(&res->best, k);
+    }
 }
 
 // argmax over the claimed cold slots (dense view, coalesced).
@@ -1887,6 +2076,102 @@ __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b, const Loop
     }
 }
 
+
+// MODE_INCR before the pass of the merge (a, b) -> c: every pair with a side a or b loses its
+// count, in the maintained hot table (rows and columns a, b) and in the cold table.
+__global__ void k_incr_invalidate(ColdTable ct, unsigned long long *__restrict__ hot, int32_t a,
+                                  int32_t b, const LoopCtl *ctl = nullptr) {
+    if (loop_off(ctl)) return;
+    if (ctl) {
+        a = ctl->a;
+        b = ctl->b;
+    }
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 4 * HOT) {   // hot bin (x, y) = y * 256 + x: column x = a / b, row y = a / b
+        const int32_t m = (t >> 8) & 1 ? b : a, o = t & 255;
+        if (m < HOT) hot[(t >> 9) ? hot_bin((uint32_t)m, (uint32_t)o) : hot_bin((uint32_t)o, (uint32_t)m)] = 0;
+    }
+    const uint32_t n = *ct.n_used;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = t; i0 < n; i0 += COLD_ILP * stride) {
+        uint32_t kk[COLD_ILP];
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const uint32_t i = i0 + q * stride;
+            kk[q] = i < n ? ct.dkeys[i] : EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const int32_t x = (int32_t)(kk[q] >> 16), y = (int32_t)(kk[q] & 0xFFFFu);
+            if ((kk[q] != EMPTY) & ((x == a) | (x == b) | (y == a) | (y == b)))
+                ct.dcounts[i0 + q * stride] = 0;
+        }
+    }
+}
+
+// MODE_INCR after the pass: sums the G slabs' rows (+ their spill, zeroed here) and adds each
+// nonzero count to its pair in the maintained tables.  A block owns 32 row dwords (64 counters):
+// its 8 lane groups each sum every 8th slab, eight loads in flight, then combine in LDS.
+constexpr int RR_COLS = 32;
+__global__ void __launch_bounds__(256)
+k_reduce_rows(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ rspill,
+              unsigned long long *__restrict__ hot, ColdTable ct, int32_t a, int32_t b, int32_t c,
+              const LoopCtl *ctl = nullptr) {
+    __shared__ uint32_t s_lo[8][RR_COLS], s_hi[8][RR_COLS];
+    if (loop_off(ctl)) return;
+    if (ctl) {
+        a = ctl->a;
+        b = ctl->b;
+        c = ctl->c;
+    }
+    const int vl = incr_vlim(c);
+    const int d0 = blockIdx.x * RR_COLS;   // first of the block's dwords (4 rows x INCR_RLIM / 2)
+    const int row = d0 / (INCR_RLIM / 2);
+    if (row >= 4 || 2 * (d0 % (INCR_RLIM / 2)) >= vl || (a == b && (row & 1))) return;
+    const int col = threadIdx.x & (RR_COLS - 1), grp = threadIdx.x / RR_COLS;
+    uint32_t lo = 0, hi = 0;
+    const uint32_t *p = partials + d0 + col;
+    int g = grp;
+    for (; g + 56 < G; g += 64) {
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = p[(size_t)(g + 8 * q) * HIST_WORDS];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            lo += v[q] & 0xFFFFu;
+            hi += v[q] >> 16;
+        }
+    }
+    for (; g < G; g += 8) {
+        const uint32_t v = p[(size_t)g * HIST_WORDS];
+        lo += v & 0xFFFFu;
+        hi += v >> 16;
+    }
+    s_lo[grp][col] = lo;
+    s_hi[grp][col] = hi;
+    __syncthreads();
+    if (grp != 0) return;
+    for (int q = 1; q < 8; ++q) {
+        lo += s_lo[q][col];
+        hi += s_hi[q][col];
+    }
+    const int wi = (d0 + col) % (INCR_RLIM / 2);
+    if (2 * wi >= vl) return;
+    const int32_t m = (row & 1) ? b : a;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int idx = 2 * wi + h;
+        const uint32_t ci = (uint32_t)(row * INCR_RLIM + idx);
+        const unsigned long long n = (unsigned long long)(h ? hi : lo) + rspill[ci];
+        rspill[ci] = 0;
+        if (!n) continue;
+        const int32_t x = row < 2 ? m : idx, y = row < 2 ? idx : m;
+        Sink k;
+        k.hot = hot;
+        k.ct = ct;
+        incr_global_add(k, x, y, n);
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // K3 tie pass (rule R3): last counted occurrence (slot + 1) of up to MAX_CAND tied pairs on the

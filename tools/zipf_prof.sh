@@ -16,7 +16,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
     -d "$OUT/sq2" -o run --output-format csv -- python3 $PMC > "$OUT/sq2.log" 2>&1
 python3 tools/sq_loop_summary.py "$OUT" > "$OUT/sq_summary.txt"
-python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_step_loop<3>" > /dev/null
-grep -A20 "k_step_loop<3>" "$OUT/sq_summary.txt" | head -24
+python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_step_loop<4>" > /dev/null
+grep -A20 "k_step_loop<4>" "$OUT/sq_summary.txt" | head -24
 # keep the merged-back output small (the raw per-dispatch CSVs are tens of MB)
 find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete
