@@ -157,9 +157,10 @@ def main():
         # this same command (tools/gpu_round.sh -> tools/pmc_summary.py; counters cannot be read
         # from inside the timed run)
         traffic = {}
-        tpath = os.path.join(ROOT, 'profiles', 'current_pmc.json')
-        if os.path.exists(tpath) and args.corpus == 'uniform':
-            # (the committed passes were taken on the uniform C3 run: no traffic for other corpora)
+        tpath = os.path.join(ROOT, 'profiles', 'current_pmc.json' if args.corpus == 'uniform'
+                             else 'current_pmc_%s.json' % args.corpus)
+        if os.path.exists(tpath):
+            # (each corpus has its own committed passes: tools/gpu_round2.sh, tools/zipf_prof.sh)
             traffic = json.load(open(tpath))
         # (the device loop times every 8th iteration: step_ms and select_ms cover step_timed passes)
         k1_ms = st['step_ms'] / max(1, st['step_timed'])
@@ -193,7 +194,10 @@ def main():
             },
             'roofline': {
                 'bound': 'hbm',
-                'kernel': 'k_step (fused K4 apply + K1 pair count, one pass per merge)',
+                'kernel': ('k_step (fused K4 apply + K1 pair count, one pass per merge)'
+                           if args.corpus == 'uniform' else
+                           'k_step (fused K4 apply + K1 pair count; in the maintained state '
+                           'k_step_loop<MODE_INCR>: apply + recount of the pairs touching the merge)'),
                 'achieved': achieved,
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',

@@ -17,6 +17,6 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_AC
     -d "$OUT/sq2" -o run --output-format csv -- python3 $PMC > "$OUT/sq2.log" 2>&1
 python3 tools/sq_loop_summary.py "$OUT" > "$OUT/sq_summary.txt"
 python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_step_loop<4>" > /dev/null
-grep -A20 "k_step_loop<4>" "$OUT/sq_summary.txt" | head -24
 # keep the merged-back output small (the raw per-dispatch CSVs are tens of MB)
 find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete
+cat "$OUT/sq_summary.txt"
