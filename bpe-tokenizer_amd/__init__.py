@@ -29,7 +29,8 @@ C_API = [
     'bpe_version', 'bpe_last_error', 'bpe_device_count', 'bpe_create', 'bpe_destroy',
     'bpe_create_multi', 'bpe_shard_count',
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
-    'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_find_next_merge',
+    'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_sample_lengths',
+    'bpe_read_samples', 'bpe_find_next_merge',
     'bpe_apply_merge', 'bpe_apply_merges', 'bpe_merge_until', 'bpe_stats_enable', 'bpe_get_stats', 'bpe_reset_stats',
     'bpe_get_stream', 'bpe_synth_latin1', 'bpe_synth_zipf', 'bpe_recount', 'bpe_export_counts',
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions', 'bpe_rank_loop_begin',
@@ -100,6 +101,8 @@ def lib():
         'bpe_clear_corpus': ([vp], ctypes.c_int),
         'bpe_corpus_size': ([vp, i64p, i64p], ctypes.c_int),
         'bpe_read_corpus': ([vp, i32p, ctypes.c_int64, i64p, ctypes.c_int64], ctypes.c_int),
+        'bpe_sample_lengths': ([vp, i64p, ctypes.c_int64], ctypes.c_int),
+        'bpe_read_samples': ([vp, i64p, ctypes.c_int64, i32p, ctypes.c_int64, i64p], ctypes.c_int),
         'bpe_find_next_merge': ([vp, ctypes.c_int64, ctypes.c_int64, i32p, i32p, i64p],
                                 ctypes.c_int),
         'bpe_apply_merge': ([vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i64p],
@@ -253,6 +256,27 @@ class Engine:
                                      ids.size, off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                      off.size), 'bpe_read_corpus')
         return ids[:nt], off
+
+    def sample_lengths(self):
+        """Live tokens per sample (int64), from the device-side sample index."""
+        ns, _ = self.corpus_size()
+        lens = np.zeros(max(ns, 1), np.int64)
+        _check(lib().bpe_sample_lengths(self._ctx, lens.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                        lens.size), 'bpe_sample_lengths')
+        return lens[:ns]
+
+    def read_samples(self, idx):
+        """The listed samples' ids: (flat ids int32, offsets int64), in the order of idx."""
+        idx = np.ascontiguousarray(idx, np.int64)
+        lens = self.sample_lengths()
+        need = int(lens[idx].sum()) if idx.size else 0
+        ids = np.zeros(max(need, 1), np.int32)
+        off = np.zeros(idx.size + 1, np.int64)
+        _check(lib().bpe_read_samples(self._ctx, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                      idx.size, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                      ids.size, off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               'bpe_read_samples')
+        return ids[:need], off
 
     def samples(self):
         ids, off = self.read_corpus()

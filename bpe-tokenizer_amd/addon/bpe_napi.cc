@@ -197,6 +197,70 @@ napi_value ReadCorpus(napi_env env, napi_callback_info info) {
     return out;
 }
 
+// sampleLengths(h) -> Float64Array: live tokens per sample (bpe_sample_lengths; the db twin's
+// changed-row test, db/core.ts:399-413)
+napi_value SampleLengths(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "sampleLengths(h)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    int64_t ns = 0;
+    if (bpe_corpus_size(ctx, &ns, nullptr) < 0) return throw_native(env, "bpe_corpus_size");
+    std::vector<int64_t> lens(std::max<int64_t>(ns, 1));
+    if (bpe_sample_lengths(ctx, lens.data(), (int64_t)lens.size()) < 0)
+        return throw_native(env, "bpe_sample_lengths");
+    void *data = nullptr;
+    napi_value ab, out;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(ns, 1) * 8, &data, &ab);
+    double *d = static_cast<double *>(data);
+    for (int64_t i = 0; i < ns; ++i) d[i] = (double)lens[i];
+    napi_create_typedarray(env, napi_float64_array, (size_t)ns, ab, 0, &out);
+    return out;
+}
+
+// readSamples(h, Float64Array idx) -> [Int32Array ids, Float64Array offsets] of those samples, in
+// that order (bpe_read_samples; the db twin's row write-back, db/core.ts:414-417)
+napi_value ReadSamples(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_arg(env, "readSamples(h, Float64Array)");
+    bpe_ctx *ctx = get_ctx(env, argv[0]);
+    napi_typedarray_type type;
+    size_t n = 0, o = 0;
+    void *data = nullptr;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[1], &type, &n, &data, &ab, &o) != napi_ok ||
+        type != napi_float64_array)
+        return throw_arg(env, "readSamples expects a Float64Array of sample indices");
+    std::vector<int64_t> idx(n);
+    for (size_t k = 0; k < n; ++k) idx[k] = (int64_t) static_cast<const double *>(data)[k];
+    int64_t ns = 0;
+    if (bpe_corpus_size(ctx, &ns, nullptr) < 0) return throw_native(env, "bpe_corpus_size");
+    std::vector<int64_t> lens(std::max<int64_t>(ns, 1));
+    if (bpe_sample_lengths(ctx, lens.data(), (int64_t)lens.size()) < 0)
+        return throw_native(env, "bpe_sample_lengths");
+    int64_t need = 0;
+    for (int64_t i : idx) {
+        if (i < 0 || i >= ns) return throw_arg(env, "readSamples: sample index out of range");
+        need += lens[i];
+    }
+    void *ids_data = nullptr, *off_data = nullptr;
+    napi_value ids_ab, off_ab, ids, offs;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(need, 1) * 4, &ids_data, &ids_ab);
+    napi_create_arraybuffer(env, (n + 1) * 8, &off_data, &off_ab);
+    std::vector<int64_t> off(n + 1);
+    if (bpe_read_samples(ctx, idx.data(), (int64_t)n, static_cast<int32_t *>(ids_data),
+                         std::max<int64_t>(need, 1), off.data()) < 0)
+        return throw_native(env, "bpe_read_samples");
+    double *od = static_cast<double *>(off_data);
+    for (size_t k = 0; k <= n; ++k) od[k] = (double)off[k];
+    napi_create_typedarray(env, napi_int32_array, (size_t)need, ids_ab, 0, &ids);
+    napi_create_typedarray(env, napi_float64_array, n + 1, off_ab, 0, &offs);
+    napi_value out;
+    napi_create_array_with_length(env, 2, &out);
+    napi_set_element(env, out, 0, ids);
+    napi_set_element(env, out, 1, offs);
+    return out;
+}
+
 // findNextMerge(h, maxLength, minWeight) -> [a, b, W] | null   (core.ts:247-326)
 napi_value FindNextMerge(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -329,7 +393,8 @@ napi_value Init(napi_env env, napi_value exports) {
         {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},
         {"findNextMerge", FindNextMerge}, {"applyMerge", ApplyMerge},
         {"applyMerges", ApplyMerges}, {"mergeUntil", MergeUntil},
-        {"encodeMerges", EncodeMerges},
+        {"encodeMerges", EncodeMerges}, {"sampleLengths", SampleLengths},
+        {"readSamples", ReadSamples},
     };
     for (auto &f : fns) {
         napi_value fn;

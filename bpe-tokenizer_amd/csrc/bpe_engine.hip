@@ -1264,6 +1264,112 @@ int append_begin(bpe_ctx *c, int64_t extra_slots) {
 int bpe_fail(int code, const char *msg) { return fail(code, msg); }
 
 // a multi-device context forwards the call; per-shard entry points refuse it
+// Device scratch freed on scope exit (the sample index is a rare, host-facing operation).
+struct Scratch {
+    std::vector<void *> p;
+    template <typename T>
+    int get(T **out, size_t n) {
+        int rc = dev_alloc(out, n);
+        if (!rc) p.push_back(*out);
+        return rc;
+    }
+    ~Scratch() {
+        for (void *q : p) dfree(q);
+    }
+};
+
+// Where every sample ends: slot_end[i] = the slot of sample i's terminator, live_end[i] = the
+// live tokens of samples 0..i.  Two reads of the corpus (k_census, k_sep_emit), one host sync.
+int sample_ends(bpe_ctx *c, std::vector<int64_t> &slot_end, std::vector<int64_t> &live_end) {
+    int rc;
+    if ((rc = settle(c))) return rc;
+    const int64_t ns = c->n_samples;
+    slot_end.assign(ns, 0);
+    live_end.assign(ns, 0);
+    if (!ns) return BPE_OK;
+    geometry(c);
+    Scratch t;
+    int64_t *d_live, *d_seps, *d_slot, *d_lend;
+    if ((rc = t.get(&d_live, c->R)) || (rc = t.get(&d_seps, c->R)) || (rc = t.get(&d_slot, ns)) ||
+        (rc = t.get(&d_lend, ns)))
+        return rc;
+    hipStream_t s = c->stream;
+    const int blocks = (c->R + 3) / 4;
+    k_census<<<blocks, 256, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, d_live, d_seps);
+    k_scan_pair<<<1, 1024, 0, s>>>(c->R, d_live, d_seps);
+    k_sep_emit<<<blocks, 256, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, d_live, d_seps, ns,
+                                      d_slot, d_lend);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(slot_end.data(), d_slot, ns * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(live_end.data(), d_lend, ns * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (live_end[ns - 1] != c->n_live)
+        return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch (sample index)");
+    return BPE_OK;
+}
+
+int sample_lengths(bpe_ctx *c, int64_t *lens, int64_t cap) {
+    if (cap < c->n_samples || (c->n_samples && !lens))
+        return fail(BPE_ERR_ARG, "bpe native: sample_lengths buffer too small");
+    std::vector<int64_t> se, le;
+    int rc = sample_ends(c, se, le);
+    if (rc) return rc;
+    for (int64_t i = 0; i < c->n_samples; ++i) lens[i] = le[i] - (i ? le[i - 1] : 0);
+    return BPE_OK;
+}
+
+// Live ids of samples idx[0..n), packed in that order: one gather of their slot ranges on the
+// device, one copy back, the dead slots dropped on the host.
+int read_samples(bpe_ctx *c, const int64_t *idx, int64_t n, int32_t *ids_out, int64_t ids_cap,
+                 int64_t *off) {
+    if (n < 0 || (n && !idx) || !off) return fail(BPE_ERR_ARG, "bpe native: bad read_samples arguments");
+    off[0] = 0;
+    if (!n) return BPE_OK;
+    std::vector<int64_t> se, le;
+    int rc = sample_ends(c, se, le);
+    if (rc) return rc;
+    std::vector<int64_t> src(n), len(n), dst(n + 1);
+    int64_t need = 0;
+    dst[0] = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t i = idx[k];
+        if (i < 0 || i >= c->n_samples) return fail(BPE_ERR_ARG, "bpe native: sample index out of range");
+        src[k] = i ? se[i - 1] + 1 : 0;
+        len[k] = se[i] - src[k];
+        dst[k + 1] = dst[k] + len[k];
+        need += le[i] - (i ? le[i - 1] : 0);
+    }
+    if (ids_cap < need || (need && !ids_out))
+        return fail(BPE_ERR_ARG, "bpe native: read_samples buffer too small");
+    const int64_t total = dst[n];
+    std::vector<int32_t> buf(total);
+    if (total) {
+        Scratch t;
+        int64_t *d_src, *d_len, *d_dst;
+        int32_t *d_out;
+        if ((rc = t.get(&d_src, n)) || (rc = t.get(&d_len, n)) || (rc = t.get(&d_dst, n)) ||
+            (rc = t.get(&d_out, total)))
+            return rc;
+        hipStream_t s = c->stream;
+        HIP_TRY(hipMemcpyAsync(d_src, src.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_len, len.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_dst, dst.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        k_gather_ranges<<<(unsigned)std::min<int64_t>(n, 1 << 16), 256, 0, s>>>(c->d_ids, d_src, d_len,
+                                                                                d_dst, n, d_out);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(buf.data(), d_out, total * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    int64_t o = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        for (int64_t j = dst[k]; j < dst[k + 1]; ++j)
+            if (buf[j] >= 0) ids_out[o++] = buf[j];
+        off[k + 1] = o;
+    }
+    if (o != need) return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch (read_samples)");
+    return BPE_OK;
+}
+
 #define MULTI(call) \
     if (c && c->multi) return multi_##call
 #define NOT_MULTI                                                                          \
@@ -1585,6 +1691,23 @@ int bpe_read_corpus(bpe_ctx *c, int32_t *ids_out, int64_t ids_cap, int64_t *samp
     if (sidx != c->n_samples || o != c->n_live)
         return fail(BPE_ERR_STATE, "bpe native: corpus layout mismatch");
     return BPE_OK;
+}
+
+int bpe_sample_lengths(bpe_ctx *c, int64_t *lens, int64_t cap) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    MULTI(sample_lengths(c->multi, lens, cap));
+    int rc = set_device(c);
+    if (rc) return rc;
+    return sample_lengths(c, lens, cap);
+}
+
+int bpe_read_samples(bpe_ctx *c, const int64_t *idx, int64_t n, int32_t *ids_out, int64_t ids_cap,
+                     int64_t *sample_off) {
+    if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
+    MULTI(read_samples(c->multi, idx, n, ids_out, ids_cap, sample_off));
+    int rc = set_device(c);
+    if (rc) return rc;
+    return read_samples(c, idx, n, ids_out, ids_cap, sample_off);
 }
 
 int bpe_find_next_merge(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a,

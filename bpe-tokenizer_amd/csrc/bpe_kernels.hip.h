@@ -2476,6 +2476,145 @@ __global__ void __launch_bounds__(256) k_compact(const int32_t *__restrict__ ids
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Sample index: where every sample ends, for reading back single samples (the rows a merge
+// changed, db/core.ts:399-417).  One wave per region, as k_compact.  k_census counts a region's
+// live tokens and sample terminators, k_scan_pair turns both into region offsets, and k_sep_emit
+// writes, per terminator in corpus order, its slot and the live tokens before it.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_census(const int32_t *__restrict__ ids, int64_t n_chunks,
+                                                int64_t cpr, int R, int64_t *__restrict__ live,
+                                                int64_t *__restrict__ seps) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int64_t c0 = (int64_t)r * cpr;
+    const int64_t c1 = min(c0 + cpr, n_chunks);
+    const int4 *v4 = reinterpret_cast<const int4 *>(ids);
+    int64_t nl = 0, ns = 0;
+    for (int64_t c = c0; c < c1; ++c) {
+        const View w = make_view(v4[c * 64 + lane]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool in = 4 * lane + e < w.len;
+            nl += in && w.t[e] >= 0;
+            ns += in && w.t[e] == SEP;
+        }
+    }
+    nl = wave_sum64(nl);
+    ns = wave_sum64(ns);
+    if (lane == 0) {
+        live[r] = nl;
+        seps[r] = ns;
+    }
+}
+
+// Exclusive prefix sums of two arrays of R <= 1024 * k entries, in place.  One block of 1024.
+__global__ void __launch_bounds__(1024) k_scan_pair(int R, int64_t *__restrict__ a,
+                                                    int64_t *__restrict__ b) {
+    __shared__ int64_t pa[1024], pb[1024];
+    const int per = (R + 1023) / 1024;
+    const int t = threadIdx.x;
+    int64_t sa = 0, sb = 0;
+    for (int i = 0; i < per; ++i) {
+        const int r = t * per + i;
+        if (r < R) {
+            sa += a[r];
+            sb += b[r];
+        }
+    }
+    pa[t] = sa;
+    pb[t] = sb;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int64_t oa = t >= d ? pa[t - d] : 0, ob = t >= d ? pb[t - d] : 0;
+        __syncthreads();
+        pa[t] += oa;
+        pb[t] += ob;
+        __syncthreads();
+    }
+    int64_t ra = pa[t] - sa, rb = pb[t] - sb;
+    for (int i = 0; i < per; ++i) {
+        const int r = t * per + i;
+        if (r < R) {
+            const int64_t va = a[r], vb = b[r];
+            a[r] = ra;
+            b[r] = rb;
+            ra += va;
+            rb += vb;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sep_emit(const int32_t *__restrict__ ids, int64_t n_chunks,
+                                                  int64_t cpr, int R,
+                                                  const int64_t *__restrict__ live_pre,
+                                                  const int64_t *__restrict__ sep_pre,
+                                                  int64_t n_samples,
+                                                  int64_t *__restrict__ slot_end,
+                                                  int64_t *__restrict__ live_end) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int64_t c0 = (int64_t)r * cpr;
+    const int64_t c1 = min(c0 + cpr, n_chunks);
+    const int4 *v4 = reinterpret_cast<const int4 *>(ids);
+    const unsigned long long below = (1ull << lane) - 1;
+    int64_t ol = live_pre[r], os = sep_pre[r];
+    for (int64_t c = c0; c < c1; ++c) {
+        const View w = make_view(v4[c * 64 + lane]);
+        bool L[4], S[4];
+        int bl = 0, bs = 0, tl = 0, ts = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool in = 4 * lane + e < w.len;
+            L[e] = in && w.t[e] >= 0;
+            S[e] = in && w.t[e] == SEP;
+            const unsigned long long ml = __ballot(L[e]), ms = __ballot(S[e]);
+            bl += __popcll(ml & below);
+            bs += __popcll(ms & below);
+            tl += __popcll(ml);
+            ts += __popcll(ms);
+        }
+        // slots of lane l precede those of lane l+1: live tokens / terminators before (lane, e)
+        // are those of the lanes below plus this lane's slots 0..e-1
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (S[e]) {
+                const int64_t k = os + bs;
+                if (k < n_samples) {
+                    slot_end[k] = c * CHUNK + 4 * lane + e;
+                    live_end[k] = ol + bl;
+                }
+            }
+            bl += L[e];
+            bs += S[e];
+        }
+        ol += tl;
+        os += ts;
+    }
+}
+
+// Packs slot ranges [src[k], src[k] + len[k]) to dst + dst_off[k], for reading chosen samples
+// back in one copy.  One block per range.
+__global__ void __launch_bounds__(256) k_gather_ranges(const int32_t *__restrict__ ids,
+                                                       const int64_t *__restrict__ src,
+                                                       const int64_t *__restrict__ len,
+                                                       const int64_t *__restrict__ dst_off,
+                                                       int64_t n, int32_t *__restrict__ dst) {
+    for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const int32_t *s = ids + src[k];
+        int32_t *d = dst + dst_off[k];
+        for (int64_t i = threadIdx.x; i < len[k]; i += 256) d[i] = s[i];
+    }
+}
+
 // Dead tail + tail tags of the last chunk after a dense write of live_slots slots.  One block of
 // CHUNK threads.
 __global__ void __launch_bounds__(CHUNK) k_seal(int32_t *__restrict__ ids, int64_t live_slots) {

@@ -356,6 +356,69 @@ int multi_read_corpus(bpe_multi *m, int32_t *ids_out, int64_t ids_cap, int64_t *
     return BPE_OK;
 }
 
+// Per-sample lengths and sample reads: the shards hold consecutive runs of samples, so sample i
+// of the corpus is sample i - first[r] of the shard r whose run contains it.
+int multi_sample_lengths(bpe_multi *m, int64_t *lens, int64_t cap) {
+    MTRY(distribute(m));
+    int64_t ns = 0;
+    MTRY(multi_corpus_size(m, &ns, nullptr));
+    if (cap < ns || (ns && !lens)) return bpe_fail(BPE_ERR_ARG, "bpe native: sample_lengths buffer too small");
+    int64_t k = 0;
+    for (auto s : m->sh) {
+        int64_t a = 0;
+        MTRY(bpe_corpus_size(s, &a, nullptr));
+        MTRY(bpe_sample_lengths(s, lens + k, a));
+        k += a;
+    }
+    return BPE_OK;
+}
+
+int multi_read_samples(bpe_multi *m, const int64_t *idx, int64_t n, int32_t *ids_out,
+                       int64_t ids_cap, int64_t *off) {
+    MTRY(distribute(m));
+    if (n < 0 || (n && !idx) || !off) return bpe_fail(BPE_ERR_ARG, "bpe native: bad read_samples arguments");
+    std::vector<int64_t> first(m->n + 1, 0);
+    for (int r = 0; r < m->n; ++r) {
+        int64_t a = 0;
+        MTRY(bpe_corpus_size(m->sh[r], &a, nullptr));
+        first[r + 1] = first[r] + a;
+    }
+    // per shard: its requested samples (local indices) and where each goes in the answer
+    std::vector<std::vector<int64_t>> local(m->n), slot(m->n);
+    for (int64_t k = 0; k < n; ++k) {
+        if (idx[k] < 0 || idx[k] >= first[m->n])
+            return bpe_fail(BPE_ERR_ARG, "bpe native: sample index out of range");
+        const int r = (int)(std::upper_bound(first.begin(), first.end(), idx[k]) - first.begin()) - 1;
+        local[r].push_back(idx[k] - first[r]);
+        slot[r].push_back(k);
+    }
+    std::vector<std::vector<int32_t>> ids(m->n);
+    std::vector<std::vector<int64_t>> offs(m->n);
+    std::vector<int64_t> len(n);
+    for (int r = 0; r < m->n; ++r) {
+        if (local[r].empty()) continue;
+        const int64_t q = (int64_t)local[r].size();
+        std::vector<int64_t> lens(first[r + 1] - first[r]);
+        MTRY(bpe_sample_lengths(m->sh[r], lens.data(), (int64_t)lens.size()));
+        int64_t need = 0;
+        for (int64_t i : local[r]) need += lens[i];
+        ids[r].resize(need);
+        offs[r].resize(q + 1);
+        MTRY(bpe_read_samples(m->sh[r], local[r].data(), q, ids[r].data(), need, offs[r].data()));
+        for (int64_t j = 0; j < q; ++j) len[slot[r][j]] = offs[r][j + 1] - offs[r][j];
+    }
+    off[0] = 0;
+    for (int64_t k = 0; k < n; ++k) off[k + 1] = off[k] + len[k];
+    if (ids_cap < off[n] || (off[n] && !ids_out))
+        return bpe_fail(BPE_ERR_ARG, "bpe native: read_samples buffer too small");
+    for (int r = 0; r < m->n; ++r)
+        for (size_t j = 0; j < slot[r].size(); ++j) {
+            const int64_t k = slot[r][j];
+            std::copy(ids[r].begin() + offs[r][j], ids[r].begin() + offs[r][j + 1], ids_out + off[k]);
+        }
+    return BPE_OK;
+}
+
 // ---- the hot path -----------------------------------------------------------------------------------
 // findNextMerge over the shards (core.ts:247-326): the host protocol (sharded.py
 // exchange_and_select, in C++).

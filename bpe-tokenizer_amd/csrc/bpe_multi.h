@@ -20,6 +20,9 @@ int multi_clear_corpus(bpe_multi *m);
 int multi_corpus_size(bpe_multi *m, int64_t *n_samples, int64_t *n_tokens);
 int multi_read_corpus(bpe_multi *m, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
                       int64_t off_cap);
+int multi_sample_lengths(bpe_multi *m, int64_t *lens, int64_t cap);
+int multi_read_samples(bpe_multi *m, const int64_t *idx, int64_t n, int32_t *ids_out,
+                       int64_t ids_cap, int64_t *off);
 int multi_find_next_merge(bpe_multi *m, int64_t max_length, int64_t min_weight, int32_t *a,
                           int32_t *b, int64_t *w);
 int multi_apply_merge(bpe_multi *m, int32_t a, int32_t b, int32_t c, int64_t *replaced);

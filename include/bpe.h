@@ -103,6 +103,18 @@ int bpe_corpus_size(bpe_ctx *ctx, int64_t *n_samples, int64_t *n_tokens);
 int bpe_read_corpus(bpe_ctx *ctx, int32_t *ids_out, int64_t ids_cap, int64_t *sample_off,
                     int64_t off_cap);
 
+/* Live token count of every sample, in corpus order (cap >= n_samples).  A merge shortens
+ * exactly the samples it rewrites, so comparing lengths before and after finds the rows
+ * BPETokenizerDB.applyMerge selects and updates (db/core.ts:399-417: `like '%from_code%'` +
+ * `update corpus`).  Two reads of the corpus on the device; n_samples x 8 B come back. */
+int bpe_sample_lengths(bpe_ctx *ctx, int64_t *lens, int64_t cap);
+
+/* Reads back the samples idx[0..n) (any order, repeats allowed): their ids packed in that order
+ * into ids_out (capacity ids_cap), sample k at [sample_off[k], sample_off[k+1]) (n+1 offsets).
+ * The db twin's row write-back (db/core.ts:414-417) without materialising the whole corpus. */
+int bpe_read_samples(bpe_ctx *ctx, const int64_t *idx, int64_t n, int32_t *ids_out, int64_t ids_cap,
+                     int64_t *sample_off);
+
 /* ---- hot path ----------------------------------------------------------------------------------
  * findNextMerge (core.ts:247-326).  max_length: 0 = falsy = unlimited (core.ts:255,272);
  * min_weight: 0 = falsy = 2 (core.ts:256).  On BPE_OK writes the chosen pair (a, b) and its count

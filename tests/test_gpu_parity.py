@@ -83,6 +83,16 @@ def test_random_vs_oracle(seed, mode):
     e, got = run_engine(samples, len16, opts, mode=mode)
     assert got == want
     assert e.samples() == st.samples()
+    check_sample_index(e, st.samples(), rng)
+
+
+def check_sample_index(e, want, rng):
+    """bpe_sample_lengths / bpe_read_samples (the db twin's row write-back) against the expected
+    samples: every length, and a random selection read back in a random order."""
+    assert e.sample_lengths().tolist() == [len(s) for s in want]
+    idx = [rng.randrange(len(want)) for _ in range(min(50, 2 * len(want)))] if want else []
+    ids, off = e.read_samples(idx)
+    assert [ids[off[k]:off[k + 1]].tolist() for k in range(len(idx))] == [list(want[i]) for i in idx]
 
 
 @pytest.mark.parametrize('mode', MODES)

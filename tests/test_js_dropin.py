@@ -33,12 +33,29 @@ def test_addon_builds_and_exports():
                                    os.path.join(ADDON_DIR, 'bpe_napi.node')], text=True)
     assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEngine,'
                            'deviceCount,encodeMerges,findNextMerge,mergeUntil,readCorpus,'
-                           'setTokenLen16')
+                           'readSamples,sampleLengths,setTokenLen16')
 
 
 def test_host_logic_against_golden():
     build_addon()
     assert 'host_only ok' in run_node('host_only.js')
+
+
+def test_db_twin_host_logic_over_sqlite():
+    """BPETokenizerDB (js/db.js) over a real sqlite database (Python's sqlite3 behind
+    tests/js/sqlite_bridge.js): schema, JSON round trips and golden encode/decode vectors, token
+    rows and weights, the proxy views, error messages.  No device needed."""
+    build_addon()
+    assert 'db_host_only ok' in run_node('db_host_only.js')
+
+
+@pytest.mark.gpu
+def test_db_twin_spec_golden_and_lockstep():
+    """BPETokenizerDB on the GPU: the reference's db spec, golden cases in both loop modes,
+    row-by-row lockstep with core.js, resume from the database, rows added out of id order."""
+    build_addon()
+    out = run_node('spec_db_gpu.js', '--expose-gc')
+    assert 'spec_db_gpu ok' in out
 
 
 @pytest.mark.gpu

@@ -10,7 +10,7 @@ import pytest
 from bpe_amd import MODES, pkg
 from golden_util import load_small
 from oracle import Corpus, OracleState
-from test_gpu_parity import random_corpus
+from test_gpu_parity import check_sample_index, random_corpus
 
 pytestmark = pytest.mark.gpu
 
@@ -61,6 +61,7 @@ def test_sharded_context_vs_oracle(seed, mode):
     got = run(e, opts, mode, alphabet)
     assert got == want
     assert e.samples() == st.samples()
+    check_sample_index(e, st.samples(), rng)
     e.close()
 
 
