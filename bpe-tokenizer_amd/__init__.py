@@ -27,7 +27,7 @@ MAX_VOCAB = 55296
 # Every symbol include/bpe.h and include/bpe_tools.h declare (checked by tests/test_capi.py).
 C_API = [
     'bpe_version', 'bpe_last_error', 'bpe_device_count', 'bpe_create', 'bpe_destroy',
-    'bpe_create_multi', 'bpe_shard_count',
+    'bpe_create_multi', 'bpe_shard_count', 'bpe_set_mode',
     'bpe_set_token_len16', 'bpe_num_tokens', 'bpe_add_sample', 'bpe_add_latin1',
     'bpe_clear_corpus', 'bpe_corpus_size', 'bpe_read_corpus', 'bpe_sample_lengths',
     'bpe_read_samples', 'bpe_find_next_merge',
@@ -41,6 +41,8 @@ TABLE_BINS = 81920
 MAX_CAND = 16       # BPE_MAX_CAND
 REDUCE_RCCL = 0     # BPE_REDUCE_RCCL
 REDUCE_HOST = 1     # BPE_REDUCE_HOST
+MODE_STREAM = 0     # BPE_MODE_STREAM
+MODE_INCREMENTAL = 1   # BPE_MODE_INCREMENTAL
 LOOP_BATCH = 64     # BPE_LOOP_BATCH
 
 
@@ -57,7 +59,8 @@ class Stats(ctypes.Structure):
         ('compactions', ctypes.c_int64), ('exact_passes', ctypes.c_int64),
         ('step_timed', ctypes.c_int64), ('tie_tail', ctypes.c_int64),
         ('tie_lone', ctypes.c_int64), ('loop_host', ctypes.c_int64),
-        ('fused_passes', ctypes.c_int64),
+        ('fused_passes', ctypes.c_int64), ('pix_builds', ctypes.c_int64),
+        ('pix_merges', ctypes.c_int64), ('pix_host', ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -93,6 +96,7 @@ def lib():
         'bpe_create_multi': ([ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                               ctypes.c_int], ctypes.c_int),
         'bpe_shard_count': ([vp, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        'bpe_set_mode': ([vp, ctypes.c_int], ctypes.c_int),
         'bpe_set_token_len16': ([vp, ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
         'bpe_num_tokens': ([vp, i32p], ctypes.c_int),
         'bpe_add_sample': ([vp, i32p, ctypes.c_int64], ctypes.c_int),
@@ -194,6 +198,12 @@ class Engine:
             _check(lib().bpe_create_multi(ctypes.byref(self._ctx), len(devices), dv,
                                           REDUCE_HOST if reduce == 'host' else REDUCE_RCCL),
                    'bpe_create_multi')
+
+    def set_mode(self, mode):
+        """'stream' (every merge one pass over the corpus) or 'incremental' (mergeUntil on the
+        position index: O(W) work per merge; bpe_set_mode)."""
+        m = {'stream': MODE_STREAM, 'incremental': MODE_INCREMENTAL}[mode]
+        _check(lib().bpe_set_mode(self._ctx, m), 'bpe_set_mode')
 
     def shard_count(self):
         n = ctypes.c_int()

@@ -9,9 +9,12 @@
 //                                               k_argmax_hot/cold, k_collect, [k_tie (rule R3)]
 // so a mergeUntil iteration streams the corpus exactly once.
 #include "bpe_kernels.hip.h"
+#include "bpe_pix.hip.h"
 #include "bpe.h"
 #include "bpe_multi.h"
 #include "bpe_tools.h"
+
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstddef>
@@ -117,6 +120,10 @@ struct bpe_ctx {
     // maintained too, and a pass counts only the pairs the merge can change); BPE_FUSED=1 keeps
     // the full hot recount with the cold refresh riding along (MODE_FUSED) instead
     bool use_incr = true;
+    // mergeUntil on the position index (bpe_set_mode BPE_MODE_INCREMENTAL, BPE_PIX=1): O(W) work
+    // per merge instead of a pass (bpe_pix.hip.h)
+    bool use_pix = false;
+    struct PixState *pix = nullptr;
     bool carry_valid = false;    // d_sums / d_carry describe the current corpus and geometry
     int64_t cpr = 0;
     int R = 0, G = 0;
@@ -1370,6 +1377,303 @@ int read_samples(bpe_ctx *c, const int64_t *idx, int64_t n, int32_t *ids_out, in
     return BPE_OK;
 }
 
+// ================================================================================================
+// The incremental mergeUntil on the position index (bpe_pix.hip.h)
+// ================================================================================================
+struct PixState {
+    PixCorpus C{};
+    PixTable T{};
+    PixBufs B{};
+    PixCtl *d_ctl = nullptr, *h_ctl = nullptr;
+    long long *d_log = nullptr, *h_log = nullptr;
+    uint64_t cap = 0;
+    int64_t max_length = 0;
+    std::vector<void *> owned;
+};
+constexpr int64_t PIX_BATCH = 256;      // merges per host round trip
+constexpr int PIX_NOT_ELIGIBLE = 100;   // (internal) the corpus does not fit the index
+
+void pix_free(bpe_ctx *c) {
+    PixState *P = c->pix;
+    if (!P) return;
+    for (void *q : P->owned) dfree(q);
+    if (P->h_ctl) (void)hipHostFree(P->h_ctl);
+    if (P->h_log) (void)hipHostFree(P->h_log);
+    delete P;
+    c->pix = nullptr;
+}
+
+template <typename T>
+int pix_alloc(PixState *P, T **out, size_t n) {
+    int rc = dev_alloc(out, n);
+    if (!rc) P->owned.push_back(*out);
+    return rc;
+}
+
+// The index of the current corpus: the slot array is the compacted corpus itself (d_ids, n live
+// slots), links i -> i+1, and one radix sort of (pair key, slot) gives every pair's list; counts
+// follow from the run offsets (an inclusive max-scan of run starts).
+int pix_build(bpe_ctx *c, int64_t max_length) {
+    int rc;
+    if ((rc = settle(c))) return rc;
+    if (!c->packed)
+        if ((rc = compact(c))) return rc;
+    const int64_t n = c->live_slots;
+    // positions and pool offsets are 32-bit; the vocabulary key is two 16-bit ids
+    if (n < 2 || n > (int64_t)0x7FFFFFFF || c->h_len16.size() > 0xFFFF) return PIX_NOT_ELIGIBLE;
+    if ((rc = ensure_vocab(c, (int64_t)c->h_len16.size()))) return rc;
+    if ((rc = sync_len16(c, 1))) return rc;
+    pix_free(c);
+    PixState *P = c->pix = new PixState();
+    P->max_length = max_length;
+    hipStream_t s = c->stream;
+    const uint32_t N = (uint32_t)n;
+    PixCorpus &C = P->C;
+    C.tok = c->d_ids;
+    C.n = N;
+    if ((rc = pix_alloc(P, &C.nxt, N)) || (rc = pix_alloc(P, &C.prv, N))) return rc;
+    const uint64_t pool_cap = std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)N + std::max<uint64_t>(N / 2, 1u << 22));
+    PixBufs &B = P->B;
+    if ((rc = pix_alloc(P, &B.pool, pool_cap))) return rc;
+    {
+        Scratch t;
+        uint32_t *A, *Bk, *V, *D, *R, *d_nruns;
+        int32_t *runmark, *run_start;
+        if ((rc = t.get(&A, N)) || (rc = t.get(&Bk, N)) || (rc = t.get(&V, N)) || (rc = t.get(&D, N)) ||
+            (rc = t.get(&R, N)) || (rc = t.get(&d_nruns, 2)))
+            return rc;
+        runmark = reinterpret_cast<int32_t *>(R);
+        run_start = reinterpret_cast<int32_t *>(D);
+        k_pix_build_keys<<<4096, 256, 0, s>>>(C, A, V, runmark);
+        HIP_TRY(hipGetLastError());
+        // temp storage for every library call below
+        size_t tb = 0, t1 = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, A, Bk, V, B.pool, N, 0, 32, s));
+        tb = std::max(tb, t1);
+        HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, t1, runmark, run_start, hipcub::Max(), N, s));
+        tb = std::max(tb, t1);
+        HIP_TRY(hipcub::DeviceReduce::ReduceByKey(nullptr, t1, Bk, V, A, R, d_nruns, hipcub::Sum(), N, s));
+        tb = std::max(tb, t1);
+        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, t1, Bk, A, D, d_nruns + 1, N, s));
+        tb = std::max(tb, t1);
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, D, Bk, N, s));
+        tb = std::max(tb, t1);
+        void *tmp;
+        if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
+        HIP_TRY(hipcub::DeviceScan::InclusiveScan(tmp, tb, runmark, run_start, hipcub::Max(), N, s));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, A, Bk, V, B.pool, N, 0, 32, s));
+        // A: counted flags in sorted order; then per pair (V: keys, R: counts)
+        k_pix_build_counted<<<4096, 256, 0, s>>>(C, B.pool, run_start, A);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipcub::DeviceReduce::ReduceByKey(tmp, tb, Bk, V, A, R, d_nruns, hipcub::Sum(), N, s));
+        // (A: keys again, D: list lengths, Bk: list offsets)
+        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(tmp, tb, Bk, A, D, d_nruns + 1, N, s));
+        uint32_t nruns[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(nruns, d_nruns, sizeof nruns, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (nruns[0] != nruns[1] || nruns[0] == 0 || nruns[0] > N)
+            return fail(BPE_ERR_STATE, "bpe native: position index: bad pair runs");
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, D, Bk, nruns[0], s));
+        // the pair table: room for the current pairs and the ones merges will add
+        uint64_t cap = 1u << 20;
+        while (cap < 4ull * nruns[0] || cap < (uint64_t)N / 8) cap <<= 1;
+        if (cap > (1ull << 31)) return PIX_NOT_ELIGIBLE;
+        P->cap = cap;
+        PixTable &T = P->T;
+        T.mask = (uint32_t)(cap - 1);
+        T.nblocks = (uint32_t)(cap / PIX_B);
+        T.nsuper = (T.nblocks + PIX_SB - 1) / PIX_SB;
+        if ((rc = pix_alloc(P, &T.keys, cap)) || (rc = pix_alloc(P, &T.cnt, cap)) ||
+            (rc = pix_alloc(P, &T.off, cap)) || (rc = pix_alloc(P, &T.len, cap)) ||
+            (rc = pix_alloc(P, &T.fill, cap)) || (rc = pix_alloc(P, &T.bmax, T.nblocks)) ||
+            (rc = pix_alloc(P, &T.sbmax, T.nsuper)) || (rc = pix_alloc(P, &T.bdirty, T.nblocks)) ||
+            (rc = pix_alloc(P, &T.sbdirty, T.nsuper)))
+            return rc;
+        HIP_TRY(hipMemsetAsync(T.keys, 0xFF, cap * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(T.cnt, 0, cap * sizeof(unsigned long long), s));
+        HIP_TRY(hipMemsetAsync(T.len, 0, cap * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(T.bdirty, 0, T.nblocks * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(T.sbdirty, 0, T.nsuper * sizeof(uint32_t), s));
+        // per-merge buffers
+        B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
+        B.ent_cap = 2 * B.site_cap + 16;
+        B.key_cap = B.ent_cap;
+        if ((rc = pix_alloc(P, &B.sites, B.site_cap)) || (rc = pix_alloc(P, &B.ent, B.ent_cap)) ||
+            (rc = pix_alloc(P, &B.newkeys, B.key_cap)) || (rc = pix_alloc(P, &B.dblocks, T.nblocks)) ||
+            (rc = pix_alloc(P, &B.dsuper, T.nsuper)))
+            return rc;
+        if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
+        HIP_TRY(hipHostMalloc((void **)&P->h_ctl, sizeof(PixCtl), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void **)&P->h_log, 3 * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
+        PixCtl *h = P->h_ctl;
+        memset(h, 0, sizeof *h);
+        h->status = PIX_RUN;
+        h->max_length = max_length;
+        h->max_id = BPE_MAX_VOCAB;
+        h->next_id = (int32_t)c->h_len16.size();
+        h->pool_top = N;
+        h->pool_cap = pool_cap;
+        h->used_cap = cap / 10 * 7;
+        HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
+        k_pix_build_insert<<<4096, 256, 0, s>>>(T, P->d_ctl, A, R, D, Bk, d_nruns);
+        k_pix_bmax<<<4096, 256, 0, s>>>(T, B, P->d_ctl, c->d_len16, 1);
+        k_pix_sbmax<<<1024, 256, 0, s>>>(T, B, P->d_ctl, 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));   // (before the scratch goes)
+        if (h->status != PIX_RUN) return fail(BPE_ERR_STATE, "bpe native: position index: pair table full");
+    }
+    c->counts_valid = c->carry_valid = c->best_ready = false;
+    c->cold_exact = false;
+    if (c->stats_on) c->stats.pix_builds += 1;
+    return BPE_OK;
+}
+
+// The corpus back into the chunk layout: the live slots of the slot array, in order, as a dense
+// prefix (then the streaming path's state is rebuilt on its next use).
+int pix_finish(bpe_ctx *c) {
+    PixState *P = c->pix;
+    if (!P) return BPE_OK;
+    hipStream_t s = c->stream;
+    const uint32_t N = P->C.n;
+    {
+        Scratch t;
+        uint8_t *flag;
+        uint32_t *d_nsel;
+        int rc;
+        if ((rc = t.get(&flag, N)) || (rc = t.get(&d_nsel, 1))) return rc;
+        k_pix_live_flags<<<4096, 256, 0, s>>>(c->d_ids, N, flag);
+        size_t tb = 0;
+        HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
+        void *tmp;
+        if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
+        HIP_TRY(hipcub::DeviceSelect::Flagged(tmp, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
+        uint32_t nsel = 0;
+        HIP_TRY(hipMemcpyAsync(&nsel, d_nsel, sizeof nsel, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if ((int64_t)nsel != c->live_slots)
+            return fail(BPE_ERR_STATE, "bpe native: position index: live slots lost");
+    }
+    std::swap(c->d_ids, c->d_tmp);
+    pix_free(c);
+    return seal_packed(c);
+}
+
+// mergeUntil on the index: batches of PIX_BATCH merges, one host round trip each.  An iteration
+// the index cannot take (PIX_HOST) runs on the streaming path, and the index is rebuilt after it.
+int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
+                    int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    int rc;
+    int64_t n = 0;
+    const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
+    int builds = 0;
+    while (!max_iterations || n < max_iterations) {                      // core.ts:374-378
+        if (!c->pix || c->pix->max_length != max_length) {
+            if ((rc = pix_finish(c))) return rc;
+            if ((rc = settle(c))) return rc;
+            if (c->n_live < 2) break;
+            rc = pix_build(c, max_length);
+            ++builds;
+            if (rc == PIX_NOT_ELIGIBLE) {
+                pix_free(c);
+                *n_merges = n;
+                return PIX_NOT_ELIGIBLE;   // the caller goes on with the streaming loop
+            }
+            if (rc) return rc;
+        }
+        PixState *P = c->pix;
+        hipStream_t s = c->stream;
+        const int64_t base = (int64_t)c->h_len16.size();
+        int64_t want = std::min<int64_t>(PIX_BATCH, BPE_MAX_VOCAB - base);
+        if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
+        if ((rc = ensure_len16_cap(c, base + std::max<int64_t>(want, 1)))) return rc;
+        if ((rc = sync_len16(c, 1))) return rc;
+        int status = PIX_HOST;
+        int64_t nd = 0;
+        if (want > 0) {
+            k_pix_begin<<<1, 1, 0, s>>>(P->d_ctl, want, (int32_t)base, mw);
+            for (int64_t i = 0; i < want; ++i) {
+                k_pix_select<<<1, 1024, 0, s>>>(P->T, P->d_ctl, c->d_len16);
+                k_pix_tie<<<MAX_CAND, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
+                k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
+                k_pix_delta<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
+                k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+                k_pix_scatter<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+                k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, c->d_len16, P->d_log);
+                k_pix_bmax<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->d_len16, 0);
+                k_pix_sbmax<<<256, 256, 0, s>>>(P->T, P->B, P->d_ctl, 0);
+            }
+            HIP_TRY(hipGetLastError());
+            PixCtl *h = P->h_ctl;
+            HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(P->h_log, P->d_log, 3 * want * sizeof(long long),
+                                   hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            status = h->status;
+            nd = h->n_done;
+            if (status == PIX_ERROR) {
+                char msg[160];
+                snprintf(msg, sizeof msg, "bpe native: position index inconsistent (code %d)", h->err);
+                return fail(BPE_ERR_STATE, msg);
+            }
+            if (nd < 0 || nd > want) return fail(BPE_ERR_STATE, "bpe native: position index: bad merge count");
+            c->h_len16.resize(base + nd, 1);
+            c->h_count.resize(base + nd, 0);
+            for (int64_t i = 0; i < nd; ++i, ++n) {
+                const int32_t a = (int32_t)P->h_log[3 * i], b = (int32_t)P->h_log[3 * i + 1];
+                const int64_t W = P->h_log[3 * i + 2];
+                const int64_t cc = base + i;
+                c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];            // core.ts:318
+                if (c->stats_on) {
+                    c->stats.iterations += 1;
+                    c->stats.live_tokens += c->n_live;
+                    c->stats.pix_merges += 1;
+                }
+                c->n_live -= W;
+                c->live_slots -= W;
+                c->h_count[a] -= W;
+                c->h_count[b] -= W;
+                c->h_count[cc] += W;
+                if (n < cap) {
+                    out_abw[3 * n] = a;
+                    out_abw[3 * n + 1] = b;
+                    out_abw[3 * n + 2] = W;
+                }
+            }
+            c->len16_lo = base + nd;   // k_pix_apply wrote the new lengths on the device
+            if (status == PIX_DONE) break;
+            if (status == PIX_RUN || status == PIX_PAUSE) continue;
+            if (c->stats_on) c->stats.pix_host += 1;
+        }
+        if (max_iterations && n >= max_iterations) break;
+        // PIX_HOST: this iteration on the streaming path, then a fresh index
+        if ((rc = pix_finish(c))) return rc;
+        if (builds > 64 && builds > n / 16) {
+            *n_merges = n;
+            return PIX_NOT_ELIGIBLE;   // (the index keeps failing here: stay on the stream)
+        }
+        int32_t a, b;
+        int64_t w;
+        rc = do_find(c, max_length, min_weight, &a, &b, &w);
+        if (rc == BPE_NO_MERGE) break;
+        if (rc) return rc;
+        const int32_t cc = (int32_t)c->h_len16.size();
+        if ((rc = do_apply(c, a, b, cc, nullptr))) return rc;
+        if (c->pending) c->pend_expect = w;
+        if ((rc = settle(c))) return rc;
+        if (n < cap) {
+            out_abw[3 * n] = a;
+            out_abw[3 * n + 1] = b;
+            out_abw[3 * n + 2] = w;
+        }
+        ++n;
+    }
+    if ((rc = pix_finish(c))) return rc;
+    *n_merges = n;
+    return settle(c);
+}
+
 #define MULTI(call) \
     if (c && c->multi) return multi_##call
 #define NOT_MULTI                                                                          \
@@ -1408,6 +1712,7 @@ int bpe_create(bpe_ctx **out, int device) {
     bpe_ctx *c = new bpe_ctx();
     c->device = device;
     c->use_incr = !getenv("BPE_FUSED");
+    c->use_pix = getenv("BPE_PIX") && atoi(getenv("BPE_PIX")) > 0;
     int rc;
     auto bail = [&](int code) {
         bpe_destroy(c);
@@ -1480,6 +1785,7 @@ int bpe_destroy(bpe_ctx *c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    pix_free(c);
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
@@ -1774,13 +2080,10 @@ int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replace
     return replay(c, abc, n, replaced, count_after != 0);
 }
 
-int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
-                    int64_t *out_abw, int64_t cap, int64_t *n_merges) {
-    if (n_merges && (cap <= 0 || out_abw)) MULTI(merge_until(c->multi, max_length, min_weight, max_iterations, out_abw, cap, n_merges));
-    if (!c || !n_merges || (cap > 0 && !out_abw))
-        return fail(BPE_ERR_ARG, "bpe native: null argument");
-    int rc = set_device(c);
-    if (rc) return rc;
+// The streaming mergeUntil: batches on the device-resident loop, host iterations between them.
+static int merge_until_stream(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
+                       int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    int rc;
     int64_t n = 0;
     const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
     int64_t abw[3 * LOOP_BATCH];
@@ -1841,6 +2144,35 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     }
     *n_merges = n;
     return settle(c);
+}
+
+int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
+                    int64_t *out_abw, int64_t cap, int64_t *n_merges) {
+    if (n_merges && (cap <= 0 || out_abw)) MULTI(merge_until(c->multi, max_length, min_weight, max_iterations, out_abw, cap, n_merges));
+    if (!c || !n_merges || (cap > 0 && !out_abw))
+        return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (!c->use_pix) return merge_until_stream(c, max_length, min_weight, max_iterations, out_abw, cap, n_merges);
+    int64_t n = 0;
+    rc = pix_merge_until(c, max_length, min_weight, max_iterations, out_abw, cap, &n);
+    *n_merges = n;
+    if (rc != PIX_NOT_ELIGIBLE) return rc;
+    // the corpus does not fit the index (or keeps failing it): the stream takes the rest
+    if (max_iterations && n >= max_iterations) return settle(c);
+    int64_t m = 0;
+    rc = merge_until_stream(c, max_length, min_weight, max_iterations ? max_iterations - n : 0,
+                            cap > n ? out_abw + 3 * n : out_abw, cap - n, &m);
+    *n_merges = n + m;
+    return rc;
+}
+
+int bpe_set_mode(bpe_ctx *c, int mode) {
+    NOT_MULTI;
+    if (!c || (mode != BPE_MODE_STREAM && mode != BPE_MODE_INCREMENTAL))
+        return fail(BPE_ERR_ARG, "bpe native: bad mode");
+    c->use_pix = mode == BPE_MODE_INCREMENTAL;
+    return BPE_OK;
 }
 
 int bpe_export_counts(bpe_ctx *c, uint64_t *table) {

@@ -1,0 +1,642 @@
+// bpe_pix.hip.h — the incremental mergeUntil: a position index, so
+// that a merge costs O(W) work instead of a pass over the corpus.
+//
+// The corpus is one dense slot array (tokens, SEP = -1 between samples, TOMB for merged-away
+// slots) with next / prev links over the live slots.  Slots never move, so a slot index is a
+// stable position.  Every adjacent pair (u, v) has
+//   - its exact count under the reference's rule (core.ts:265-293: each adjacency once, except
+//     that a run of L equal tokens x counts floor(L / 2) pairs (x, x)),
+//   - a list of the slots where it occurs (a segment of one pool).  A list is written once: the
+//     adjacencies of a pair are all born together, either in the initial index or in the merge
+//     that creates the newer of its two tokens (a merge makes new adjacencies only with the token
+//     it creates).  Entries go stale as merges consume them and are filtered on use.
+// in one open-addressing table keyed (u << 16 | v).  A two-level max (per 256-slot block, per 256
+// blocks) over the packed selection keys (W << 17 | 0x1FFFF - (u + v), core.ts:294-305) finds the
+// best pair; ties on the packed key go to the earliest last counted occurrence (rule R3), taken
+// from the candidates' lists.
+//
+// One merge (a, b) -> c, every kernel reading the decision from PixCtl (no host round trip):
+//   k_pix_select   best key, candidates, W, min_weight / vocabulary checks
+//   k_pix_tie      R3 over the candidates' lists (only with a tie)
+//   k_pix_sites    the merge sites from the (a, b) list; for a == b the runs, walked from their
+//                  heads (sites at even offsets, replaceAll's left-to-right rule), with their
+//                  count changes
+//   k_pix_delta    a != b: count changes around each site, the adjacencies of c
+//   k_pix_alloc / k_pix_scatter   segments for the new pairs (all contain c), their slots
+//   k_pix_apply    tokens and links (the only kernel that changes the corpus)
+//   k_pix_bmax / k_pix_sbmax      the two-level max over the touched blocks
+// Anything the index cannot do in bounded work (a run or chain longer than PIX_WALK, a full
+// buffer, more than MAX_CAND tied pairs) sets PIX_HOST before k_pix_apply: the corpus is still
+// that of the last completed merge, and the host takes the iteration on the streaming path.
+#pragma once
+#include "bpe_kernels.hip.h"
+
+namespace bpe {
+
+constexpr uint32_t PIX_NONE = 0xFFFFFFFFu;    // no slot (links), empty table key
+constexpr int PIX_B = 256;                    // table slots per block (block max)
+constexpr int PIX_SB = 256;                   // blocks per superblock
+constexpr int PIX_WALK = 1 << 16;             // longest run / chain one thread walks
+constexpr int PIX_PROBE = 4096;               // longest probe sequence in the table
+constexpr int PIX_GRID = 1024;                // blocks of the grid-stride kernels
+
+// PIX_PAUSE: the batch's merges are done (the next batch goes on)
+enum PixStatus { PIX_RUN = 0, PIX_DONE = 1, PIX_HOST = 2, PIX_ERROR = 3, PIX_PAUSE = 4 };
+
+struct PixCorpus {
+    int32_t *tok;
+    uint32_t *nxt, *prv;
+    uint32_t n;
+};
+
+struct PixTable {
+    uint32_t *keys;
+    unsigned long long *cnt;
+    uint32_t *off, *len, *fill;
+    unsigned long long *bmax, *sbmax;
+    uint32_t *bdirty, *sbdirty;
+    uint32_t mask;
+    uint32_t nblocks, nsuper;
+};
+
+struct PixBufs {
+    uint32_t *pool;      // list segments
+    uint32_t *sites;     // this merge's sites
+    uint2 *ent;          // this merge's new adjacencies: (table slot, position)
+    uint32_t *newkeys;   // table slots of this merge's new pairs
+    uint32_t *dblocks, *dsuper;   // touched blocks / superblocks
+    uint32_t site_cap, ent_cap, key_cap;
+};
+
+struct PixCtl {
+    int status;
+    int tie;
+    int32_t a, b, c;
+    int32_t next_id, max_id;
+    int err;
+    unsigned long long W, best;
+    long long min_weight, max_length;
+    long long n_done, n_want;          // merges done / allowed in this batch
+    uint32_t pair_slot, n_cand, tie_done, pad0;
+    uint32_t n_sites, n_ent, n_keys, n_dblocks, n_dsuper, pad1;
+    unsigned long long n_check;        // merges made (== W when the index is consistent)
+    unsigned long long pool_top, pool_cap;
+    unsigned long long used, used_cap; // table claims / the claims it may hold
+    uint32_t cand_slot[MAX_CAND];
+    unsigned long long last[MAX_CAND];
+};
+
+__device__ __forceinline__ uint32_t pix_key(int32_t u, int32_t v) {
+    return ((uint32_t)u << 16) | (uint32_t)v;
+}
+
+__device__ __forceinline__ uint32_t pix_hash(uint32_t key) {
+    uint32_t h = key * 0x9E3779B1u;
+    return h ^ (h >> 15);
+}
+
+// the packed selection key of a table slot (0: no pair, empty, or filtered by max_length)
+__device__ __forceinline__ unsigned long long pix_sel(const PixTable &t, uint32_t s,
+                                                      const int32_t *len16, long long ml) {
+    const uint32_t k = t.keys[s];
+    if (k == PIX_NONE) return 0;
+    const unsigned long long w = t.cnt[s];
+    if (w == 0 || ml < 0) return 0;
+    const int32_t u = (int32_t)(k >> 16), v = (int32_t)(k & 0xFFFF);
+    if (ml > 0 && (long long)len16[u] + len16[v] > ml) return 0;      // core.ts:270-273
+    return (w << 17) | (unsigned long long)(0x1FFFF - (u + v));        // core.ts:294-305
+}
+
+__device__ __forceinline__ void pix_mark(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                         uint32_t s) {
+    const uint32_t blk = s / PIX_B;
+    if (atomicExch(&t.bdirty[blk], 1u) == 0u) {
+        const uint32_t i = atomicAdd(&ctl->n_dblocks, 1u);
+        if (i < t.nblocks) B.dblocks[i] = blk;
+    }
+}
+
+__device__ __forceinline__ void pix_fail(PixCtl *ctl, int why) {
+    if (atomicCAS(&ctl->status, PIX_RUN, PIX_HOST) == PIX_RUN) ctl->err = why;
+}
+
+// find-or-claim the slot of a pair; PIX_NONE when the probe sequence is exhausted
+__device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uint32_t key,
+                                             bool claim) {
+    uint32_t s = pix_hash(key) & t.mask;
+    for (int i = 0; i < PIX_PROBE; ++i, s = (s + 1) & t.mask) {
+        const uint32_t k = t.keys[s];
+        if (k == key) return s;
+        if (k == PIX_NONE) {
+            if (!claim) return PIX_NONE;
+            const uint32_t old = atomicCAS(&t.keys[s], PIX_NONE, key);
+            if (old == PIX_NONE) {
+                atomicAdd(&ctl->used, 1ull);
+                return s;
+            }
+            if (old == key) return s;
+        }
+    }
+    return PIX_NONE;
+}
+
+// count change of an existing or new pair
+__device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                            int32_t u, int32_t v, long long d) {
+    const uint32_t s = pix_slot(t, ctl, pix_key(u, v), true);
+    if (s == PIX_NONE) {
+        pix_fail(ctl, 1);
+        return s;
+    }
+    if (d) atomicAdd(&t.cnt[s], (unsigned long long)d);
+    pix_mark(t, B, ctl, s);
+    return s;
+}
+
+// a new adjacency (u, v) at slot pos (u or v is c): list entry + one more slot in its segment
+__device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                          int32_t u, int32_t v, uint32_t pos, long long d) {
+    const uint32_t s = pix_add(t, B, ctl, u, v, d);
+    if (s == PIX_NONE) return;
+    if (atomicAdd(&t.len[s], 1u) == 0u) {
+        const uint32_t k = atomicAdd(&ctl->n_keys, 1u);
+        if (k < B.key_cap) B.newkeys[k] = s;
+        else pix_fail(ctl, 2);
+    }
+    const uint32_t e = atomicAdd(&ctl->n_ent, 1u);
+    if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos);
+    else pix_fail(ctl, 3);
+}
+
+__device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32_t x) {
+    return p != PIX_NONE && C.tok[p] == x;
+}
+
+// ---- index build ------------------------------------------------------------------------------
+__global__ void k_pix_build_keys(PixCorpus C, uint32_t *keys, uint32_t *vals, int32_t *runmark) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < C.n; i += gridDim.x * blockDim.x) {
+        const int32_t t = C.tok[i];
+        const int32_t u = i + 1 < C.n ? C.tok[i + 1] : SEP;
+        keys[i] = (t >= 0 && u >= 0) ? pix_key(t, u) : PIX_NONE;
+        vals[i] = i;
+        runmark[i] = (i == 0 || C.tok[i - 1] != t) ? (int32_t)i : 0;
+        C.nxt[i] = i + 1 < C.n ? i + 1 : PIX_NONE;
+        C.prv[i] = i > 0 ? i - 1 : PIX_NONE;
+    }
+}
+
+// counted[j] for the sorted position pool[j]: 1, except a pair (x, x) at an odd offset of its run
+__global__ void k_pix_build_counted(PixCorpus C, const uint32_t *pool, const int32_t *run_start,
+                                    uint32_t *counted) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < C.n; j += gridDim.x * blockDim.x) {
+        const uint32_t i = pool[j];
+        uint32_t k = 1;
+        if (i + 1 < C.n && C.tok[i] == C.tok[i + 1]) k = ((i - (uint32_t)run_start[i]) & 1u) ? 0u : 1u;
+        counted[j] = k;
+    }
+}
+
+__global__ void k_pix_build_insert(PixTable t, PixCtl *ctl, const uint32_t *uniq,
+                                   const uint32_t *counts, const uint32_t *lens,
+                                   const uint32_t *offs, const uint32_t *n_runs) {
+    const uint32_t n = *n_runs;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        if (uniq[j] == PIX_NONE) continue;
+        const uint32_t s = pix_slot(t, ctl, uniq[j], true);
+        if (s == PIX_NONE) {
+            ctl->err = 9;
+            ctl->status = PIX_ERROR;
+            continue;
+        }
+        t.cnt[s] = counts[j];
+        t.len[s] = lens[j];
+        t.off[s] = offs[j];
+    }
+}
+
+// block maxima of every block (build) or of the touched ones (after a merge)
+__global__ void __launch_bounds__(256) k_pix_bmax(PixTable t, PixBufs B, PixCtl *ctl,
+                                                  const int32_t *len16, int all) {
+    const uint32_t nb = all ? t.nblocks : min(ctl->n_dblocks, t.nblocks);
+    if (!all && ctl->status != PIX_RUN) return;
+    __shared__ unsigned long long red[4];
+    for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
+        const uint32_t blk = all ? i : B.dblocks[i];
+        const unsigned long long v = pix_sel(t, blk * PIX_B + threadIdx.x, len16, ctl->max_length);
+        unsigned long long m = v;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            m = max(max(red[0], red[1]), max(red[2], red[3]));
+            t.bmax[blk] = m;
+            t.bdirty[blk] = 0;
+            const uint32_t sb = blk / PIX_SB;
+            if (!all && atomicExch(&t.sbdirty[sb], 1u) == 0u) {
+                const uint32_t k = atomicAdd(&ctl->n_dsuper, 1u);
+                if (k < t.nsuper) B.dsuper[k] = sb;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pix_sbmax(PixTable t, PixBufs B, PixCtl *ctl, int all) {
+    const uint32_t ns = all ? t.nsuper : min(ctl->n_dsuper, t.nsuper);
+    if (!all && ctl->status != PIX_RUN) return;
+    __shared__ unsigned long long red[4];
+    for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
+        const uint32_t sb = all ? i : B.dsuper[i];
+        const uint32_t blk = sb * PIX_SB + threadIdx.x;
+        unsigned long long m = blk < t.nblocks ? t.bmax[blk] : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            t.sbmax[sb] = max(max(red[0], red[1]), max(red[2], red[3]));
+            t.sbdirty[sb] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// a batch of n merges from the next vocabulary id on
+__global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight) {
+    if (ctl->status == PIX_PAUSE) ctl->status = PIX_RUN;
+    ctl->n_done = 0;
+    ctl->n_want = n;
+    ctl->next_id = next_id;
+    ctl->min_weight = min_weight;
+}
+
+// ---- one merge --------------------------------------------------------------------------------
+// Best key, candidates (every pair sharing it), the decision.  One block of 1024.
+__global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixCtl *ctl, const int32_t *len16) {
+    __shared__ unsigned long long red[16];
+    __shared__ uint32_t lst[64];
+    __shared__ uint32_t n_lst, n_blk;
+    __shared__ uint32_t blks[64];
+    const int tid = threadIdx.x;
+    if (ctl->status != PIX_RUN) return;
+    if (tid == 0) {
+        // counters of the previous merge (nothing else reads them now)
+        ctl->n_sites = ctl->n_ent = ctl->n_keys = ctl->n_dblocks = ctl->n_dsuper = 0;
+        ctl->n_cand = 0;
+        ctl->tie = 0;
+        ctl->tie_done = 0;
+        ctl->n_check = 0;
+        n_lst = n_blk = 0;
+    }
+    if (ctl->n_done >= ctl->n_want) {
+        if (tid == 0) ctl->status = PIX_PAUSE;
+        return;
+    }
+    unsigned long long m = 0;
+    for (uint32_t i = tid; i < t.nsuper; i += 1024) m = max(m, t.sbmax[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    unsigned long long best = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) best = max(best, red[i]);
+    const long long W = (long long)(best >> 17);
+    if (best == 0 || W < ctl->min_weight) {                           // core.ts:312-313
+        if (tid == 0) ctl->status = PIX_DONE;
+        return;
+    }
+    // superblocks, then blocks, then slots holding the best key
+    for (uint32_t i = tid; i < t.nsuper; i += 1024)
+        if (t.sbmax[i] == best) {
+            const uint32_t k = atomicAdd(&n_lst, 1u);
+            if (k < 64) lst[k] = i;
+        }
+    __syncthreads();
+    const uint32_t ns = min(n_lst, 64u);
+    for (uint32_t q = 0; q < ns; ++q) {
+        const uint32_t blk = lst[q] * PIX_SB + tid;
+        if (tid < PIX_SB && blk < t.nblocks && t.bmax[blk] == best) {
+            const uint32_t k = atomicAdd(&n_blk, 1u);
+            if (k < 64) blks[k] = blk;
+        }
+    }
+    __syncthreads();
+    const uint32_t nbk = min(n_blk, 64u);
+    for (uint32_t q = 0; q < nbk; ++q) {
+        if (tid < PIX_B) {
+            const uint32_t s = blks[q] * PIX_B + tid;
+            if (pix_sel(t, s, len16, ctl->max_length) == best) {
+                const uint32_t k = atomicAdd(&ctl->n_cand, 1u);
+                if (k < MAX_CAND) ctl->cand_slot[k] = s;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t nc = ctl->n_cand;
+        if (n_lst > 64 || n_blk > 64 || nc > (uint32_t)MAX_CAND || nc == 0) {
+            ctl->status = PIX_HOST;
+            ctl->err = nc == 0 ? 10 : 4;
+            return;
+        }
+        if (ctl->next_id >= ctl->max_id) {
+            ctl->status = PIX_HOST;                                   // vocabulary limit
+            ctl->err = 5;
+            return;
+        }
+        // room for this merge's claims (<= 2 per site) within the table's fill limit
+        const uint32_t s0 = ctl->cand_slot[0];
+        unsigned long long room = 0;
+        for (uint32_t j = 0; j < nc; ++j) room = max(room, (unsigned long long)t.len[ctl->cand_slot[j]]);
+        if (ctl->used + 2 * room + 64 > ctl->used_cap) {
+            ctl->status = PIX_HOST;
+            ctl->err = 6;
+            return;
+        }
+        ctl->best = best;
+        ctl->W = (unsigned long long)W;
+        ctl->c = ctl->next_id;
+        ctl->tie = nc > 1;
+        ctl->pair_slot = s0;
+        ctl->a = (int32_t)(t.keys[s0] >> 16);
+        ctl->b = (int32_t)(t.keys[s0] & 0xFFFF);
+    }
+}
+
+// R3 (core.ts:296-305): among the tied pairs, the one whose last counted occurrence comes first.
+// Block j takes candidate j: the last valid slot of its list; for (x, x) the last counted one is
+// the last valid slot at an even offset of its run.  The last block to finish decides.
+__global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
+    if (ctl->status != PIX_RUN || !ctl->tie) return;
+    const uint32_t j = blockIdx.x;
+    const uint32_t nc = ctl->n_cand;
+    __shared__ unsigned long long red[4];
+    __shared__ bool last_block;
+    if (j < nc) {
+        const uint32_t s = ctl->cand_slot[j];
+        const int32_t u = (int32_t)(t.keys[s] >> 16), v = (int32_t)(t.keys[s] & 0xFFFF);
+        const uint32_t off = t.off[s], len = t.len[s];
+        unsigned long long m = 0;
+        for (uint32_t i = threadIdx.x; i < len; i += 256) {
+            const uint32_t p = B.pool[off + i];
+            if (C.tok[p] == u && pix_tok_is(C, C.nxt[p], v)) m = max(m, (unsigned long long)p + 1);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            m = max(max(red[0], red[1]), max(red[2], red[3]));
+            if (m && u == v) {
+                // offset of the last (x, x) slot in its run: odd -> the one before it is counted
+                uint32_t p = (uint32_t)(m - 1), q = p;
+                int k = 0;
+                while (k <= PIX_WALK && pix_tok_is(C, C.prv[q], u)) {
+                    q = C.prv[q];
+                    ++k;
+                }
+                if (k > PIX_WALK) pix_fail(ctl, 7);
+                if (k & 1) m = (unsigned long long)C.prv[p] + 1;
+            }
+            ctl->last[j] = m;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last_block = atomicAdd(&ctl->tie_done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last_block && threadIdx.x == 0 && ctl->status == PIX_RUN) {
+        __threadfence();
+        unsigned long long bp = ~0ull;
+        uint32_t bj = 0;
+        for (uint32_t q = 0; q < nc; ++q) {
+            const unsigned long long l = atomicAdd(&ctl->last[q], 0ull);
+            if (l && l < bp) {
+                bp = l;
+                bj = q;
+            }
+        }
+        if (bp == ~0ull) {
+            ctl->status = PIX_ERROR;
+            ctl->err = 8;
+            return;
+        }
+        const uint32_t s = ctl->cand_slot[bj];
+        ctl->pair_slot = s;
+        ctl->a = (int32_t)(t.keys[s] >> 16);
+        ctl->b = (int32_t)(t.keys[s] & 0xFFFF);
+    }
+}
+
+__device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uint32_t p) {
+    const uint32_t i = atomicAdd(&ctl->n_sites, 1u);
+    if (i < B.site_cap) B.sites[i] = p;
+    else pix_fail(ctl, 11);
+}
+
+// The merge sites.  a != b: every valid slot of the (a, b) list.  a == b: the runs of a, each
+// walked by the thread holding its head: sites at even offsets (replaceAll's left-to-right
+// matches), and the run's count changes: L a's become floor(L/2) c's (+ a trailing a when L is
+// odd), so (l, a) -> (l, c) on the left, (a, r) -> (c, r) on the right when L is even, (c, a)
+// when L is odd, and floor(m/2) pairs (c, c) for the m c's.
+__global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
+    if (ctl->status != PIX_RUN) return;
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    const uint32_t s = ctl->pair_slot;
+    const uint32_t off = t.off[s], len = t.len[s];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
+        const uint32_t p = B.pool[off + i];
+        if (C.tok[p] != a || !pix_tok_is(C, C.nxt[p], b)) continue;
+        if (a != b) {
+            pix_push_site(B, ctl, p);
+            continue;
+        }
+        const uint32_t l = C.prv[p];
+        if (pix_tok_is(C, l, a)) continue;             // not the head of its run
+        // walk the run: s_0 = p, s_1, ...; sites at even offsets followed by another a
+        uint32_t cur = p, prev_site = PIX_NONE;
+        uint32_t k = 0;
+        unsigned long long m = 0;
+        for (;;) {
+            const uint32_t nx = C.nxt[cur];
+            if (!pix_tok_is(C, nx, a)) break;
+            if ((k & 1u) == 0) {
+                pix_push_site(B, ctl, cur);
+                if (prev_site != PIX_NONE) pix_entry(t, B, ctl, c, c, prev_site, 0);
+                prev_site = cur;
+                ++m;
+            }
+            cur = nx;
+            if (++k > (uint32_t)PIX_WALK) {
+                pix_fail(ctl, 12);
+                return;
+            }
+        }
+        const uint32_t L = k + 1;                       // run length (cur = its last slot)
+        atomicAdd(&ctl->n_check, m);
+        if (l != PIX_NONE && C.tok[l] >= 0) {
+            pix_add(t, B, ctl, C.tok[l], a, -1);
+            pix_entry(t, B, ctl, C.tok[l], c, l, 1);
+        }
+        if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
+        if (L & 1u) {
+            pix_entry(t, B, ctl, c, a, prev_site, 1);   // the trailing a
+        } else {
+            const uint32_t r = C.nxt[cur];
+            if (r != PIX_NONE && C.tok[r] >= 0) {
+                pix_add(t, B, ctl, a, C.tok[r], -1);
+                pix_entry(t, B, ctl, c, C.tok[r], prev_site, 1);
+            }
+        }
+    }
+}
+
+// a != b: the count changes around each site p (q = next, l = prev of p, r = next of q).
+//   left adjacency: chained to a site ending at l -> (b, a) is lost and (c, c) is counted by the
+//   chain's head; else (l, a) -> (l, c), where l == a shortens a run of a's: one pair fewer when
+//   that run had even length;
+//   right adjacency (unless a site starts at r): (b, r) -> (c, r), likewise for a run of b's;
+//   a chain of m consecutive sites becomes m c's: floor(m/2) pairs (c, c).
+__global__ void __launch_bounds__(256) k_pix_delta(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
+    if (ctl->status != PIX_RUN) return;
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    if (a == b) return;
+    const uint32_t ns = min(ctl->n_sites, B.site_cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        const uint32_t p = B.sites[i];
+        const uint32_t q = C.nxt[p];
+        const uint32_t l = C.prv[p];
+        const uint32_t r = C.nxt[q];
+        const int32_t tl = l != PIX_NONE ? C.tok[l] : SEP;
+        const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
+        const bool lchain = tl == b && pix_tok_is(C, C.prv[l], a);
+        const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
+        if (lchain) {
+            pix_add(t, B, ctl, b, a, -1);
+        } else {
+            if (tl >= 0) {
+                if (tl == a) {
+                    uint32_t L = 1, x = l;
+                    while (pix_tok_is(C, x, a)) {
+                        ++L;
+                        x = C.prv[x];
+                        if (L > (uint32_t)PIX_WALK) {
+                            pix_fail(ctl, 13);
+                            return;
+                        }
+                    }
+                    if ((L & 1u) == 0) pix_add(t, B, ctl, a, a, -1);
+                } else {
+                    pix_add(t, B, ctl, tl, a, -1);
+                }
+                pix_entry(t, B, ctl, tl, c, l, 1);
+            }
+            // the head of a chain: its length, its (c, c) pairs
+            uint32_t m = 1, x = p;
+            for (;;) {
+                const uint32_t xr = C.nxt[C.nxt[x]];
+                if (!(pix_tok_is(C, xr, a) && pix_tok_is(C, C.nxt[xr], b))) break;
+                pix_entry(t, B, ctl, c, c, x, 0);
+                x = xr;
+                if (++m > (uint32_t)PIX_WALK) {
+                    pix_fail(ctl, 14);
+                    return;
+                }
+            }
+            if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
+        }
+        if (!rchain && tr >= 0) {
+            if (tr == b) {
+                uint32_t L = 1, x = r;
+                while (pix_tok_is(C, x, b)) {
+                    ++L;
+                    x = C.nxt[x];
+                    if (L > (uint32_t)PIX_WALK) {
+                        pix_fail(ctl, 15);
+                        return;
+                    }
+                }
+                if ((L & 1u) == 0) pix_add(t, B, ctl, b, b, -1);
+            } else {
+                pix_add(t, B, ctl, b, tr, -1);
+            }
+            pix_entry(t, B, ctl, c, tr, p, 1);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctl->n_check, (unsigned long long)ns);
+}
+
+// segments for this merge's new pairs, then their slots
+__global__ void k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
+    if (ctl->status != PIX_RUN) return;
+    const uint32_t nk = min(ctl->n_keys, B.key_cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
+        const uint32_t s = B.newkeys[i];
+        const unsigned long long o = atomicAdd(&ctl->pool_top, (unsigned long long)t.len[s]);
+        if (o + t.len[s] > ctl->pool_cap) {
+            pix_fail(ctl, 16);
+            continue;
+        }
+        t.off[s] = (uint32_t)o;
+        t.fill[s] = 0;
+    }
+}
+
+__global__ void k_pix_scatter(PixTable t, PixBufs B, PixCtl *ctl) {
+    if (ctl->status != PIX_RUN) return;
+    const uint32_t ne = min(ctl->n_ent, B.ent_cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += gridDim.x * blockDim.x) {
+        const uint2 e = B.ent[i];
+        const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
+        B.pool[t.off[e.x] + k] = e.y;
+    }
+}
+
+// the corpus rewrite: c at every site, its right slot merged away, the links around it.  The
+// merge is then logged; W must equal the sites found.
+__global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl,
+                                                   int32_t *len16, long long *log) {
+    if (ctl->status != PIX_RUN) return;
+    const unsigned long long W = ctl->W;
+    if (ctl->n_sites != W || ctl->n_check != W) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ctl->status = PIX_ERROR;
+            ctl->err = 20;
+        }
+        return;
+    }
+    const int32_t c = ctl->c;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)W; i += gridDim.x * blockDim.x) {
+        const uint32_t p = B.sites[i];
+        const uint32_t q = C.nxt[p];
+        const uint32_t r = C.nxt[q];
+        C.tok[p] = c;
+        C.tok[q] = TOMB;
+        C.nxt[p] = r;
+        if (r != PIX_NONE) C.prv[r] = p;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t s = ctl->pair_slot;
+        t.cnt[s] = 0;                                                   // every (a, b) merged
+        pix_mark(t, B, ctl, s);
+        const long long k = ctl->n_done;
+        log[3 * k] = ctl->a;
+        log[3 * k + 1] = ctl->b;
+        log[3 * k + 2] = (long long)W;
+        len16[c] = len16[ctl->a] + len16[ctl->b];                      // core.ts:318
+        ctl->n_done = k + 1;
+        ctl->next_id = c + 1;
+    }
+}
+
+// dense corpus back from the slot array: live slots (tokens and SEPs) in order
+__global__ void k_pix_live_flags(const int32_t *tok, uint32_t n, uint8_t *flag) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        flag[i] = tok[i] >= SEP;
+}
+
+}  // namespace bpe

@@ -206,6 +206,18 @@ int bpe_rank_loop_decide(bpe_ctx *ctx);
 int bpe_rank_loop_count(bpe_ctx *ctx);
 int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status);
 
+/* ---- modes -------------------------------------------------------------------------------------
+ * BPE_MODE_STREAM (default): every merge is one fused streaming pass over the corpus (apply the
+ * merge, recount every pair): the reference's own full recount (core.ts:265-310), at HBM rate.
+ * BPE_MODE_INCREMENTAL: bpe_merge_until works on a position index: per
+ * merge only the W match sites and their neighbours are touched, O(W) instead of O(N).  Same
+ * merges, counts and corpus; it changes what pair-scans/s measures, so it is reported apart.
+ * Built per call (one radix sort of the corpus); needs < 2^31 live slots.  Env BPE_PIX=1 selects
+ * it for new contexts.  Single-device contexts only. */
+#define BPE_MODE_STREAM 0
+#define BPE_MODE_INCREMENTAL 1
+int bpe_set_mode(bpe_ctx *ctx, int mode);
+
 /* ---- measurement -------------------------------------------------------------------------------
  * HIP-event timings of the kernels, recorded on the context's own stream. */
 typedef struct {
@@ -228,6 +240,9 @@ typedef struct {
                                  buckets, > BPE_MAX_CAND tied pairs, >= 2 tied pairs missing from
                                  the tail window, the vocabulary limit) */
     int64_t fused_passes;     /* merge passes that also refreshed the maintained cold-pair table */
+    int64_t pix_builds;       /* incremental mode: position-index builds (one sort of the corpus) */
+    int64_t pix_merges;       /* incremental mode: merges made on the index (O(W) each) */
+    int64_t pix_host;         /* incremental mode: iterations the index handed to the stream */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

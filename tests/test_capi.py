@@ -37,9 +37,23 @@ def test_library_loads_and_reports_no_device_without_gpu():
 
 
 def test_code_object_is_gfx950():
+    """Every device code object in the offload bundles is gfx950 (host-side library code may
+    name other targets in strings, so the bundle headers are parsed)."""
+    import struct
     data = open(pkg.LIB_PATH, 'rb').read()
-    assert b'hipv4-amdgcn-amd-amdhsa--gfx950' in data
-    assert b'gfx942' not in data and b'gfx90a' not in data
+    magic = b'__CLANG_OFFLOAD_BUNDLE__'
+    ids = []
+    i = data.find(magic)
+    while i >= 0:
+        n = struct.unpack_from('<Q', data, i + len(magic))[0]
+        q = i + len(magic) + 8
+        for _ in range(n):
+            _off, _size, idlen = struct.unpack_from('<QQQ', data, q)
+            ids.append(data[q + 24:q + 24 + idlen].decode())
+            q += 24 + idlen
+        i = data.find(magic, q)
+    dev = [x for x in ids if not x.startswith('host')]
+    assert dev and all(x.endswith('gfx950') for x in dev), ids
 
 
 def test_synthetic_generator_matches_oracle_and_jumps():

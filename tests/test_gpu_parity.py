@@ -269,6 +269,8 @@ def test_compaction_under_heavy_merging(mode):
     e, got = run_engine([sample], [1, 1], {}, mode=mode, stats=True)
     assert got == want
     assert e.samples() == st.samples()
+    if mode == 'pix':       # runs of 1.5M: the first merges walk too far and go to the stream
+        assert e.stats()['pix_host'] >= 1
 
 
 @pytest.mark.parametrize('mode', MODES)
@@ -349,6 +351,8 @@ def test_ties_resolved_from_the_corpus_tail(early, mode):
     assert [m[2] for m in got[:6]] == [200] * 6 and sorted(m[0] + m[1] for m in got[:6]) == [11] * 6
     assert e.samples() == st.samples()
     s = e.stats()
+    if mode == 'pix':       # every merge on the index, R3 from the candidates' lists
+        assert s['pix_merges'] == len(got) and s['pix_host'] == 0, s
     if mode == 'loop':
         assert s['exact_passes'] == 0, s
         if early == 0:      # every tie decided from the window

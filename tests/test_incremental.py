@@ -1,0 +1,111 @@
+"""The incremental mode (bpe_set_mode BPE_MODE_INCREMENTAL, csrc/bpe_pix.hip.h): mergeUntil on a
+position index, O(W) work per merge.  The same merges and corpus as the reference's full recount
+are required: against the oracle, against the streaming mode on corpora the oracle cannot finish,
+and across the hand-offs between the index and the stream.  (The randomized, golden, tie, run and
+compaction tests of test_gpu_parity.py run in this mode too: MODES includes 'pix'.)"""
+import random
+
+import numpy as np
+import pytest
+
+from bpe_amd import make_engine, pkg
+from oracle import CpuMT, OracleState
+from test_gpu_parity import check_sample_index, random_corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def _flat(samples):
+    ids = np.concatenate(samples).astype(np.int32) if samples else np.zeros(0, np.int32)
+    return ids, np.concatenate([[0], np.cumsum([len(s) for s in samples])]).astype(np.int64)
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_mixed_calls_and_option_changes(seed):
+    """mergeUntil on the index, single findNextMerge/applyMerge calls on the stream between, and
+    max_length changing from call to call (each call builds its index): the oracle's merges."""
+    rng = random.Random(900 + seed)
+    alphabet = rng.choice([3, 30, 256, 280])
+    samples = random_corpus(rng, rng.choice([30000, 400000]), alphabet, rng.choice([0.0, 0.3]),
+                            rng.choice([1, 9, 100]))
+    len16 = [rng.choice([1, 1, 2]) for _ in range(alphabet)]
+    ids, off = _flat(samples)
+    st = OracleState(ids, off, len16, alphabet)
+    e = make_engine(samples, len16)
+    e.set_mode('incremental')
+    e.stats_enable(True)
+    n_tok = alphabet
+    for step in range(6):
+        ml = rng.choice([0, 0, 4, 6])
+        if step % 2 == 0:
+            want = st.merge_until(ml, 2, 15)
+            got = e.merge_until(ml, 2, 15)
+            assert got == want, (step, got[:3], want[:3])
+            n_tok += len(got)
+        else:
+            w = st.merge_until(ml, 2, 1)
+            m = e.find_next_merge(ml, 2)
+            assert (m is None and not w) or [m] == w
+            if m is not None:
+                assert e.apply_merge(m[0], m[1], n_tok) == m[2]
+                n_tok += 1
+    assert e.samples() == st.samples()
+    check_sample_index(e, st.samples(), rng)
+    assert e.stats()['pix_merges'] > 0
+
+
+@pytest.mark.parametrize('n', [5, 9, 10, 1023, 70000, 300001])
+def test_runs_in_the_index(n):
+    """'x' * n between other tokens: runs walked by one thread up to PIX_WALK, longer ones handed
+    to the stream; x x merges, their (c, c) runs, trailing x's."""
+    sample = np.array([1] + [0] * n + [2, 0, 0, 0, 1], np.int32)
+    st = OracleState(sample, np.array([0, len(sample)], np.int64), [1, 1, 1], 3)
+    want = st.merge_until(0, 2, 0)
+    e = make_engine([sample], [1, 1, 1])
+    e.set_mode('incremental')
+    e.stats_enable(True)
+    assert e.merge_until(0, 2, 0) == want
+    assert e.samples() == st.samples()
+    s = e.stats()
+    assert s['pix_merges'] > 0
+    if n > 1 << 16:
+        assert s['pix_host'] >= 1
+
+
+def test_uniform_c3_slice_matches_the_stream():
+    """A 32 MiB slice of BASELINE config 3, 2500 merges: the incremental mode against the
+    streaming mode and the multi-threaded CPU restatement (first 300 merges)."""
+    data = pkg.synth_latin1(32 << 20, seed=12345, A=256, base=0)
+    a = pkg.Engine(0)
+    a.add_latin1(data, sample_bytes=1 << 20)
+    b = pkg.Engine(0)
+    cmap, nt, _ = b.add_latin1(data, sample_bytes=1 << 20)
+    b.set_mode('incremental')
+    b.stats_enable(True)
+    want = a.merge_until(0, 2, 2500)
+    got = b.merge_until(0, 2, 2500)
+    assert got == want
+    s = b.stats()
+    assert s['pix_merges'] == 2500 and s['pix_host'] == 0, s
+    ia, oa = a.read_corpus()
+    ib, ob = b.read_corpus()
+    assert np.array_equal(ia, ib) and np.array_equal(oa, ob)
+    ids = cmap[data]
+    off = np.arange(0, len(data) + 1, 1 << 20, dtype=np.int64)
+    cpu = CpuMT(ids, off, [1] * nt, nt, threads=8)
+    assert cpu.merge_until(0, 2, 300) == got[:300]
+    cpu.close()
+
+
+def test_zipf_words_match_the_stream():
+    """Skewed corpus (Zipf words): long merged tokens, cold pairs, runs of merged tokens."""
+    data = pkg.synth_zipf(8 << 20, seed=3)
+    a = pkg.Engine(0)
+    a.add_latin1(data, sample_bytes=1 << 20)
+    b = pkg.Engine(0)
+    b.add_latin1(data, sample_bytes=1 << 20)
+    b.set_mode('incremental')
+    want = a.merge_until(0, 2, 1500)
+    got = b.merge_until(0, 2, 1500)
+    assert got == want
+    assert np.array_equal(a.read_corpus()[0], b.read_corpus()[0])
