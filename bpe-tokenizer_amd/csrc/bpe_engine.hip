@@ -10,11 +10,10 @@
 // so a mergeUntil iteration streams the corpus exactly once.
 #include "bpe_kernels.hip.h"
 #include "bpe_pix.hip.h"
+#include "bpe_pixlib.h"
 #include "bpe.h"
 #include "bpe_multi.h"
 #include "bpe_tools.h"
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstddef>
@@ -1448,32 +1447,32 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
         HIP_TRY(hipGetLastError());
         // temp storage for every library call below
         size_t tb = 0, t1 = 0;
-        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, A, Bk, V, B.pool, N, 0, 32, s));
+        HIP_TRY(pixlib_sort_pairs(nullptr, t1, A, Bk, V, B.pool, N, s));
         tb = std::max(tb, t1);
-        HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, t1, runmark, run_start, hipcub::Max(), N, s));
+        HIP_TRY(pixlib_max_scan(nullptr, t1, runmark, run_start, N, s));
         tb = std::max(tb, t1);
-        HIP_TRY(hipcub::DeviceReduce::ReduceByKey(nullptr, t1, Bk, V, A, R, d_nruns, hipcub::Sum(), N, s));
+        HIP_TRY(pixlib_reduce_by_key(nullptr, t1, Bk, V, A, R, d_nruns, N, s));
         tb = std::max(tb, t1);
-        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, t1, Bk, A, D, d_nruns + 1, N, s));
+        HIP_TRY(pixlib_run_lengths(nullptr, t1, Bk, A, D, d_nruns + 1, N, s));
         tb = std::max(tb, t1);
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, D, Bk, N, s));
+        HIP_TRY(pixlib_exclusive_sum(nullptr, t1, D, Bk, N, s));
         tb = std::max(tb, t1);
         void *tmp;
         if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
-        HIP_TRY(hipcub::DeviceScan::InclusiveScan(tmp, tb, runmark, run_start, hipcub::Max(), N, s));
-        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, A, Bk, V, B.pool, N, 0, 32, s));
+        HIP_TRY(pixlib_max_scan(tmp, tb, runmark, run_start, N, s));
+        HIP_TRY(pixlib_sort_pairs(tmp, tb, A, Bk, V, B.pool, N, s));
         // A: counted flags in sorted order; then per pair (V: keys, R: counts)
         k_pix_build_counted<<<4096, 256, 0, s>>>(C, B.pool, run_start, A);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipcub::DeviceReduce::ReduceByKey(tmp, tb, Bk, V, A, R, d_nruns, hipcub::Sum(), N, s));
+        HIP_TRY(pixlib_reduce_by_key(tmp, tb, Bk, V, A, R, d_nruns, N, s));
         // (A: keys again, D: list lengths, Bk: list offsets)
-        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(tmp, tb, Bk, A, D, d_nruns + 1, N, s));
+        HIP_TRY(pixlib_run_lengths(tmp, tb, Bk, A, D, d_nruns + 1, N, s));
         uint32_t nruns[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(nruns, d_nruns, sizeof nruns, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (nruns[0] != nruns[1] || nruns[0] == 0 || nruns[0] > N)
             return fail(BPE_ERR_STATE, "bpe native: position index: bad pair runs");
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, D, Bk, nruns[0], s));
+        HIP_TRY(pixlib_exclusive_sum(tmp, tb, D, Bk, nruns[0], s));
         // the pair table: room for the current pairs and the ones merges will add
         uint64_t cap = 1u << 20;
         while (cap < 4ull * nruns[0] || cap < (uint64_t)N / 8) cap <<= 1;
@@ -1544,11 +1543,11 @@ int pix_finish(bpe_ctx *c) {
         if ((rc = t.get(&flag, N)) || (rc = t.get(&d_nsel, 1))) return rc;
         k_pix_live_flags<<<4096, 256, 0, s>>>(c->d_ids, N, flag);
         size_t tb = 0;
-        HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
+        HIP_TRY(pixlib_select_flagged(nullptr, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
         void *tmp;
         if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
-        HIP_TRY(hipcub::DeviceSelect::Flagged(tmp, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
+        HIP_TRY(pixlib_select_flagged(tmp, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
         uint32_t nsel = 0;
         HIP_TRY(hipMemcpyAsync(&nsel, d_nsel, sizeof nsel, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
