@@ -87,6 +87,45 @@ def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
                       % (sample_mib, it_mt, dt_mt, used, it_1, dt_1)}
 
 
+def incremental_mode(args, stream_merges):
+    """The same workload in the incremental mode (bpe_set_mode BPE_MODE_INCREMENTAL: mergeUntil on
+    a position index, O(W) work per merge), on a fresh copy of the corpus:
+    the W warmup merges untimed, then the K timed ones in one mergeUntil call, whose time includes
+    the index build.  Reported apart from `value`, as the survey asks: its pair-scans are the
+    reference's definition, not the work done.  The merge log must equal the streaming run's."""
+    pkg = importlib.import_module('bpe-tokenizer_amd')
+    n = args.corpus_mib << 20
+    base = 0 if args.alphabet == 256 else 0x20
+    data = (pkg.synth_zipf(n, seed=12345) if args.corpus == 'zipf' else
+            pkg.synth_latin1(n, seed=12345, A=args.alphabet, base=base))
+    e = pkg.Engine(0)
+    e.add_latin1(data, sample_bytes=1 << 20)
+    del data
+    e.set_mode('incremental')
+    e.merge_until(0, 2, args.warmup)
+    live0 = e.corpus_size()[1]
+    e.stats_enable(True)
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    got = e.merge_until(0, 2, args.steps)
+    dt = time.perf_counter() - t0
+    scans, live = 0, live0
+    for m in got:
+        scans += live
+        live -= m[2]
+    st = e.stats()
+    e.close()
+    same = [tuple(map(int, m)) for m in got] == [tuple(map(int, m)) for m in stream_merges]
+    return {'what': 'mergeUntil on the position index (csrc/bpe_pix.hip.h), one call of the K '
+                    'timed merges, index build included',
+            'ms_per_step': dt * 1e3 / max(1, len(got)), 'seconds': dt,
+            'equiv_pair_scans_per_s': scans / dt, 'speedup_vs_stream_loop': None,
+            'merges': len(got), 'identical_merges_to_stream': same,
+            'index_builds': st['pix_builds'], 'merges_on_index': st['pix_merges'],
+            'handed_to_stream': st['pix_host']}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -99,6 +138,8 @@ def main():
     ap.add_argument('--cpu-sample-mib', type=int, default=256)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-incremental', action='store_true',
+                    help='skip the incremental-mode measurement reported beside the line')
     args = ap.parse_args()
 
     import torch
@@ -218,6 +259,10 @@ def main():
                 'exact_passes': st['exact_passes'],
             },
         }
+        if world == 1 and not args.no_incremental:
+            inc = incremental_mode(args, merges)
+            inc['speedup_vs_stream_loop'] = (dt * 1e3 / args.steps) / inc['ms_per_step']
+            out['incremental_mode'] = inc
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s, args.corpus)
         print(json.dumps(out), flush=True)

@@ -1480,6 +1480,8 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
         P->cap = cap;
         PixTable &T = P->T;
         T.mask = (uint32_t)(cap - 1);
+        T.len16 = c->d_len16;
+        T.ml = max_length;
         T.nblocks = (uint32_t)(cap / PIX_B);
         T.nsuper = (T.nblocks + PIX_SB - 1) / PIX_SB;
         if ((rc = pix_alloc(P, &T.keys, cap)) || (rc = pix_alloc(P, &T.cnt, cap)) ||
@@ -1515,7 +1517,7 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
         h->used_cap = cap / 10 * 7;
         HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
         k_pix_build_insert<<<4096, 256, 0, s>>>(T, P->d_ctl, A, R, D, Bk, d_nruns);
-        k_pix_bmax<<<4096, 256, 0, s>>>(T, B, P->d_ctl, c->d_len16, 1);
+        k_pix_bmax_all<<<4096, 256, 0, s>>>(T);
         k_pix_sbmax<<<1024, 256, 0, s>>>(T, B, P->d_ctl, 1);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
@@ -1591,16 +1593,14 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
         int status = PIX_HOST;
         int64_t nd = 0;
         if (want > 0) {
+            P->T.len16 = c->d_len16;   // (ensure_len16_cap may have moved it)
             k_pix_begin<<<1, 1, 0, s>>>(P->d_ctl, want, (int32_t)base, mw);
             for (int64_t i = 0; i < want; ++i) {
                 k_pix_select<<<1, 1024, 0, s>>>(P->T, P->d_ctl, c->d_len16);
-                k_pix_tie<<<MAX_CAND, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
+                k_pix_tie<<<MAX_CAND * PIX_TIE_SPLIT, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
                 k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
-                k_pix_delta<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
-                k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
-                k_pix_scatter<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+                k_pix_alloc<<<64, 256, 0, s>>>(P->T, P->B, P->d_ctl);
                 k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, c->d_len16, P->d_log);
-                k_pix_bmax<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->d_len16, 0);
                 k_pix_sbmax<<<256, 256, 0, s>>>(P->T, P->B, P->d_ctl, 0);
             }
             HIP_TRY(hipGetLastError());

@@ -18,13 +18,13 @@
 // One merge (a, b) -> c, every kernel reading the decision from PixCtl (no host round trip):
 //   k_pix_select   best key, candidates, W, min_weight / vocabulary checks
 //   k_pix_tie      R3 over the candidates' lists (only with a tie)
-//   k_pix_sites    the merge sites from the (a, b) list; for a == b the runs, walked from their
-//                  heads (sites at even offsets, replaceAll's left-to-right rule), with their
-//                  count changes
-//   k_pix_delta    a != b: count changes around each site, the adjacencies of c
-//   k_pix_alloc / k_pix_scatter   segments for the new pairs (all contain c), their slots
-//   k_pix_apply    tokens and links (the only kernel that changes the corpus)
-//   k_pix_bmax / k_pix_sbmax      the two-level max over the touched blocks
+//   k_pix_sites    the merge sites from the (a, b) list and the count changes around them (for
+//                  a == b the runs, walked from their heads: sites at even offsets, replaceAll's
+//                  left-to-right rule); the new adjacencies, all of which contain c
+//   k_pix_alloc    segments for the new pairs
+//   k_pix_apply    tokens and links (the only kernel that changes the corpus), the new pairs'
+//                  slots into their segments, the maxima of the touched blocks
+//   k_pix_sbmax    the superblock maxima over them
 // Anything the index cannot do in bounded work (a run or chain longer than PIX_WALK, a full
 // buffer, more than MAX_CAND tied pairs) sets PIX_HOST before k_pix_apply: the corpus is still
 // that of the last completed merge, and the host takes the iteration on the streaming path.
@@ -50,6 +50,8 @@ struct PixCorpus {
 };
 
 struct PixTable {
+    const int32_t *len16;    // UTF-16 lengths (max_length filter)
+    long long ml;            // max_length of this index's selections
     uint32_t *keys;
     unsigned long long *cnt;
     uint32_t *off, *len, *fill;
@@ -95,16 +97,17 @@ __device__ __forceinline__ uint32_t pix_hash(uint32_t key) {
     return h ^ (h >> 15);
 }
 
-// the packed selection key of a table slot (0: no pair, empty, or filtered by max_length)
-__device__ __forceinline__ unsigned long long pix_sel(const PixTable &t, uint32_t s,
-                                                      const int32_t *len16, long long ml) {
-    const uint32_t k = t.keys[s];
-    if (k == PIX_NONE) return 0;
-    const unsigned long long w = t.cnt[s];
-    if (w == 0 || ml < 0) return 0;
+// the packed selection key of pair `k` with count w (0: no pair, or filtered by max_length)
+__device__ __forceinline__ unsigned long long pix_sel_of(const PixTable &t, uint32_t k,
+                                                         unsigned long long w) {
+    if (k == PIX_NONE || w == 0 || (long long)w < 0 || t.ml < 0) return 0;
     const int32_t u = (int32_t)(k >> 16), v = (int32_t)(k & 0xFFFF);
-    if (ml > 0 && (long long)len16[u] + len16[v] > ml) return 0;      // core.ts:270-273
-    return (w << 17) | (unsigned long long)(0x1FFFF - (u + v));        // core.ts:294-305
+    if (t.ml > 0 && (long long)t.len16[u] + t.len16[v] > t.ml) return 0;   // core.ts:270-273
+    return (w << 17) | (unsigned long long)(0x1FFFF - (u + v));             // core.ts:294-305
+}
+
+__device__ __forceinline__ unsigned long long pix_sel(const PixTable &t, uint32_t s) {
+    return pix_sel_of(t, t.keys[s], t.cnt[s]);
 }
 
 __device__ __forceinline__ void pix_mark(const PixTable &t, const PixBufs &B, PixCtl *ctl,
@@ -140,22 +143,32 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
     return PIX_NONE;
 }
 
-// count change of an existing or new pair
+// Count change of an existing or new pair, keeping the block maxima exact.  Only new pairs (they
+// all contain c) rise: k_pix_alloc lifts their block's and superblock's max once per pair.  A fall
+// only matters to the entry that was its block's max, whose block is then recomputed after the
+// merge (k_pix_apply).
 __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
                                             int32_t u, int32_t v, long long d) {
-    const uint32_t s = pix_slot(t, ctl, pix_key(u, v), true);
+    const uint32_t key = pix_key(u, v);
+    const uint32_t s = pix_slot(t, ctl, key, true);
     if (s == PIX_NONE) {
         pix_fail(ctl, 1);
         return s;
     }
-    if (d) atomicAdd(&t.cnt[s], (unsigned long long)d);
-    pix_mark(t, B, ctl, s);
+    if (d == 0) return s;
+    const unsigned long long old = atomicAdd(&t.cnt[s], (unsigned long long)d);
+    if (d < 0) {
+        const unsigned long long sel = pix_sel_of(t, key, old);
+        if (sel && sel >= t.bmax[s / PIX_B]) pix_mark(t, B, ctl, s);
+    }
     return s;
 }
 
-// a new adjacency (u, v) at slot pos (u or v is c): list entry + one more slot in its segment
+// A new adjacency (u, v) at slot pos (u or v is c): its count, one more slot in its segment, the
+// entry at index e of this merge's entry list (e = ~0u: the next free one).
 __device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
-                                          int32_t u, int32_t v, uint32_t pos, long long d) {
+                                          int32_t u, int32_t v, uint32_t pos, long long d,
+                                          uint32_t e = ~0u) {
     const uint32_t s = pix_add(t, B, ctl, u, v, d);
     if (s == PIX_NONE) return;
     if (atomicAdd(&t.len[s], 1u) == 0u) {
@@ -163,7 +176,7 @@ __device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, P
         if (k < B.key_cap) B.newkeys[k] = s;
         else pix_fail(ctl, 2);
     }
-    const uint32_t e = atomicAdd(&ctl->n_ent, 1u);
+    if (e == ~0u) e = atomicAdd(&ctl->n_ent, 1u);
     if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos);
     else pix_fail(ctl, 3);
 }
@@ -214,31 +227,39 @@ __global__ void k_pix_build_insert(PixTable t, PixCtl *ctl, const uint32_t *uniq
     }
 }
 
-// block maxima of every block (build) or of the touched ones (after a merge)
-__global__ void __launch_bounds__(256) k_pix_bmax(PixTable t, PixBufs B, PixCtl *ctl,
-                                                  const int32_t *len16, int all) {
-    const uint32_t nb = all ? t.nblocks : min(ctl->n_dblocks, t.nblocks);
-    if (!all && ctl->status != PIX_RUN) return;
-    __shared__ unsigned long long red[4];
-    for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
-        const uint32_t blk = all ? i : B.dblocks[i];
-        const unsigned long long v = pix_sel(t, blk * PIX_B + threadIdx.x, len16, ctl->max_length);
-        unsigned long long m = v;
+// Block maxima: of every block (build), or recomputed for the blocks whose max entry fell
+// (after a merge; one wave per block).  A block whose max fell may take its superblock's max
+// with it: that superblock is recomputed next (k_pix_sbmax).
+__global__ void __launch_bounds__(256) k_pix_bmax_all(PixTable t) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t blk = blockIdx.x * 4 + (threadIdx.x >> 6); blk < t.nblocks; blk += gridDim.x * 4) {
+        unsigned long long m = 0;
+        for (int k = lane; k < PIX_B; k += 64) m = max(m, pix_sel(t, blk * PIX_B + k));
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            m = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (lane == 0) t.bmax[blk] = m;
+    }
+}
+
+__device__ __forceinline__ void pix_bmax_dirty(const PixTable &t, const PixBufs &B, PixCtl *ctl) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nb = min(ctl->n_dblocks, t.nblocks);
+    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nb; i += gridDim.x * 4) {
+        const uint32_t blk = B.dblocks[i];
+        unsigned long long m = 0;
+        for (int k = lane; k < PIX_B; k += 64) m = max(m, pix_sel(t, blk * PIX_B + k));
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+        if (lane == 0) {
+            const unsigned long long old = t.bmax[blk];
             t.bmax[blk] = m;
             t.bdirty[blk] = 0;
             const uint32_t sb = blk / PIX_SB;
-            if (!all && atomicExch(&t.sbdirty[sb], 1u) == 0u) {
+            if (m < old && old >= t.sbmax[sb] && atomicExch(&t.sbdirty[sb], 1u) == 0u) {
                 const uint32_t k = atomicAdd(&ctl->n_dsuper, 1u);
                 if (k < t.nsuper) B.dsuper[k] = sb;
             }
         }
-        __syncthreads();
     }
 }
 
@@ -287,6 +308,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixCtl *ctl, co
         ctl->tie = 0;
         ctl->tie_done = 0;
         ctl->n_check = 0;
+        for (int q = 0; q < MAX_CAND; ++q) ctl->last[q] = 0;
         n_lst = n_blk = 0;
     }
     if (ctl->n_done >= ctl->n_want) {
@@ -327,7 +349,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixCtl *ctl, co
     for (uint32_t q = 0; q < nbk; ++q) {
         if (tid < PIX_B) {
             const uint32_t s = blks[q] * PIX_B + tid;
-            if (pix_sel(t, s, len16, ctl->max_length) == best) {
+            if (pix_sel(t, s) == best) {
                 const uint32_t k = atomicAdd(&ctl->n_cand, 1u);
                 if (k < MAX_CAND) ctl->cand_slot[k] = s;
             }
@@ -366,11 +388,13 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixCtl *ctl, co
 }
 
 // R3 (core.ts:296-305): among the tied pairs, the one whose last counted occurrence comes first.
-// Block j takes candidate j: the last valid slot of its list; for (x, x) the last counted one is
-// the last valid slot at an even offset of its run.  The last block to finish decides.
+// PIX_TIE_SPLIT blocks per candidate find the last valid slot of its list (atomicMax); the last
+// block to finish turns it into the last counted one (for (x, x): the last valid slot at an even
+// offset of its run) and decides.
+constexpr int PIX_TIE_SPLIT = 16;
 __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
     if (ctl->status != PIX_RUN || !ctl->tie) return;
-    const uint32_t j = blockIdx.x;
+    const uint32_t j = blockIdx.x / PIX_TIE_SPLIT, part = blockIdx.x % PIX_TIE_SPLIT;
     const uint32_t nc = ctl->n_cand;
     __shared__ unsigned long long red[4];
     __shared__ bool last_block;
@@ -379,7 +403,7 @@ __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBuf
         const int32_t u = (int32_t)(t.keys[s] >> 16), v = (int32_t)(t.keys[s] & 0xFFFF);
         const uint32_t off = t.off[s], len = t.len[s];
         unsigned long long m = 0;
-        for (uint32_t i = threadIdx.x; i < len; i += 256) {
+        for (uint32_t i = part * 256 + threadIdx.x; i < len; i += PIX_TIE_SPLIT * 256) {
             const uint32_t p = B.pool[off + i];
             if (C.tok[p] == u && pix_tok_is(C, C.nxt[p], v)) m = max(m, (unsigned long long)p + 1);
         }
@@ -389,18 +413,7 @@ __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBuf
         __syncthreads();
         if (threadIdx.x == 0) {
             m = max(max(red[0], red[1]), max(red[2], red[3]));
-            if (m && u == v) {
-                // offset of the last (x, x) slot in its run: odd -> the one before it is counted
-                uint32_t p = (uint32_t)(m - 1), q = p;
-                int k = 0;
-                while (k <= PIX_WALK && pix_tok_is(C, C.prv[q], u)) {
-                    q = C.prv[q];
-                    ++k;
-                }
-                if (k > PIX_WALK) pix_fail(ctl, 7);
-                if (k & 1) m = (unsigned long long)C.prv[p] + 1;
-            }
-            ctl->last[j] = m;
+            if (m) atomicMax(&ctl->last[j], m);
         }
     }
     __syncthreads();
@@ -409,27 +422,119 @@ __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBuf
         last_block = atomicAdd(&ctl->tie_done, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last_block && threadIdx.x == 0 && ctl->status == PIX_RUN) {
-        __threadfence();
-        unsigned long long bp = ~0ull;
-        uint32_t bj = 0;
-        for (uint32_t q = 0; q < nc; ++q) {
-            const unsigned long long l = atomicAdd(&ctl->last[q], 0ull);
-            if (l && l < bp) {
-                bp = l;
-                bj = q;
+    if (!(last_block && threadIdx.x == 0 && ctl->status == PIX_RUN)) return;
+    __threadfence();
+    unsigned long long bp = ~0ull;
+    uint32_t bj = 0;
+    for (uint32_t q = 0; q < nc; ++q) {
+        unsigned long long m = atomicAdd(&ctl->last[q], 0ull);
+        const uint32_t s = ctl->cand_slot[q];
+        const int32_t u = (int32_t)(t.keys[s] >> 16), v = (int32_t)(t.keys[s] & 0xFFFF);
+        if (m && u == v) {
+            // offset of the last (x, x) slot in its run: odd -> the one before it is counted
+            const uint32_t p = (uint32_t)(m - 1);
+            uint32_t x = p;
+            int k = 0;
+            while (k <= PIX_WALK && pix_tok_is(C, C.prv[x], u)) {
+                x = C.prv[x];
+                ++k;
+            }
+            if (k > PIX_WALK) {
+                pix_fail(ctl, 7);
+                return;
+            }
+            if (k & 1) m = (unsigned long long)C.prv[p] + 1;
+        }
+        if (m && m < bp) {
+            bp = m;
+            bj = q;
+        }
+    }
+    if (bp == ~0ull) {
+        ctl->status = PIX_ERROR;
+        ctl->err = 8;
+        return;
+    }
+    const uint32_t s = ctl->cand_slot[bj];
+    ctl->pair_slot = s;
+    ctl->a = (int32_t)(t.keys[s] >> 16);
+    ctl->b = (int32_t)(t.keys[s] & 0xFFFF);
+}
+
+// a != b: the count changes around each site p (q = next, l = prev of p, r = next of q).
+//   left adjacency: chained to a site ending at l -> (b, a) is lost and (c, c) is counted by the
+//   chain's head; else (l, a) -> (l, c), where l == a shortens a run of a's: one pair fewer when
+//   that run had even length;
+//   right adjacency (unless a site starts at r): (b, r) -> (c, r), likewise for a run of b's;
+//   a chain of m consecutive sites becomes m c's: floor(m/2) pairs (c, c).
+__device__ void pix_site_delta(const PixCorpus &C, const PixTable &t, const PixBufs &B,
+                               PixCtl *ctl, uint32_t p, uint32_t idx, int32_t a, int32_t b,
+                               int32_t c) {
+    const uint32_t q = C.nxt[p];
+    const uint32_t l = C.prv[p];
+    const uint32_t r = C.nxt[q];
+    const int32_t tl = l != PIX_NONE ? C.tok[l] : SEP;
+    const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
+    const bool lchain = tl == b && pix_tok_is(C, C.prv[l], a);
+    const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
+    // this site's entries: [2 idx] its left adjacency, [2 idx + 1] its right one
+    bool left_done = false, right_done = false;
+    if (lchain) {
+        pix_add(t, B, ctl, b, a, -1);
+        pix_entry(t, B, ctl, c, c, C.prv[l], 0, 2 * idx);      // (c, c) from the site before
+        left_done = true;
+    } else {
+        if (tl >= 0) {
+            if (tl == a) {
+                uint32_t L = 1, x = l;
+                while (pix_tok_is(C, x, a)) {
+                    ++L;
+                    x = C.prv[x];
+                    if (L > (uint32_t)PIX_WALK) {
+                        pix_fail(ctl, 13);
+                        return;
+                    }
+                }
+                if ((L & 1u) == 0) pix_add(t, B, ctl, a, a, -1);
+            } else {
+                pix_add(t, B, ctl, tl, a, -1);
+            }
+            pix_entry(t, B, ctl, tl, c, l, 1, 2 * idx);
+            left_done = true;
+        }
+        // the head of a chain: its length m, floor(m/2) pairs (c, c)
+        uint32_t m = 1, x = p;
+        for (;;) {
+            const uint32_t xr = C.nxt[C.nxt[x]];
+            if (!(pix_tok_is(C, xr, a) && pix_tok_is(C, C.nxt[xr], b))) break;
+            x = xr;
+            if (++m > (uint32_t)PIX_WALK) {
+                pix_fail(ctl, 14);
+                return;
             }
         }
-        if (bp == ~0ull) {
-            ctl->status = PIX_ERROR;
-            ctl->err = 8;
-            return;
-        }
-        const uint32_t s = ctl->cand_slot[bj];
-        ctl->pair_slot = s;
-        ctl->a = (int32_t)(t.keys[s] >> 16);
-        ctl->b = (int32_t)(t.keys[s] & 0xFFFF);
+        if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
     }
+    if (!rchain && tr >= 0) {
+        if (tr == b) {
+            uint32_t L = 1, x = r;
+            while (pix_tok_is(C, x, b)) {
+                ++L;
+                x = C.nxt[x];
+                if (L > (uint32_t)PIX_WALK) {
+                    pix_fail(ctl, 15);
+                    return;
+                }
+            }
+            if ((L & 1u) == 0) pix_add(t, B, ctl, b, b, -1);
+        } else {
+            pix_add(t, B, ctl, b, tr, -1);
+        }
+        pix_entry(t, B, ctl, c, tr, p, 1, 2 * idx + 1);
+        right_done = true;
+    }
+    if (!left_done && 2 * idx < B.ent_cap) B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
+    if (!right_done && 2 * idx + 1 < B.ent_cap) B.ent[2 * idx + 1] = make_uint2(PIX_NONE, 0);
 }
 
 __device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uint32_t p) {
@@ -438,7 +543,8 @@ __device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uin
     else pix_fail(ctl, 11);
 }
 
-// The merge sites.  a != b: every valid slot of the (a, b) list.  a == b: the runs of a, each
+// The merge sites and their count changes.  a != b: every valid slot of the (a, b) list, each
+// with pix_site_delta.  a == b: the runs of a, each
 // walked by the thread holding its head: sites at even offsets (replaceAll's left-to-right
 // matches), and the run's count changes: L a's become floor(L/2) c's (+ a trailing a when L is
 // odd), so (l, a) -> (l, c) on the left, (a, r) -> (c, r) on the right when L is even, (c, a)
@@ -448,13 +554,33 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
     const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
     const uint32_t s = ctl->pair_slot;
     const uint32_t off = t.off[s], len = t.len[s];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // every (a, b) is merged (no count change below touches the pair itself)
+        t.cnt[s] = 0;
+        pix_mark(t, B, ctl, s);           // (it was the global max: its block is recomputed)
+    }
+    const int lane = threadIdx.x & 63;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
         const uint32_t p = B.pool[off + i];
-        if (C.tok[p] != a || !pix_tok_is(C, C.nxt[p], b)) continue;
+        const bool valid = C.tok[p] == a && pix_tok_is(C, C.nxt[p], b);
         if (a != b) {
-            pix_push_site(B, ctl, p);
+            // one atomic per wave for the site indices
+            const unsigned long long mask = __ballot(valid);
+            if (!valid) continue;
+            const int leader = __ffsll((long long)mask) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&ctl->n_sites, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            const uint32_t idx = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+            if (idx >= B.site_cap) {
+                pix_fail(ctl, 11);
+                continue;
+            }
+            B.sites[idx] = p;
+            pix_site_delta(C, t, B, ctl, p, idx, a, b, c);
             continue;
         }
+        if (!valid) continue;
         const uint32_t l = C.prv[p];
         if (pix_tok_is(C, l, a)) continue;             // not the head of its run
         // walk the run: s_0 = p, s_1, ...; sites at even offsets followed by another a
@@ -495,114 +621,51 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
     }
 }
 
-// a != b: the count changes around each site p (q = next, l = prev of p, r = next of q).
-//   left adjacency: chained to a site ending at l -> (b, a) is lost and (c, c) is counted by the
-//   chain's head; else (l, a) -> (l, c), where l == a shortens a run of a's: one pair fewer when
-//   that run had even length;
-//   right adjacency (unless a site starts at r): (b, r) -> (c, r), likewise for a run of b's;
-//   a chain of m consecutive sites becomes m c's: floor(m/2) pairs (c, c).
-__global__ void __launch_bounds__(256) k_pix_delta(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
-    if (ctl->status != PIX_RUN) return;
-    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
-    if (a == b) return;
-    const uint32_t ns = min(ctl->n_sites, B.site_cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
-        const uint32_t p = B.sites[i];
-        const uint32_t q = C.nxt[p];
-        const uint32_t l = C.prv[p];
-        const uint32_t r = C.nxt[q];
-        const int32_t tl = l != PIX_NONE ? C.tok[l] : SEP;
-        const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
-        const bool lchain = tl == b && pix_tok_is(C, C.prv[l], a);
-        const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
-        if (lchain) {
-            pix_add(t, B, ctl, b, a, -1);
-        } else {
-            if (tl >= 0) {
-                if (tl == a) {
-                    uint32_t L = 1, x = l;
-                    while (pix_tok_is(C, x, a)) {
-                        ++L;
-                        x = C.prv[x];
-                        if (L > (uint32_t)PIX_WALK) {
-                            pix_fail(ctl, 13);
-                            return;
-                        }
-                    }
-                    if ((L & 1u) == 0) pix_add(t, B, ctl, a, a, -1);
-                } else {
-                    pix_add(t, B, ctl, tl, a, -1);
-                }
-                pix_entry(t, B, ctl, tl, c, l, 1);
-            }
-            // the head of a chain: its length, its (c, c) pairs
-            uint32_t m = 1, x = p;
-            for (;;) {
-                const uint32_t xr = C.nxt[C.nxt[x]];
-                if (!(pix_tok_is(C, xr, a) && pix_tok_is(C, C.nxt[xr], b))) break;
-                pix_entry(t, B, ctl, c, c, x, 0);
-                x = xr;
-                if (++m > (uint32_t)PIX_WALK) {
-                    pix_fail(ctl, 14);
-                    return;
-                }
-            }
-            if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
-        }
-        if (!rchain && tr >= 0) {
-            if (tr == b) {
-                uint32_t L = 1, x = r;
-                while (pix_tok_is(C, x, b)) {
-                    ++L;
-                    x = C.nxt[x];
-                    if (L > (uint32_t)PIX_WALK) {
-                        pix_fail(ctl, 15);
-                        return;
-                    }
-                }
-                if ((L & 1u) == 0) pix_add(t, B, ctl, b, b, -1);
-            } else {
-                pix_add(t, B, ctl, b, tr, -1);
-            }
-            pix_entry(t, B, ctl, c, tr, p, 1);
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctl->n_check, (unsigned long long)ns);
-}
-
-// segments for this merge's new pairs, then their slots
-__global__ void k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
+// segments for this merge's new pairs (one pool atomic per wave)
+__global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
     if (ctl->status != PIX_RUN) return;
     const uint32_t nk = min(ctl->n_keys, B.key_cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += gridDim.x * blockDim.x) {
-        const uint32_t s = B.newkeys[i];
-        const unsigned long long o = atomicAdd(&ctl->pool_top, (unsigned long long)t.len[s]);
-        if (o + t.len[s] > ctl->pool_cap) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < nk; i0 += stride) {
+        const uint32_t i = i0 + lane;
+        const uint32_t s = i < nk ? B.newkeys[i] : 0;
+        const unsigned long long len = i < nk ? t.len[s] : 0;
+        unsigned long long incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        unsigned long long base = 0;
+        if (lane == 63) base = atomicAdd(&ctl->pool_top, incl);
+        base = __shfl(base, 63);
+        if (i >= nk) continue;
+        const unsigned long long o = base + incl - len;
+        if (o + len > ctl->pool_cap) {
             pix_fail(ctl, 16);
             continue;
         }
         t.off[s] = (uint32_t)o;
         t.fill[s] = 0;
+        // the new pair's count is final: lift the maxima
+        const unsigned long long sel = pix_sel(t, s);
+        const uint32_t blk = s / PIX_B;
+        if (sel > t.bmax[blk]) {
+            atomicMax(&t.bmax[blk], sel);
+            atomicMax(&t.sbmax[blk / PIX_SB], sel);
+        }
     }
 }
 
-__global__ void k_pix_scatter(PixTable t, PixBufs B, PixCtl *ctl) {
-    if (ctl->status != PIX_RUN) return;
-    const uint32_t ne = min(ctl->n_ent, B.ent_cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += gridDim.x * blockDim.x) {
-        const uint2 e = B.ent[i];
-        const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
-        B.pool[t.off[e.x] + k] = e.y;
-    }
-}
-
-// the corpus rewrite: c at every site, its right slot merged away, the links around it.  The
-// merge is then logged; W must equal the sites found.
+// The corpus rewrite: c at every site, its right slot merged away, the links around it; the new
+// pairs' slots into their segments; the maxima of the touched blocks.  The merge is then logged;
+// W must equal the sites found.
 __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl,
                                                    int32_t *len16, long long *log) {
     if (ctl->status != PIX_RUN) return;
     const unsigned long long W = ctl->W;
-    if (ctl->n_sites != W || ctl->n_check != W) {
+    if (ctl->n_sites != W || (ctl->a == ctl->b && ctl->n_check != W)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             ctl->status = PIX_ERROR;
             ctl->err = 20;
@@ -610,7 +673,8 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         return;
     }
     const int32_t c = ctl->c;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)W; i += gridDim.x * blockDim.x) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (uint32_t i = tid; i < (uint32_t)W; i += stride) {
         const uint32_t p = B.sites[i];
         const uint32_t q = C.nxt[p];
         const uint32_t r = C.nxt[q];
@@ -619,10 +683,16 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         C.nxt[p] = r;
         if (r != PIX_NONE) C.prv[r] = p;
     }
+    // (a != b: two entries per site, some empty; a == b: packed)
+    const uint32_t ne = min(ctl->a != ctl->b ? 2 * (uint32_t)W : ctl->n_ent, B.ent_cap);
+    for (uint32_t i = tid; i < ne; i += stride) {
+        const uint2 e = B.ent[i];
+        if (e.x == PIX_NONE) continue;
+        const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
+        B.pool[t.off[e.x] + k] = e.y;
+    }
+    pix_bmax_dirty(t, B, ctl);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const uint32_t s = ctl->pair_slot;
-        t.cnt[s] = 0;                                                   // every (a, b) merged
-        pix_mark(t, B, ctl, s);
         const long long k = ctl->n_done;
         log[3 * k] = ctl->a;
         log[3 * k + 1] = ctl->b;

@@ -29,7 +29,7 @@ if has prof; then
       -- python3 bench.py > "$OUT/trace.log" 2>&1
   find "$OUT/trace" -name '*kernel_stats.csv' -exec head -12 {} \;
 fi
-PMC_BENCH="bench.py --steps 300 --warmup 5 --no-cpu-baseline"
+PMC_BENCH="bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-incremental"
 if has pmc; then
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
       -- python3 $PMC_BENCH > "$OUT/fetch.log" 2>&1
