@@ -1576,6 +1576,14 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             if (c->n_live < 2) break;
             rc = pix_build(c, max_length);
             ++builds;
+            if (rc == BPE_ERR_OOM) {
+                // (the index does not fit next to the corpus: the stream needs no extra memory)
+                if (c->pix) {
+                    (void)hipStreamSynchronize(c->stream);
+                    pix_free(c);
+                }
+                rc = PIX_NOT_ELIGIBLE;
+            }
             if (rc == PIX_NOT_ELIGIBLE) {
                 pix_free(c);
                 *n_merges = n;
