@@ -1498,9 +1498,8 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
         // per-merge buffers
         B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
         B.ent_cap = 2 * B.site_cap + 16;
-        B.key_cap = B.ent_cap;
         if ((rc = pix_alloc(P, &B.sites, B.site_cap)) || (rc = pix_alloc(P, &B.ent, B.ent_cap)) ||
-            (rc = pix_alloc(P, &B.newkeys, B.key_cap)) || (rc = pix_alloc(P, &B.dblocks, T.nblocks)) ||
+            (rc = pix_alloc(P, &B.dblocks, T.nblocks)) ||
             (rc = pix_alloc(P, &B.dsuper, T.nsuper)))
             return rc;
         if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
@@ -1604,12 +1603,11 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             P->T.len16 = c->d_len16;   // (ensure_len16_cap may have moved it)
             k_pix_begin<<<1, 1, 0, s>>>(P->d_ctl, want, (int32_t)base, mw);
             for (int64_t i = 0; i < want; ++i) {
-                k_pix_select<<<1, 1024, 0, s>>>(P->T, P->d_ctl, c->d_len16);
+                k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
                 k_pix_tie<<<MAX_CAND * PIX_TIE_SPLIT, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
                 k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
-                k_pix_alloc<<<64, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+                k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
                 k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, c->d_len16, P->d_log);
-                k_pix_sbmax<<<256, 256, 0, s>>>(P->T, P->B, P->d_ctl, 0);
             }
             HIP_TRY(hipGetLastError());
             PixCtl *h = P->h_ctl;

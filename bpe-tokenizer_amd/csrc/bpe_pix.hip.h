@@ -16,15 +16,15 @@
 // from the candidates' lists.
 //
 // One merge (a, b) -> c, every kernel reading the decision from PixCtl (no host round trip):
-//   k_pix_select   best key, candidates, W, min_weight / vocabulary checks
+//   k_pix_select   the superblock maxima the previous merge lowered, then the best key, the
+//                  candidates, W, min_weight / vocabulary checks
 //   k_pix_tie      R3 over the candidates' lists (only with a tie)
 //   k_pix_sites    the merge sites from the (a, b) list and the count changes around them (for
 //                  a == b the runs, walked from their heads: sites at even offsets, replaceAll's
 //                  left-to-right rule); the new adjacencies, all of which contain c
 //   k_pix_alloc    segments for the new pairs
 //   k_pix_apply    tokens and links (the only kernel that changes the corpus), the new pairs'
-//                  slots into their segments, the maxima of the touched blocks
-//   k_pix_sbmax    the superblock maxima over them
+//                  slots into their segments, the maxima of the blocks whose max entry fell
 // Anything the index cannot do in bounded work (a run or chain longer than PIX_WALK, a full
 // buffer, more than MAX_CAND tied pairs) sets PIX_HOST before k_pix_apply: the corpus is still
 // that of the last completed merge, and the host takes the iteration on the streaming path.
@@ -65,9 +65,8 @@ struct PixBufs {
     uint32_t *pool;      // list segments
     uint32_t *sites;     // this merge's sites
     uint2 *ent;          // this merge's new adjacencies: (table slot, position)
-    uint32_t *newkeys;   // table slots of this merge's new pairs
     uint32_t *dblocks, *dsuper;   // touched blocks / superblocks
-    uint32_t site_cap, ent_cap, key_cap;
+    uint32_t site_cap, ent_cap;
 };
 
 struct PixCtl {
@@ -80,7 +79,7 @@ struct PixCtl {
     long long min_weight, max_length;
     long long n_done, n_want;          // merges done / allowed in this batch
     uint32_t pair_slot, n_cand, tie_done, pad0;
-    uint32_t n_sites, n_ent, n_keys, n_dblocks, n_dsuper, pad1;
+    uint32_t n_sites, n_ent, n_dblocks, n_dsuper;
     unsigned long long n_check;        // merges made (== W when the index is consistent)
     unsigned long long pool_top, pool_cap;
     unsigned long long used, used_cap; // table claims / the claims it may hold
@@ -125,7 +124,7 @@ __device__ __forceinline__ void pix_fail(PixCtl *ctl, int why) {
 
 // find-or-claim the slot of a pair; PIX_NONE when the probe sequence is exhausted
 __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uint32_t key,
-                                             bool claim) {
+                                             bool claim, bool count_claim = false) {
     uint32_t s = pix_hash(key) & t.mask;
     for (int i = 0; i < PIX_PROBE; ++i, s = (s + 1) & t.mask) {
         const uint32_t k = t.keys[s];
@@ -134,7 +133,7 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
             if (!claim) return PIX_NONE;
             const uint32_t old = atomicCAS(&t.keys[s], PIX_NONE, key);
             if (old == PIX_NONE) {
-                atomicAdd(&ctl->used, 1ull);
+                if (count_claim) atomicAdd(&ctl->used, 1ull);
                 return s;
             }
             if (old == key) return s;
@@ -165,19 +164,17 @@ __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B,
 }
 
 // A new adjacency (u, v) at slot pos (u or v is c): its count, one more slot in its segment, the
-// entry at index e of this merge's entry list (e = ~0u: the next free one).
+// entry at index e of this merge's entry list (e = ~0u: the next free one).  The entry that
+// opened the pair's segment carries PIX_OWNER: k_pix_alloc places the segment from it.
+constexpr uint32_t PIX_OWNER = 0x80000000u;
 __device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
                                           int32_t u, int32_t v, uint32_t pos, long long d,
                                           uint32_t e = ~0u) {
     const uint32_t s = pix_add(t, B, ctl, u, v, d);
     if (s == PIX_NONE) return;
-    if (atomicAdd(&t.len[s], 1u) == 0u) {
-        const uint32_t k = atomicAdd(&ctl->n_keys, 1u);
-        if (k < B.key_cap) B.newkeys[k] = s;
-        else pix_fail(ctl, 2);
-    }
+    const uint32_t owner = atomicAdd(&t.len[s], 1u) == 0u ? PIX_OWNER : 0u;
     if (e == ~0u) e = atomicAdd(&ctl->n_ent, 1u);
-    if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos);
+    if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos | owner);
     else pix_fail(ctl, 3);
 }
 
@@ -215,7 +212,7 @@ __global__ void k_pix_build_insert(PixTable t, PixCtl *ctl, const uint32_t *uniq
     const uint32_t n = *n_runs;
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
         if (uniq[j] == PIX_NONE) continue;
-        const uint32_t s = pix_slot(t, ctl, uniq[j], true);
+        const uint32_t s = pix_slot(t, ctl, uniq[j], true, true);
         if (s == PIX_NONE) {
             ctl->err = 9;
             ctl->status = PIX_ERROR;
@@ -294,16 +291,37 @@ __global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long
 
 // ---- one merge --------------------------------------------------------------------------------
 // Best key, candidates (every pair sharing it), the decision.  One block of 1024.
-__global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixCtl *ctl, const int32_t *len16) {
+__global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixCtl *ctl) {
     __shared__ unsigned long long red[16];
     __shared__ uint32_t lst[64];
     __shared__ uint32_t n_lst, n_blk;
     __shared__ uint32_t blks[64];
     const int tid = threadIdx.x;
     if (ctl->status != PIX_RUN) return;
+    {
+        // the superblocks the previous merge may have lowered (one wave each)
+        const int lane = tid & 63, wv = tid >> 6;
+        const uint32_t nd = min(ctl->n_dsuper, t.nsuper);
+        for (uint32_t q = wv; q < nd; q += 16) {
+            const uint32_t sb = B.dsuper[q];
+            unsigned long long m = 0;
+            for (int k = lane; k < PIX_SB; k += 64) {
+                const uint32_t blk = sb * PIX_SB + k;
+                if (blk < t.nblocks) m = max(m, t.bmax[blk]);
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+            if (lane == 0) {
+                t.sbmax[sb] = m;
+                t.sbdirty[sb] = 0;
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
     if (tid == 0) {
         // counters of the previous merge (nothing else reads them now)
-        ctl->n_sites = ctl->n_ent = ctl->n_keys = ctl->n_dblocks = ctl->n_dsuper = 0;
+        ctl->n_sites = ctl->n_ent = ctl->n_dblocks = ctl->n_dsuper = 0;
         ctl->n_cand = 0;
         ctl->tie = 0;
         ctl->tie_done = 0;
@@ -467,22 +485,19 @@ __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBuf
 //   that run had even length;
 //   right adjacency (unless a site starts at r): (b, r) -> (c, r), likewise for a run of b's;
 //   a chain of m consecutive sites becomes m c's: floor(m/2) pairs (c, c).
-__device__ void pix_site_delta(const PixCorpus &C, const PixTable &t, const PixBufs &B,
-                               PixCtl *ctl, uint32_t p, uint32_t idx, int32_t a, int32_t b,
-                               int32_t c) {
-    const uint32_t q = C.nxt[p];
+// (two lanes per site: the even one takes the left adjacency and the chain, the odd one the right
+// adjacency; each writes its entry, [2 idx] / [2 idx + 1], or an empty one)
+__device__ void pix_site_left(const PixCorpus &C, const PixTable &t, const PixBufs &B,
+                              PixCtl *ctl, uint32_t p, uint32_t q, uint32_t idx, int32_t a,
+                              int32_t b, int32_t c) {
     const uint32_t l = C.prv[p];
-    const uint32_t r = C.nxt[q];
     const int32_t tl = l != PIX_NONE ? C.tok[l] : SEP;
-    const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
-    const bool lchain = tl == b && pix_tok_is(C, C.prv[l], a);
-    const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
-    // this site's entries: [2 idx] its left adjacency, [2 idx + 1] its right one
-    bool left_done = false, right_done = false;
-    if (lchain) {
+    bool done = false;
+    if (tl == b && pix_tok_is(C, C.prv[l], a)) {
+        // chained to the site before: (b, a) is lost, (c, c) from that site's slot
         pix_add(t, B, ctl, b, a, -1);
-        pix_entry(t, B, ctl, c, c, C.prv[l], 0, 2 * idx);      // (c, c) from the site before
-        left_done = true;
+        pix_entry(t, B, ctl, c, c, C.prv[l], 0, 2 * idx);
+        done = true;
     } else {
         if (tl >= 0) {
             if (tl == a) {
@@ -500,14 +515,16 @@ __device__ void pix_site_delta(const PixCorpus &C, const PixTable &t, const PixB
                 pix_add(t, B, ctl, tl, a, -1);
             }
             pix_entry(t, B, ctl, tl, c, l, 1, 2 * idx);
-            left_done = true;
+            done = true;
         }
         // the head of a chain: its length m, floor(m/2) pairs (c, c)
-        uint32_t m = 1, x = p;
+        uint32_t m = 1, xq = q;
         for (;;) {
-            const uint32_t xr = C.nxt[C.nxt[x]];
-            if (!(pix_tok_is(C, xr, a) && pix_tok_is(C, C.nxt[xr], b))) break;
-            x = xr;
+            const uint32_t xr = C.nxt[xq];
+            if (!pix_tok_is(C, xr, a)) break;
+            const uint32_t xrq = C.nxt[xr];
+            if (!pix_tok_is(C, xrq, b)) break;
+            xq = xrq;
             if (++m > (uint32_t)PIX_WALK) {
                 pix_fail(ctl, 14);
                 return;
@@ -515,6 +532,16 @@ __device__ void pix_site_delta(const PixCorpus &C, const PixTable &t, const PixB
         }
         if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
     }
+    if (!done && 2 * idx < B.ent_cap) B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
+}
+
+__device__ void pix_site_right(const PixCorpus &C, const PixTable &t, const PixBufs &B,
+                               PixCtl *ctl, uint32_t p, uint32_t q, uint32_t idx, int32_t a,
+                               int32_t b, int32_t c) {
+    const uint32_t r = C.nxt[q];
+    const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
+    // (a site starting at r takes this adjacency as its left one)
+    const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
     if (!rchain && tr >= 0) {
         if (tr == b) {
             uint32_t L = 1, x = r;
@@ -531,10 +558,9 @@ __device__ void pix_site_delta(const PixCorpus &C, const PixTable &t, const PixB
             pix_add(t, B, ctl, b, tr, -1);
         }
         pix_entry(t, B, ctl, c, tr, p, 1, 2 * idx + 1);
-        right_done = true;
+    } else if (2 * idx + 1 < B.ent_cap) {
+        B.ent[2 * idx + 1] = make_uint2(PIX_NONE, 0);
     }
-    if (!left_done && 2 * idx < B.ent_cap) B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
-    if (!right_done && 2 * idx + 1 < B.ent_cap) B.ent[2 * idx + 1] = make_uint2(PIX_NONE, 0);
 }
 
 __device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uint32_t p) {
@@ -560,26 +586,52 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
         pix_mark(t, B, ctl, s);           // (it was the global max: its block is recomputed)
     }
     const int lane = threadIdx.x & 63;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
-        const uint32_t p = B.pool[off + i];
-        const bool valid = C.tok[p] == a && pix_tok_is(C, C.nxt[p], b);
-        if (a != b) {
-            // one atomic per wave for the site indices
-            const unsigned long long mask = __ballot(valid);
+    if (a != b) {
+        // two lanes per list entry (pix_site_left / pix_site_right); one atomic per wave for the
+        // site indices
+        const uint64_t total = 2ull * len;
+        const int role = lane & 1, wv = threadIdx.x >> 6;
+        __shared__ uint32_t wcnt[4], bbase;
+        for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x; g0 < total;
+             g0 += (uint64_t)gridDim.x * blockDim.x) {
+            const uint64_t g = g0 + threadIdx.x;
+            uint32_t p = 0, q = PIX_NONE;
+            bool valid = false;
+            if (g < total) {
+                p = B.pool[off + (uint32_t)(g >> 1)];
+                q = C.nxt[p];
+                valid = C.tok[p] == a && pix_tok_is(C, q, b);
+            }
+            // one atomic per block for the site indices
+            const unsigned long long m0 = __ballot(valid && role == 0);
+            if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m0);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const uint32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+                bbase = tot ? atomicAdd(&ctl->n_sites, tot) : 0;
+            }
+            __syncthreads();
+            uint32_t base = bbase;
+            for (int w = 0; w < wv; ++w) base += wcnt[w];
+            __syncthreads();
             if (!valid) continue;
-            const int leader = __ffsll((long long)mask) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&ctl->n_sites, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
-            const uint32_t idx = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+            const uint32_t idx = base + (uint32_t)__popcll(m0 & ((1ull << (lane & ~1)) - 1));
             if (idx >= B.site_cap) {
                 pix_fail(ctl, 11);
                 continue;
             }
-            B.sites[idx] = p;
-            pix_site_delta(C, t, B, ctl, p, idx, a, b, c);
-            continue;
+            if (role == 0) {
+                B.sites[idx] = p;
+                pix_site_left(C, t, B, ctl, p, q, idx, a, b, c);
+            } else {
+                pix_site_right(C, t, B, ctl, p, q, idx, a, b, c);
+            }
         }
+        return;
+    }
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
+        const uint32_t p = B.pool[off + i];
+        const bool valid = C.tok[p] == a && pix_tok_is(C, C.nxt[p], b);
         if (!valid) continue;
         const uint32_t l = C.prv[p];
         if (pix_tok_is(C, l, a)) continue;             // not the head of its run
@@ -621,34 +673,49 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
     }
 }
 
-// segments for this merge's new pairs (one pool atomic per wave)
+// Segments for this merge's new pairs, from their owner entries (one pool atomic per block), and
+// the new pairs' maxima: their counts are final now.
 __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
     if (ctl->status != PIX_RUN) return;
-    const uint32_t nk = min(ctl->n_keys, B.key_cap);
-    const int lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < nk; i0 += stride) {
-        const uint32_t i = i0 + lane;
-        const uint32_t s = i < nk ? B.newkeys[i] : 0;
-        const unsigned long long len = i < nk ? t.len[s] : 0;
+    __shared__ unsigned long long wsum[4], wown[4], base_s;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t ne = min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
+    for (uint32_t i0 = blockIdx.x * 256; i0 < ne; i0 += gridDim.x * 256) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint2 e = make_uint2(PIX_NONE, 0);
+        if (i < ne) e = B.ent[i];
+        const bool own = e.x != PIX_NONE && (e.y & PIX_OWNER);
+        const unsigned long long len = own ? t.len[e.x] : 0;
         unsigned long long incl = len;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const unsigned long long o = __shfl_up(incl, d);
             if (lane >= d) incl += o;
         }
-        unsigned long long base = 0;
-        if (lane == 63) base = atomicAdd(&ctl->pool_top, incl);
-        base = __shfl(base, 63);
-        if (i >= nk) continue;
-        const unsigned long long o = base + incl - len;
+        const unsigned long long nown = __popcll(__ballot(own));
+        if (lane == 63) {
+            wsum[wv] = incl;
+            wown[wv] = nown;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            const unsigned long long no = wown[0] + wown[1] + wown[2] + wown[3];
+            base_s = tot ? atomicAdd(&ctl->pool_top, tot) : 0;
+            if (no) atomicAdd(&ctl->used, no);
+        }
+        __syncthreads();
+        unsigned long long o = base_s + incl - len;
+        for (int w = 0; w < wv; ++w) o += wsum[w];
+        __syncthreads();
+        if (!own) continue;
         if (o + len > ctl->pool_cap) {
             pix_fail(ctl, 16);
             continue;
         }
+        const uint32_t s = e.x;
         t.off[s] = (uint32_t)o;
         t.fill[s] = 0;
-        // the new pair's count is final: lift the maxima
         const unsigned long long sel = pix_sel(t, s);
         const uint32_t blk = s / PIX_B;
         if (sel > t.bmax[blk]) {
@@ -689,7 +756,7 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         const uint2 e = B.ent[i];
         if (e.x == PIX_NONE) continue;
         const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
-        B.pool[t.off[e.x] + k] = e.y;
+        B.pool[t.off[e.x] + k] = e.y & ~PIX_OWNER;
     }
     pix_bmax_dirty(t, B, ctl);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
