@@ -52,6 +52,12 @@ constexpr int WAVES_PER_WG = BPE_WAVES;
 #endif
 constexpr int RING = BPE_RING;
 static_assert(RING >= 5, "ring depth");
+// Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
+// pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
+// this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
+#ifndef BPE_LOAD_AUX
+#define BPE_LOAD_AUX 2
+#endif
 
 // f(integral_constant<I>) for I = 0 .. N-1, unrolled in the source (the ring's slot indices must be
 // compile-time constants, or the ring is moved to scratch memory)
@@ -345,10 +351,14 @@ __device__ __forceinline__ void add_pairs_global(const Sink &k, int32_t x, int32
 //  - sketch bucket b of a cold pair: dword HOT_BINS / 2 + (b >> 1), half b & 1, with
 //    b = ((hash & 0x1FFF) << 1) | (x & 1): the dword from the hash, the half from x, so both
 //    classes share the increment.
-// A counter reaching 0x8000 spills 0x8000 to the global u64 table (indexed by table_index):
-// exactly one lane observes each 0x7FFF -> 0x8000 transition, and the 32K of headroom absorbs
-// every add that lands before its subtraction (a CU issues far fewer in flight), so no field
-// ever carries into its neighbour.
+// Overflow: the adds return the dword they found.  Each wave ORs the returns of a ring round
+// (RING chunks) together and, at the round's end, when some half it touched stood at >= 0x4000,
+// sweeps the table (lds_sweep): every half >= 0x4000 gives its top two bits to the global u64
+// spill (indexed by the bin, 2 * dword + half) with one atomic AND, race-free against the other
+// waves' adds and sweeps.  No half can pass 0xFFFF: it receives at most 49152 adds between
+// reaching 0x4000 and the first sweep, and every one of those adds comes from a wave that saw
+// it at >= 0x4000 and sweeps at the end of its round, after at most RING chunks of at most 256
+// adds to any one counter: 16 waves x 7 x 256 = 28672.
 constexpr uint32_t HOT_BYTES = HOT_BINS * 2;   // 128 KiB
 
 __device__ __forceinline__ uint32_t hot_addr(int32_t x, int32_t y) {
@@ -376,17 +386,26 @@ __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
     return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + addr);
 }
 
-// After an add of inc (1 << sh) at addr returned old: spill if this add reached 0x8000.
-__device__ __forceinline__ void lds_fix(const Sink &k, uint32_t addr, uint32_t inc, uint32_t bin,
-                                        uint32_t old) {
-    const uint32_t sh = inc == 1u ? 0u : 16u;
-    if (((old >> sh) & 0xFFFFu) != 0x7FFFu) return;
-    atomicSub(lds_word(k, addr), 0x8000u << sh);
-    // (the constant is made opaque so it is materialised here, not held in registers across the
-    // streaming loop for this rare path)
-    uint32_t big = 0x8000u;
-    asm volatile("" : "+v"(big));
-    atomicAdd(&k.spill[bin], (unsigned long long)big);
+// The halves a sweep moves: bits 14 and 15 of each.
+constexpr uint32_t SWEEP_BITS = 0xC000C000u;
+
+// One wave's sweep of LDS dwords [0, NW): each half >= 0x4000 moves its top two bits to the
+// spill.  (Rare: no counter of the uniform C3 corpus ever reaches 0x4000 in a workgroup.)
+template <int NW>
+__device__ __attribute__((noinline)) void lds_sweep(uint32_t *hist, unsigned long long *spill,
+                                                    int lane) {
+    for (int i = 4 * lane; i < NW; i += 4 * 64) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(hist + i);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (w[j] & SWEEP_BITS) {
+                const uint32_t old = atomicAnd(&hist[i + j], ~SWEEP_BITS);
+                const uint32_t lo = old & 0xC000u, hi = (old >> 16) & 0xC000u;
+                if (lo) atomicAdd(&spill[2 * (i + j)], (unsigned long long)lo);
+                if (hi) atomicAdd(&spill[2 * (i + j) + 1], (unsigned long long)hi);
+            }
+    }
 }
 
 // MODE_EXACT: each workgroup first sums its cold-pair counts in an LDS hash (open addressing,
@@ -502,27 +521,20 @@ __device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y) {
 }
 
 // One counted occurrence of (x, y) (outside the streaming fast paths).
+// (MODE_TABLE / MODE_FUSED: the dword the add found is ORed into `seen`, the wave's overflow
+// screen; see lds_sweep)
 template <int MODE>
-__device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y) {
+__device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y, uint32_t &seen) {
     if (MODE == MODE_NONE) return;
     if (MODE == MODE_INCR) {
         if (incr_touched(k, x, y)) incr_add(k, x, y);
         return;
     }
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
-        uint32_t addr, inc, bin;
         const bool hot = ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT;
-        if (hot) {
-            addr = hot_addr(x, y);
-            inc = hot_inc(x);
-            bin = hot_bin((uint32_t)x, (uint32_t)y);
-        } else {
-            addr = cold_addr(sketch_hash(x, y));
-            inc = hot_inc(x);
-            bin = HOT_BINS + sketch_bucket(x, y);
-        }
+        const uint32_t addr = hot ? hot_addr(x, y) : cold_addr(sketch_hash(x, y));
         // (MODE_FUSED keeps no sketch: its cold pairs go to the maintained table only)
-        if (MODE == MODE_TABLE || hot) lds_fix(k, addr, inc, bin, atomicAdd(lds_word(k, addr), inc));
+        if (MODE == MODE_TABLE || hot) seen |= atomicAdd(lds_word(k, addr), hot_inc(x));
         if (MODE == MODE_FUSED && exact_wanted<MODE>(k, x, y)) lds_fused_add(k, pair_key(x, y), 1u);
     } else if (exact_wanted<MODE>(k, x, y)) {
         lds_cold_add(k, pair_key(x, y), 1u);
@@ -811,6 +823,7 @@ struct Tally {
     int32_t par;         // run-offset parity of prev (the first run counts from the region start)
     int32_t first_tok;   // the region's first live token
     int32_t in_lead;     // every live token so far belongs to the region's first run
+    uint32_t seen;       // (per lane) OR of the words the exact path's LDS adds returned
 };
 
 // LDS adds of one chunk's pairs (x[e], y[e]), then the overflow screen.  Per pair: the hot
@@ -837,8 +850,8 @@ __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, 
     }
 }
 
-// The LDS adds of a fast-path chunk; their returned words go to o (the overflow screen runs a
-// stage later, check_deferred, so no wave waits on its LDS atomics' return).
+// The LDS adds of a fast-path chunk; their returned words go to o, screened at the end of the
+// ring round (Returns), so no wave waits on its LDS atomics' return before then.
 template <bool FUSED = false>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
                                           const Sink &k, uint32_t (&o)[4]) {
@@ -850,37 +863,14 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
     }
 }
 
-// A fast-path count whose overflow screen is still due: the words its LDS adds returned.  The
-// screen runs one stage later (the chunk and its right-hand neighbour are still in the ring), so
-// the adds' return latency hides behind the next chunk's work.  The delay is safe: a counter
-// that reached 0x8000 takes at most two stages of the workgroup's adds (16 waves x 512 pairs)
-// before its 0x8000 is moved to the spill, far below the 32K of headroom under 0xFFFF.
+// The words a fast-path count's LDS adds returned (0 when the chunk took another path).  Each
+// stage of a ring round keeps its own, and they are all screened together at the round's end, so
+// the waves wait on LDS returns once per RING chunks, not once per chunk.  (Screening each chunk's
+// returns one stage later left the compiler a wait for every add still in flight at each stage:
+// 5 % of the pass.)
 struct Defer {
     uint32_t o[4];
-    int pend;   // o holds the returns of a fast-path chunk (wave-uniform)
 };
-
-// The deferred overflow screen of the chunk w counted at the previous stage (nxt = the first
-// post-merge token after it).  Conservative: only a counter at >= 0x4000 can be at 0x7FFF; then
-// the chunk's pairs are recomputed (rare) and each lane that saw 0x7FFF spills.
-template <bool FUSED>
-__device__ __forceinline__ void check_deferred(const Chunk &w, int32_t nxt, const Defer &d,
-                                               const Sink &k) {
-    if (!d.pend) return;
-    if (__ballot(((d.o[0] | d.o[1] | d.o[2] | d.o[3]) & 0x40004000u) != 0u) == 0ull) return;
-    int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
-    asm volatile("" : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3));
-    const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
-    const int32_t x3 = sel(lane_in(P63), w.last, t3);
-    const int32_t r3 = from_next(t0, nxt);
-    const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        uint32_t addr, inc;
-        pair_slot<FUSED>(x[e], y[e], addr, inc);
-        if (inc) lds_fix(k, addr, inc, (uint32_t)table_index(x[e], y[e]), d.o[e]);
-    }
-}
 
 // The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (MODE_FUSED's refresh
 // of the maintained cold table): per-token membership masks (compares into lane masks,
@@ -921,9 +911,8 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
 // TAIL: the region's last chunk (nxt = NONE).  It always takes the exact path: the parity of its
 // last token's run offset feeds RegionSum::trail_odd, which k_runs needs whenever that run goes on
 // in the next region, and the fast path does not work that parity out.
-// Fast-path counts of MODE_TABLE / MODE_FUSED leave their overflow screen in `df` (check_deferred
-// at the next stage); every other path finishes here.  (Screening before the next chunk's adds
-// instead, so that it waits on nothing newer, timed 2.4 % slower.)
+// Fast-path counts of MODE_TABLE / MODE_FUSED leave the words their adds returned in `df`, and the
+// other paths OR theirs into s.seen: the overflow screen of the ring round (screen_round).
 template <int MODE, bool TAIL = false>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k, Defer &df) {
@@ -971,8 +960,6 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 cold = __ballot(mx >= (uint32_t)HOT);
             }
             if (cold == 0ull) {
-                // (the deferred screen recomputes these as pair_slot, which equals the hot form
-                // for valid hot pairs)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     df.o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
@@ -981,11 +968,10 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 add_pairs<MODE == MODE_FUSED>(x, y, k, df.o);
                 if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
             }
-            df.pend = 1;
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e]);
+                if ((x[e] | y[e]) >= HOT) count_pair<MODE>(k, x[e], y[e], s.seen);
         } else if (MODE == MODE_INCR) {
             // only the pairs with a side in {ma, mb, mc}: membership masks per slot (compares into
             // lane masks, combined on the scalar unit), the LDS only for chunks that hold one
@@ -1091,7 +1077,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        if (cnt[e]) count_pair<MODE>(k, w.t[e], rr[e]);
+        if (cnt[e]) count_pair<MODE>(k, w.t[e], rr[e], s.seen);
     s.first_tok = s.n_live ? s.first_tok : w.first;
     s.prev = w.last;
     s.par = par_last;
@@ -1280,6 +1266,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         s.par = 0;
         s.first_tok = NONE;
         s.in_lead = 1;
+        s.seen = 0;
         Apply ap;
         ap.prev = rc.prev_tok;
         ap.par = (int32_t)(rc.carry_off & 1) ^ 1;   // the token before the region (if linked)
@@ -1291,7 +1278,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             ids + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
         const int lo = lane * 16;
         auto load = [&](Chunk &q, int c) __attribute__((always_inline)) {
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), BPE_LOAD_AUX);
             q.t[0] = (int)x[0];
             q.t[1] = (int)x[1];
             q.t[2] = (int)x[2];
@@ -1313,14 +1300,29 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             return v;
         };
         const uint32_t key = pack_pair_s(ma, mb);
-        // Ring of RING slots: stage c applies chunk c (cur), counts chunk c-1 (prv), runs the
-        // deferred overflow screen of chunk c-2 (chk, counted at stage c-1) and loads chunk
+        // Ring of RING slots: stage c applies chunk c (cur), counts chunk c-1 (prv) and loads chunk
         // c+RING-3 into the slot of chunk c-3 (fre), which the previous stage freed, so the load
-        // can issue at once without its registers overlapping a chunk still in use.
-        Defer dq;
-        dq.pend = 0;
-        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, const Chunk &chk,
-                         Chunk &fre, int c) __attribute__((always_inline)) {
+        // can issue at once without its registers overlapping a chunk still in use.  Stage i of a
+        // round keeps its count's LDS returns in D[i] until the round's overflow screen.
+        Defer D[RING];
+        static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
+            D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
+        });
+        // The overflow screen of a round (MODE_TABLE / MODE_FUSED): every word the wave's adds
+        // returned since the last screen, then a sweep if some half stood at >= 0x4000 (lds_sweep)
+        auto screen_round = [&]() __attribute__((always_inline)) {
+            if (MODE != MODE_TABLE && MODE != MODE_FUSED) return;
+            uint32_t acc = s.seen;
+            s.seen = 0;
+            static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
+                acc |= D[i].o[0] | D[i].o[1] | D[i].o[2] | D[i].o[3];
+                D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
+            });
+            if (__ballot((acc & SWEEP_BITS) != 0u) != 0ull)
+                lds_sweep < MODE == MODE_FUSED ? HOT_BINS / 2 : HIST_WORDS > (hist, spill, lane);
+        };
+        auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
+                         Defer &df) __attribute__((always_inline)) {
             load(fre, c + RING - 3);
             if (c < nc) {
                 finish_load(cur);
@@ -1334,16 +1336,11 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             if (MERGE && cur.len)
                 apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, key,
                                    rs, c, lane, ap);
-            Defer dn;
-            dn.pend = 0;
             if (cur.len) {
-                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, dn);
+                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, df);
             } else {
                 cur = prv;   // rare: hand the pending chunk on
             }
-            // (chk was counted at the previous stage against prv's first token, both unchanged)
-            check_deferred<MODE == MODE_FUSED>(chk, prv.first, dq, k);
-            dq = dn;
         };
         if (nc > 0) {
             Chunk S[RING];   // (constant indices only: the ring stays in registers)
@@ -1362,13 +1359,13 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
                     constexpr int i = decltype(I)::value;
                     stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
-                          S[(i + RING - 2) % RING], S[(i + RING - 3) % RING], c + i);
+                          S[(i + RING - 3) % RING], c + i, D[i]);
                 });
+                screen_round();
             }
-            check_deferred<MODE == MODE_FUSED>(S[RING - 2], S[RING - 1].first, dq, k);
-            Defer dt;
-            dt.pend = 0;
+            Defer dt;   // (the region's last chunk takes the exact path: s.seen)
             if (S[RING - 1].len) count_chunk<MODE, true>(S[RING - 1], NONE, lane, s, k, dt);
+            screen_round();
         }
         if (lane == 0) {
             RegionSum o;
@@ -2368,7 +2365,7 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
         const_cast<int32_t *>(A.ids) + c0 * CHUNK, 0, nc * CHUNK * 4, 0x00020000);
     const int lo = lane * 16;
     auto load = [&](Chunk &q, int c) __attribute__((always_inline)) {
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), 0);
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, c * (CHUNK * 4), BPE_LOAD_AUX);
         q.t[0] = (int)x[0];
         q.t[1] = (int)x[1];
         q.t[2] = (int)x[2];

@@ -260,6 +260,27 @@ def test_restore_style_apply_and_append_after_merges():
 
 
 @pytest.mark.parametrize('mode', MODES)
+def test_lds_counters_past_16_bits(mode):
+    """Pairs so frequent that every workgroup's 16-bit LDS counters pass 0x4000 many times in one
+    pass (each workgroup sees ~30 K of each pair here): a hot pair on the fast path, a cold pair in
+    its sketch bucket, a hot/cold mix, and one long run counted by the exact path.  The round-end
+    overflow screen and the sweep to the global spill (lds_sweep) must keep every count exact."""
+    n = 8 << 20
+    samples = [np.tile(np.array([0, 1], np.int32), n // 2),
+               np.tile(np.array([300, 301], np.int32), n // 2),
+               np.tile(np.array([2, 300], np.int32), n // 2),
+               np.full(n, 3, np.int32)]
+    ids, off = _flat(samples)
+    len16 = [1] * 302
+    st = OracleState(ids, off, len16, 302, extra=64)
+    want = st.merge_until(0, 2, 6)
+    e, got = run_engine(samples, len16, {'max_iterations': 6}, mode=mode)
+    assert got == want
+    assert [m[2] for m in got[:2]] == [n // 2, n // 2]
+    assert e.samples() == st.samples()
+
+
+@pytest.mark.parametrize('mode', MODES)
 def test_compaction_under_heavy_merging(mode):
     """'ab' * 1.5M: the first merge halves the corpus, which triggers the dead-slot compaction."""
     n = 3_000_000
@@ -499,7 +520,7 @@ def test_c3_dynamics_through_the_device_loop():
     """The bench's timed path (bpe_merge_until: k_step_loop, k_select_multi, k_decide, the
     tail-window tie pass, the dead-slot compaction) over the dynamics of BASELINE config 3, scaled
     down: a 32 MiB uniform 256-char corpus (xorshift32 seed 12345, 1 MiB samples), 3000 merges.
-    Each merge removes ~W/N = 1/65536 of the stream, so the run crosses the 3 % compaction, and
+    Each merge removes ~W/N = 1/65536 of the stream, so the run crosses the 1 % compaction, and
     about one iteration in ten is an R3 tie.  Checked against the multi-threaded CPU restatement
     (itself pinned to the reference's fixtures): every merge and the final corpus."""
     n = 32 << 20
