@@ -534,7 +534,13 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y, 
         const bool hot = ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT;
         const uint32_t addr = hot ? hot_addr(x, y) : cold_addr(sketch_hash(x, y));
         // (MODE_FUSED keeps no sketch: its cold pairs go to the maintained table only)
-        if (MODE == MODE_TABLE || hot) seen |= atomicAdd(lds_word(k, addr), hot_inc(x));
+        if (MODE == MODE_TABLE || hot) {
+            // (consumed at once: a `seen` still in flight would make every later join wait for
+            // all of the wave's LDS adds, the fast path's deferred ones included)
+            uint32_t old = atomicAdd(lds_word(k, addr), hot_inc(x));
+            asm volatile("" : "+v"(old));
+            seen |= old;
+        }
         if (MODE == MODE_FUSED && exact_wanted<MODE>(k, x, y)) lds_fused_add(k, pair_key(x, y), 1u);
     } else if (exact_wanted<MODE>(k, x, y)) {
         lds_cold_add(k, pair_key(x, y), 1u);
