@@ -52,6 +52,9 @@ constexpr int WAVES_PER_WG = BPE_WAVES;
 #endif
 constexpr int RING = BPE_RING;
 static_assert(RING >= 5, "ring depth");
+// (the overflow screen runs once per ring round: 16 waves x RING chunks x 256 adds must stay
+// below the 49152 adds of headroom above 0x4000, see lds_sweep)
+static_assert(WAVES_PER_WG * RING * 256 < 49152, "ring depth vs the LDS overflow screen");
 // Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
 // pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
 // this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
@@ -1011,6 +1014,9 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 }
                 // a counter that reached 0x8000: exactly one lane saw 0x7FFF (rare)
                 bool spill = false;
+#ifdef BPE_EXP_NORET
+                if (lane < 0)   // (timing experiment only: no spill check; wrong on overflow)
+#endif
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     spill |= ((rok >> e) & 1ull) && ((o[e] >> sh[e]) & 0xFFFFu) == 0x7FFFu;
