@@ -392,23 +392,29 @@ __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
 // The halves a sweep moves: bits 14 and 15 of each.
 constexpr uint32_t SWEEP_BITS = 0xC000C000u;
 
-// One wave's sweep of LDS dwords [0, NW): each half >= 0x4000 moves its top two bits to the
-// spill.  (Rare: no counter of the uniform C3 corpus ever reaches 0x4000 in a workgroup.)
-template <int NW>
+__device__ __forceinline__ void sweep_word(uint32_t *hist, unsigned long long *spill, int i,
+                                           uint32_t w) {
+    if (!(w & SWEEP_BITS)) return;
+    const uint32_t old = atomicAnd(&hist[i], ~SWEEP_BITS);
+    const uint32_t lo = old & 0xC000u, hi = (old >> 16) & 0xC000u;
+    if (lo) atomicAdd(&spill[2 * i], (unsigned long long)lo);
+    if (hi) atomicAdd(&spill[2 * i + 1], (unsigned long long)hi);
+}
+
+// One wave's sweep of LDS dwords [begin, end) (begin a multiple of 4): each half >= 0x4000 moves
+// its top two bits to spill[2 * dword + half].  (Rare: no counter of the uniform C3 corpus ever
+// reaches 0x4000 in a workgroup.)
 __device__ __attribute__((noinline)) void lds_sweep(uint32_t *hist, unsigned long long *spill,
-                                                    int lane) {
-    for (int i = 4 * lane; i < NW; i += 4 * 64) {
+                                                    int lane, int begin, int end) {
+    const int end4 = begin + ((end - begin) & ~3);
+    for (int i = begin + 4 * lane; i < end4; i += 4 * 64) {
         const uint4 v = *reinterpret_cast<const uint4 *>(hist + i);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (w[j] & SWEEP_BITS) {
-                const uint32_t old = atomicAnd(&hist[i + j], ~SWEEP_BITS);
-                const uint32_t lo = old & 0xC000u, hi = (old >> 16) & 0xC000u;
-                if (lo) atomicAdd(&spill[2 * (i + j)], (unsigned long long)lo);
-                if (hi) atomicAdd(&spill[2 * (i + j) + 1], (unsigned long long)hi);
-            }
+        sweep_word(hist, spill, i, v.x);
+        sweep_word(hist, spill, i + 1, v.y);
+        sweep_word(hist, spill, i + 2, v.z);
+        sweep_word(hist, spill, i + 3, v.w);
     }
+    for (int i = end4 + lane; i < end; i += 64) sweep_word(hist, spill, i, hist[i]);
 }
 
 // MODE_EXACT: each workgroup first sums its cold-pair counts in an LDS hash (open addressing,
@@ -462,8 +468,8 @@ __device__ __forceinline__ void lds_fused_add(const Sink &k, uint32_t key, uint3
 // MODE_INCR's LDS: four rows of 16-bit counters indexed by the pair's other token, for the pairs
 // (ma, y), (mb, y), (x, ma), (x, mb) in this order of precedence (each pair counts once), the
 // other token below INCR_RLIM; then a hash of (key, count) dwords for everything else touched
-// (the pairs of mc, and other tokens >= INCR_RLIM).  A counter reaching 0x8000 spills 0x8000 to the
-// global rspill row (one lane sees each transition, as in the hot table).
+// (the pairs of mc, and other tokens >= INCR_RLIM).  Overflow as in the hot table: the round's
+// screen and lds_sweep over the rows' used part, to the global rspill rows.
 constexpr int INCR_RLIM = 18432;                       // counters per row
 constexpr int IH_SLOTS = 2048;
 constexpr int IH_BASE = 4 * INCR_RLIM / 2;             // dword index of the hash keys
@@ -492,7 +498,7 @@ __device__ __forceinline__ void incr_hash_add(const Sink &k, uint32_t key, uint3
 }
 
 // One occurrence of a pair touched by the merge (incr_touched) into MODE_INCR's LDS.
-__device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y) {
+__device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y, uint32_t &seen) {
     int row, idx;
     if (x == k.ma) {
         row = 0;
@@ -516,11 +522,10 @@ __device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y) {
     }
     const uint32_t c = (uint32_t)(row * INCR_RLIM + idx);
     const uint32_t sh = (c & 1u) << 4;
-    const uint32_t old = atomicAdd(&k.hist[c >> 1], 1u << sh);
-    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-        atomicSub(&k.hist[c >> 1], 0x8000u << sh);
-        atomicAdd(&k.rspill[c], 0x8000ull);
-    }
+    // (the round's overflow screen, as for the hot table: consumed at once, see count_pair)
+    uint32_t old = atomicAdd(&k.hist[c >> 1], 1u << sh);
+    asm volatile("" : "+v"(old));
+    seen |= old;
 }
 
 // One counted occurrence of (x, y) (outside the streaming fast paths).
@@ -530,7 +535,7 @@ template <int MODE>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y, uint32_t &seen) {
     if (MODE == MODE_NONE) return;
     if (MODE == MODE_INCR) {
-        if (incr_touched(k, x, y)) incr_add(k, x, y);
+        if (incr_touched(k, x, y)) incr_add(k, x, y, seen);
         return;
     }
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
@@ -995,8 +1000,8 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 // branch-free on the common route (a row counter): every lane adds, 0 when its
                 // pair is not touched (to a counter of its own: no two lanes on one address);
                 // pairs of mc, and other tokens past the rows, take the hash (rare)
-                uint32_t o[4], dw[4], sh[4];
-                unsigned long long hsh = 0, rok = 0;
+                uint32_t dw[4], sh[4];
+                unsigned long long hsh = 0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int32_t xx = x[e], yy = y[e];
@@ -1008,25 +1013,10 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                     const uint32_t cc = (uint32_t)(row * INCR_RLIM + idx);
                     sh[e] = (cc & 1u) << 4;
                     dw[e] = inrow ? (cc >> 1) : (uint32_t)lane;
-                    o[e] = atomicAdd(&k.hist[dw[e]], (uint32_t)inrow << sh[e]);
-                    rok |= (unsigned long long)inrow << e;   // (per lane: bit e)
+                    // (the returns wait for the round's overflow screen; a lane's own dword
+                    // `lane` is a row 0 counter, so its return can only raise a false alarm)
+                    df.o[e] = atomicAdd(&k.hist[dw[e]], (uint32_t)inrow << sh[e]);
                     hsh |= (unsigned long long)(act & !inrow) << e;
-                }
-                // a counter that reached 0x8000: exactly one lane saw 0x7FFF (rare)
-                bool spill = false;
-#ifdef BPE_EXP_NORET
-                if (lane < 0)   // (timing experiment only: no spill check; wrong on overflow)
-#endif
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    spill |= ((rok >> e) & 1ull) && ((o[e] >> sh[e]) & 0xFFFFu) == 0x7FFFu;
-                if (__ballot(spill) != 0ull) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (((rok >> e) & 1ull) && ((o[e] >> sh[e]) & 0xFFFFu) == 0x7FFFu) {
-                            atomicSub(&k.hist[dw[e]], 0x8000u << sh[e]);
-                            atomicAdd(&k.rspill[2 * dw[e] + (sh[e] >> 4)], 0x8000ull);
-                        }
                 }
                 if (__ballot(hsh != 0ull) != 0ull) {
 #pragma unroll
@@ -1323,15 +1313,23 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         // The overflow screen of a round (MODE_TABLE / MODE_FUSED): every word the wave's adds
         // returned since the last screen, then a sweep if some half stood at >= 0x4000 (lds_sweep)
         auto screen_round = [&]() __attribute__((always_inline)) {
-            if (MODE != MODE_TABLE && MODE != MODE_FUSED) return;
+            if (MODE != MODE_TABLE && MODE != MODE_FUSED && MODE != MODE_INCR) return;
             uint32_t acc = s.seen;
             s.seen = 0;
             static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
                 acc |= D[i].o[0] | D[i].o[1] | D[i].o[2] | D[i].o[3];
                 D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
             });
-            if (__ballot((acc & SWEEP_BITS) != 0u) != 0ull)
-                lds_sweep < MODE == MODE_FUSED ? HOT_BINS / 2 : HIST_WORDS > (hist, spill, lane);
+            if (__ballot((acc & SWEEP_BITS) != 0u) != 0ull) {
+                if (MODE == MODE_INCR) {
+                    const int vl = incr_vlim(mc);
+                    for (int rw = 0; rw < 4; ++rw)
+                        lds_sweep(hist, rspill, lane, rw * (INCR_RLIM / 2),
+                                  rw * (INCR_RLIM / 2) + vl / 2);
+                } else {
+                    lds_sweep(hist, spill, lane, 0, MODE == MODE_FUSED ? HOT_BINS / 2 : HIST_WORDS);
+                }
+            }
         };
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
                          Defer &df) __attribute__((always_inline)) {

@@ -492,6 +492,32 @@ def test_zipf_words_vs_oracle(mib, n, max_length):
 
 
 @pytest.mark.slow
+def test_zipf_maintained_rows_past_16_bits():
+    """256 MiB of Zipf words (a workgroup holds 1 MiB of it), so that in the maintained state the
+    merge pass's LDS rows (MODE_INCR: the pairs (a, y), (b, y), (x, a), (x, b) of the merge
+    (a, b)) of frequent tokens pass 0x4000 in a workgroup: the round's overflow screen and the
+    rows' sweep must keep every count exact.  mergeUntil against the multi-threaded CPU
+    restatement: every merge and the final corpus."""
+    mib, n = 256, 300
+    data = pkg.synth_zipf(mib << 20, seed=77)
+    e = pkg.Engine(0)
+    e.stats_enable(True)
+    cmap, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    ids = cmap[data]
+    del data
+    off = np.arange(0, (mib << 20) + 1, 1 << 20, dtype=np.int64)
+    cpu = CpuMT(ids, off, [1] * nt, nt, threads=16, extra=n + 8)
+    del ids
+    want = cpu.merge_until(0, 2, n)
+    got = e.merge_until(0, 2, n)
+    assert got == want
+    flat, eoff = e.read_corpus()
+    cflat, coff = cpu.read()
+    assert np.array_equal(eoff, coff) and np.array_equal(flat, cflat)
+    assert e.stats()['fused_passes'] > 0, e.stats()
+
+
+@pytest.mark.slow
 def test_cold_pair_count_beyond_2_32():
     """A cold pair whose count exceeds 2^32 (the reference's Map counts are JS numbers, exact to
     2^53, core.ts:280-292): 'x' * (2^33 + 2) ingested as token id 300, so (300, 300) occurs
