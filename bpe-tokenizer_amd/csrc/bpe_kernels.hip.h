@@ -1834,53 +1834,58 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
 __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
                          long long *log, int phase, const unsigned long long *__restrict__ tie_pos,
                          long long *__restrict__ count = nullptr) {
-    if (threadIdx.x != 0 || ctl->status != LOOP_RUN) return;
-    const unsigned long long best = res->best;
+    if (threadIdx.x != 0) return;
+    // Snapshots of the control block and the Result (their loads issue together: one memory
+    // latency instead of a chain of dependent ones); the fields are written back one by one.
+    const LoopCtl C = *ctl;
+    const Result R = *res;
+    const int2 cand0 = cand[0];
+    if (C.status != LOOP_RUN) return;
+    const unsigned long long best = R.best;
     const long long W = (long long)(best >> 17);
-    const unsigned n = res->n_cand;
+    const unsigned n = R.n_cand;
     int32_t a = -1, b = -1;
     auto to_host = [&]() {
         ctl->status = LOOP_HOST;
-        ctl->n_host += 1;
+        ctl->n_host = C.n_host + 1;
     };
     // room in the maintained table for the refresh of the merge: every pair the merge creates
     // has the new token c as a side, and c occurs W times, so it claims at most 2 W new slots
     auto room = [&]() -> bool {
-        if (!ctl->maintained) return true;
-        const unsigned long long V = (unsigned long long)ctl->next_id + 1;
+        if (!C.maintained) return true;
+        const unsigned long long V = (unsigned long long)C.next_id + 1;
         const unsigned long long claims = 2 * (unsigned long long)W < V * V ? 2 * W : V * V;
-        return (res->cold_flags & 0xFFFFFFFFull) + claims + 64 <= ctl->cold_cap / 4 * 3;
+        return (R.cold_flags & 0xFFFFFFFFull) + claims + 64 <= C.cold_cap / 4 * 3;
     };
     if (phase == 0) {
-        if (ctl->w >= 0) {
+        if (C.w >= 0) {
             // the previous merge's replacement count: == W on the whole corpus, logged per shard
-            if (!ctl->sharded && res->replaced != (unsigned long long)ctl->w) {
+            if (!C.sharded && R.replaced != (unsigned long long)C.w) {
                 ctl->status = LOOP_ERROR;
                 return;
             }
-            log[LOG_WORDS * (ctl->n_done - 1) + 3] = (long long)res->replaced;
+            log[LOG_WORDS * (C.n_done - 1) + 3] = (long long)R.replaced;
         }
         ctl->w = -1;
-        if (ctl->maintained) {
-            const unsigned long long used = res->cold_flags & 0xFFFFFFFFull;
-            if ((res->cold_flags >> 32) || used * 4 > ctl->cold_cap * 3 ||
-                2 * res->cold_dead > used + 65536) {
+        if (C.maintained) {
+            const unsigned long long used = R.cold_flags & 0xFFFFFFFFull;
+            if ((R.cold_flags >> 32) || used * 4 > C.cold_cap * 3 ||
+                2 * R.cold_dead > used + 65536) {
                 to_host();
                 return;
             }
-        } else if (res->n_heavy) {
+        } else if (R.n_heavy) {
             // a heavy sketch bucket may hold a cold pair above the best hot one (even when no
             // hot pair exists at all): only the host path's exact counts can tell
             to_host();
             return;
         }
-        if (best == 0 || W < ctl->min_weight) {                   // core.ts:312-313
+        if (best == 0 || W < C.min_weight) {                      // core.ts:312-313
             ctl->status = LOOP_DONE;
             return;
         }
-        if (n == 0 || n > (unsigned)MAX_CAND || ctl->next_id >= ctl->max_id) {
-            ctl->status = LOOP_HOST;
-            ctl->n_host += 1;
+        if (n == 0 || n > (unsigned)MAX_CAND || C.next_id >= C.max_id) {
+            to_host();
             return;
         }
         if (n > 1) {
@@ -1893,25 +1898,25 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
                 cand[i] = v;
             }
             // X Y candidates only (one corpus): the tail window first; else the full pass
-            int all_xy = !ctl->sharded;
+            int all_xy = !C.sharded;
             for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
             for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
             ctl->tie = all_xy ? 1 : 2;
-            ctl->n_tie += 1;
+            ctl->n_tie = C.n_tie + 1;
             return;
         }
-        a = cand[0].x;
-        b = cand[0].y;
+        a = cand0.x;
+        b = cand0.y;
         if (!room()) {
             to_host();
             return;
         }
     } else {
-        if (!ctl->tie) return;
+        if (!C.tie) return;
         unsigned long long bp = ~0ull;
         unsigned missing = 0;
         for (unsigned j = 0; j < n; ++j) {
-            const unsigned long long p = tie_pos ? tie_pos[j] : res->last[j];
+            const unsigned long long p = tie_pos ? tie_pos[j] : R.last[j];
             if (p && p < bp) {
                 bp = p;
                 a = cand[j].x;
@@ -1919,22 +1924,21 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
             }
             missing += p == 0;
         }
-        if (ctl->tie == 1 && missing) {
+        if (C.tie == 1 && missing) {
             if (missing > 1) {
                 // two or more occur only before the tail window: the host path's full pass
-                ctl->status = LOOP_HOST;
-                ctl->n_host += 1;
+                to_host();
                 return;
             }
             // the only one missing occurs only earlier: its last occurrence is the earliest
             for (unsigned j = 0; j < n; ++j)
-                if ((tie_pos ? tie_pos[j] : res->last[j]) == 0) {
+                if ((tie_pos ? tie_pos[j] : R.last[j]) == 0) {
                     a = cand[j].x;
                     b = cand[j].y;
                 }
-            ctl->n_lone += 1;
+            ctl->n_lone = C.n_lone + 1;
         }
-        if (ctl->tie == 1) ctl->n_tail += 1;
+        if (C.tie == 1) ctl->n_tail = C.n_tail + 1;
         if (a < 0) {
             ctl->status = LOOP_ERROR;
             return;
@@ -1945,9 +1949,9 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
         }
         ctl->tie = 0;
     }
-    const int32_t c = ctl->next_id;
+    const int32_t c = C.next_id;
     len16[c] = len16[a] + len16[b];
-    const long long i = ctl->n_done;
+    const long long i = C.n_done;
     log[LOG_WORDS * i] = a;
     log[LOG_WORDS * i + 1] = b;
     log[LOG_WORDS * i + 2] = W;
