@@ -968,11 +968,13 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
         if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
             // full chunks of hot tokens only (a fresh corpus): unmasked adds
             unsigned long long cold = 1;
+#ifndef BPE_EXP_NOHOTPATH
             if (P63 == 0ull) {
                 const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1),
                                         max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
                 cold = __ballot(mx >= (uint32_t)HOT);
             }
+#endif
             if (cold == 0ull) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
