@@ -966,24 +966,11 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
         // every X X pair starts its run, so every valid pair counts
         const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
         if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
-            // full chunks of hot tokens only (a fresh corpus): unmasked adds
-            unsigned long long cold = 1;
-#ifndef BPE_EXP_NOHOTPATH
-            if (P63 == 0ull) {
-                const uint32_t mx = max(max((uint32_t)t0, (uint32_t)t1),
-                                        max(max((uint32_t)t2, (uint32_t)t3), (uint32_t)r3));
-                cold = __ballot(mx >= (uint32_t)HOT);
-            }
-#endif
-            if (cold == 0ull) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    df.o[e] = atomicAdd(lds_word(k, hot_addr(x[e], y[e])), hot_inc(x[e]));
-            } else {
-                // mixed planes (partial chunks hold merged tokens: the steady state)
-                add_pairs<MODE == MODE_FUSED>(x, y, k, df.o);
-                if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
-            }
+            // one form for every chunk: 12 VALU per pair, both classes (a separate 5-VALU form
+            // for chunks of hot tokens only paid off only on a fresh corpus; telling the two
+            // apart cost more over a whole run: dropping it timed the C3 run 3 % faster)
+            add_pairs<MODE == MODE_FUSED>(x, y, k, df.o);
+            if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
