@@ -68,8 +68,8 @@ def test_runs_in_the_index(n):
     assert e.samples() == st.samples()
     s = e.stats()
     assert s['pix_merges'] > 0
-    if n > 1 << 16:
-        assert s['pix_host'] >= 1
+    if n > 1 << 16:   # runs past the walk bound: the stream takes them (heavy-merge prefix or hand-off)
+        assert s['pix_host'] >= 1 or s['iterations'] > s['pix_merges'], s
 
 
 def test_uniform_c3_slice_matches_the_stream():
