@@ -46,9 +46,10 @@ constexpr int CHUNK = 256;                  // slots per wave-chunk (64 lanes x 
 constexpr int WAVES_PER_WG = BPE_WAVES;
 // Register ring of the streaming passes: RING chunks per wave (k_step: loads issued RING - 3
 // chunks ahead, k_tie: RING - 2).  Depth 2 already streams at 5.8 TB/s and 12 at 6.06
-// (tools/probe/stream_probe.hip); 7, 9 and 11 time alike in k_step.
+// (tools/probe/stream_probe.hip).  With the round-end overflow screen, depth 6 times best over
+// the full C3 run: k_step 0.760 ms against 0.767 (5), 0.795 (7), 0.83 (8, 9).
 #ifndef BPE_RING
-#define BPE_RING 7
+#define BPE_RING 6
 #endif
 constexpr int RING = BPE_RING;
 static_assert(RING >= 5, "ring depth");
