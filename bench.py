@@ -12,7 +12,8 @@ With N > 1 GPUs each rank holds its own contiguous 1 GiB shard of one corpus str
 scaling); the per-iteration pair-count exchange is an RCCL all-reduce enqueued on the engine's
 stream between the selection and apply kernels (the rank loop, bpe-tokenizer_amd/sharded.py).
 
-Prints ONE JSON line (rank 0).
+Prints ONE JSON line (rank 0), right after the timed region (the CPU baseline is measured before
+any GPU work).  --incremental adds a second line: the same workload in the incremental mode.
 """
 import argparse
 import importlib
@@ -138,8 +139,9 @@ def main():
     ap.add_argument('--cpu-sample-mib', type=int, default=256)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-incremental', action='store_true',
-                    help='skip the incremental-mode measurement reported beside the line')
+    ap.add_argument('--incremental', action='store_true',
+                    help='also run the incremental mode on the same workload, printed as a second '
+                         'JSON line after the bench line')
     args = ap.parse_args()
 
     import torch
@@ -148,6 +150,11 @@ def main():
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    # the CPU baseline first (host cores only, before any GPU work), so that nothing but the print
+    # follows the timed region
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s, args.corpus)
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
@@ -259,13 +266,14 @@ def main():
                 'exact_passes': st['exact_passes'],
             },
         }
-        if world == 1 and not args.no_incremental:
+        if cpu is not None:
+            out['cpu_baseline'] = cpu
+        print(json.dumps(out), flush=True)
+        if world == 1 and args.incremental:
+            trainer.engine.close()
             inc = incremental_mode(args, merges)
             inc['speedup_vs_stream_loop'] = (dt * 1e3 / args.steps) / inc['ms_per_step']
-            out['incremental_mode'] = inc
-        if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(args.cpu_sample_mib, args.cpu_budget_s, args.corpus)
-        print(json.dumps(out), flush=True)
+            print(json.dumps({'incremental_mode': inc}), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -35,6 +35,7 @@ C_API = [
     'bpe_get_stream', 'bpe_synth_latin1', 'bpe_synth_zipf', 'bpe_recount', 'bpe_export_counts',
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions', 'bpe_rank_loop_begin',
     'bpe_rank_loop_select', 'bpe_rank_loop_decide', 'bpe_rank_loop_count', 'bpe_rank_loop_end',
+    'bpe_cold_counts', 'bpe_set_global_counts',
 ]
 HOT_BINS = 65536
 TABLE_BINS = 81920
@@ -44,6 +45,10 @@ REDUCE_HOST = 1     # BPE_REDUCE_HOST
 MODE_STREAM = 0     # BPE_MODE_STREAM
 MODE_INCREMENTAL = 1   # BPE_MODE_INCREMENTAL
 LOOP_BATCH = 64     # BPE_LOOP_BATCH
+XCHG_HDR = 8        # BPE_XCHG_HDR
+DELTA_ROWS = 6      # BPE_DELTA_ROWS
+XCHG_WORDS = XCHG_HDR + DELTA_ROWS * MAX_VOCAB   # BPE_XCHG_WORDS
+TIE_WORDS = 32      # BPE_TIE_WORDS
 
 
 class BpeError(RuntimeError):
@@ -125,8 +130,10 @@ def lib():
                                i32p, ctypes.c_int64, i64p, i64p], ctypes.c_int),
         'bpe_tie_positions': ([vp, i32p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)],
                               ctypes.c_int),
-        'bpe_rank_loop_begin': ([vp, ctypes.c_int64, ctypes.c_int64, vp, vp, ctypes.c_int],
-                                ctypes.c_int),
+        'bpe_rank_loop_begin': ([vp, ctypes.c_int64, ctypes.c_int64, vp, vp, ctypes.c_int,
+                                 ctypes.c_int, i64p], ctypes.c_int),
+        'bpe_cold_counts': ([vp, vp, vp, ctypes.c_int64, i64p], ctypes.c_int),
+        'bpe_set_global_counts': ([vp, vp, vp, vp, ctypes.c_int64], ctypes.c_int),
         'bpe_rank_loop_select': ([vp], ctypes.c_int),
         'bpe_rank_loop_decide': ([vp], ctypes.c_int),
         'bpe_rank_loop_count': ([vp], ctypes.c_int),
@@ -387,9 +394,13 @@ class Engine:
         _check(lib().bpe_get_stream(self._ctx, ctypes.byref(st)), 'bpe_get_stream')
         return st.value or 0
 
-    def rank_loop_begin(self, max_length, min_weight, table_ptr, tie_ptr, rank):
+    def rank_loop_begin(self, max_length, min_weight, xchg_ptr, tie_ptr, rank, world):
+        """Returns the number of exchange words to all-reduce per iteration of this batch."""
+        nw = ctypes.c_int64()
         _check(lib().bpe_rank_loop_begin(self._ctx, int(max_length or 0), int(min_weight or 0),
-                                         table_ptr, tie_ptr, rank), 'bpe_rank_loop_begin')
+                                         xchg_ptr, tie_ptr, rank, world, ctypes.byref(nw)),
+               'bpe_rank_loop_begin')
+        return nw.value
 
     def rank_loop_select(self):
         _check(lib().bpe_rank_loop_select(self._ctx), 'bpe_rank_loop_select')
@@ -401,14 +412,31 @@ class Engine:
         _check(lib().bpe_rank_loop_count(self._ctx), 'bpe_rank_loop_count')
 
     def rank_loop_end(self):
-        """Syncs; returns ([(a, b, W)] merged in this batch, status) with status 0 = run on,
-        1 = no pair qualifies, 2 = the next iteration needs the host protocol."""
-        out = np.zeros(3 * LOOP_BATCH, np.int64)
+        """Syncs; returns ([(a, b, W)] merged in this batch, [this shard's replacement count of
+        each], status) with status 0 = run on, 1 = no pair qualifies, 2 = the next iteration needs
+        the host protocol."""
+        out = np.zeros(4 * LOOP_BATCH, np.int64)
         n, st = ctypes.c_int64(), ctypes.c_int()
         _check(lib().bpe_rank_loop_end(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                        LOOP_BATCH, ctypes.byref(n), ctypes.byref(st)),
                'bpe_rank_loop_end')
-        return [tuple(int(v) for v in out[3 * i:3 * i + 3]) for i in range(n.value)], st.value
+        k = n.value
+        return ([tuple(int(v) for v in out[4 * i:4 * i + 3]) for i in range(k)],
+                [int(out[4 * i + 3]) for i in range(k)], st.value)
+
+    def cold_counts(self, keys_ptr, counts_ptr, cap):
+        """This shard's exact count of every cold pair (one pass, kept for a second call): the
+        entry count (> cap: nothing written, call again with room)."""
+        n = ctypes.c_int64()
+        _check(lib().bpe_cold_counts(self._ctx, keys_ptr, counts_ptr, cap, ctypes.byref(n)),
+               'bpe_cold_counts')
+        return n.value
+
+    def set_global_counts(self, table_ptr, keys_ptr, counts_ptr, n):
+        """The maintained state of a sharded corpus: the global table and every shard's cold
+        lists (device pointers, duplicates summed) become this rank's global tables."""
+        _check(lib().bpe_set_global_counts(self._ctx, table_ptr, keys_ptr, counts_ptr, n),
+               'bpe_set_global_counts')
 
     def recount(self):
         """One plain streaming count pass (K1 alone; measurement helper)."""

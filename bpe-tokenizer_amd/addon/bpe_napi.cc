@@ -33,14 +33,23 @@ bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value *ar
     return argc >= want;
 }
 
+// An engine handle: the context behind a JS external.  destroyEngine() frees the context (its
+// device memory) at once; the holder itself goes with the external's finalizer.
+struct Holder {
+    bpe_ctx *c = nullptr;
+};
+
 void finalize_ctx(napi_env, void *data, void *) {
-    if (data) bpe_destroy(static_cast<bpe_ctx *>(data));
+    Holder *h = static_cast<Holder *>(data);
+    if (!h) return;
+    if (h->c) bpe_destroy(h->c);
+    delete h;
 }
 
 bpe_ctx *get_ctx(napi_env env, napi_value v) {
     void *p = nullptr;
-    if (napi_get_value_external(env, v, &p) != napi_ok) return nullptr;
-    return static_cast<bpe_ctx *>(p);
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) return nullptr;
+    return static_cast<Holder *>(p)->c;   // (null after destroyEngine: every call then fails)
 }
 
 int64_t get_i64(napi_env env, napi_value v) {
@@ -82,8 +91,23 @@ napi_value CreateEngine(napi_env env, napi_callback_info info) {
         return throw_native(env, "bpe_create");
     }
     napi_value ext;
-    napi_create_external(env, ctx, finalize_ctx, nullptr, &ext);
+    Holder *h = new Holder();
+    h->c = ctx;
+    napi_create_external(env, h, finalize_ctx, nullptr, &ext);
     return ext;
+}
+
+// destroyEngine(h): frees the context and its device memory now, not at garbage collection
+napi_value DestroyEngine(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "destroyEngine(h)");
+    void *p = nullptr;
+    if (napi_get_value_external(env, argv[0], &p) != napi_ok || !p)
+        return throw_arg(env, "destroyEngine expects an engine handle");
+    Holder *h = static_cast<Holder *>(p);
+    if (h->c) bpe_destroy(h->c);
+    h->c = nullptr;
+    return nullptr;
 }
 
 // deviceCount() -> number of HIP devices
@@ -340,8 +364,27 @@ napi_value MergeUntil(napi_env env, napi_callback_info info) {
     return out;
 }
 
+// The encoder's scratch engine (created on first use, destroyed with the addon's environment).
+bpe_ctx *g_scratch = nullptr;
+
+void destroy_scratch(void *) {
+    if (g_scratch) bpe_destroy(g_scratch);
+    g_scratch = nullptr;
+}
+
+bpe_ctx *scratch_engine(napi_env env) {
+    if (!g_scratch) {
+        if (bpe_create(&g_scratch, 0) != BPE_OK) {
+            g_scratch = nullptr;
+            return nullptr;
+        }
+        napi_add_env_cleanup_hook(env, destroy_scratch, nullptr);
+    }
+    return g_scratch;
+}
+
 // encodeMerges(Int32Array ids, Int32Array abc) -> Int32Array: one text through a run of merges
-// (a, b, c) on a scratch engine (bpe_apply_merges: encodeToCode's replay, core.ts:392-409)
+// (a, b, c) on the scratch engine (bpe_apply_merges: encodeToCode's replay, core.ts:392-409)
 napi_value EncodeMerges(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv)) return throw_arg(env, "encodeMerges(Int32Array, Int32Array)");
@@ -358,14 +401,19 @@ napi_value EncodeMerges(napi_env env, napi_callback_info info) {
     int32_t vocab = 0;
     for (size_t i = 0; i < n1; ++i) vocab = std::max(vocab, static_cast<const int32_t *>(ids)[i] + 1);
     for (size_t i = 0; i < n2; ++i) vocab = std::max(vocab, m[i] + 1);
-    bpe_ctx *ctx = nullptr;
-    if (bpe_create(&ctx, 0) != BPE_OK) return throw_native(env, "bpe_create");
+    // one scratch engine per addon instance, emptied between calls (its stream, tables and
+    // pinned buffers are set up once, and token lengths registered once per id)
+    bpe_ctx *ctx = scratch_engine(env);
+    if (!ctx) return throw_native(env, "bpe_create");
     struct Guard {
         bpe_ctx *c;
-        ~Guard() { bpe_destroy(c); }
+        ~Guard() { bpe_clear_corpus(c); }
     } guard{ctx};
+    if (bpe_clear_corpus(ctx) < 0) return throw_native(env, "bpe_clear_corpus");
     // lengths only matter to the max_length filter of a find, which never runs here
-    for (int32_t i = 0; i < vocab; ++i)
+    int32_t known = 0;
+    if (bpe_num_tokens(ctx, &known) < 0) return throw_native(env, "bpe_num_tokens");
+    for (int32_t i = known; i < vocab; ++i)
         if (bpe_set_token_len16(ctx, i, 1) < 0) return throw_native(env, "bpe_set_token_len16");
     if (bpe_add_sample(ctx, static_cast<const int32_t *>(ids), (int64_t)n1) < 0 ||
         bpe_apply_merges(ctx, m, (int64_t)(n2 / 3), nullptr, 0) < 0)
@@ -387,7 +435,8 @@ napi_value Init(napi_env env, napi_value exports) {
         const char *name;
         napi_callback cb;
     } fns[] = {
-        {"createEngine", CreateEngine}, {"deviceCount", DeviceCount},
+        {"createEngine", CreateEngine}, {"destroyEngine", DestroyEngine},
+        {"deviceCount", DeviceCount},
         {"setTokenLen16", SetTokenLen16}, {"addSample", AddSample},
         {"addLatin1", AddLatin1}, {"clearCorpus", ClearCorpus},
         {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},

@@ -52,6 +52,9 @@ constexpr int64_t REPLAY_BATCH = 256;
 
 static_assert(TABLE_BINS == BPE_TABLE_BINS && HOT_BINS == BPE_HOT_BINS, "include/bpe.h table layout");
 static_assert(MAX_CAND == BPE_MAX_CAND && LOOP_BATCH == BPE_LOOP_BATCH, "include/bpe.h rank loop sizes");
+static_assert(XCHG_HDR == BPE_XCHG_HDR && XCHG_WORDS == BPE_XCHG_WORDS && TIE_WORDS == BPE_TIE_WORDS &&
+                  DELTA_ROWS == BPE_DELTA_ROWS,
+              "include/bpe.h exchange layout");
 
 template <typename T>
 int dev_alloc(T **p, size_t n) {
@@ -144,16 +147,26 @@ struct bpe_ctx {
     std::vector<hipEvent_t> ev_pool;
     // device-resident mergeUntil loop: control block + merge log (pinned host mirrors)
     LoopCtl *d_ctl = nullptr, *h_ctl = nullptr;
-    long long *d_count = nullptr;   // per-token occurrence counts (maintained-table loop)
-    int64_t count_cap = 0;
     long long *d_log = nullptr, *h_log = nullptr;
     // apply-only replay: per-merge replacement counts
     unsigned long long *d_repl = nullptr, *h_repl = nullptr;
-    // sharded device loop (one rank): the caller's all-reduced table and tie positions
+    // sharded device loop (one rank): the caller's all-reduced exchange buffer (include/bpe.h
+    // BPE_XCHG_*: header + this shard's table, or + the delta rows) and tie positions
     unsigned long long *rl_table = nullptr, *rl_tie = nullptr;
-    int rl_rank = 0;
+    int rl_rank = 0, rl_world = 1;
     int64_t rl_base = 0, rl_enqueued = 0, rl_max_length = 0;
     bool rl_open = false;
+    // d_hot and the cold table hold the GLOBAL counts of a sharded corpus, replicated on every
+    // rank (bpe_set_global_counts): the rank loop keeps them merge by merge from the all-reduced
+    // delta rows.  Anything that needs this shard's own counts leaves that state first.
+    bool rl_global = false;
+    // the last batch's last merge left its delta rows in rl_table, not yet all-reduced: the next
+    // batch's first exchange carries them (same buffer)
+    bool rl_delta_pending = false;
+    int32_t rl_last_a = 0, rl_last_b = 0, rl_last_c = 0;
+    int64_t rl_last_w = -1;
+    // the cold table holds this shard's exact count of every cold pair (bpe_cold_counts)
+    bool cold_list = false;
 };
 
 namespace {
@@ -161,6 +174,17 @@ namespace {
 int set_device(bpe_ctx *c) {
     HIP_TRY(hipSetDevice(c->device));
     return BPE_OK;
+}
+
+// Before anything that reads or updates this shard's own counts: global tables (the sharded
+// maintained state) are dropped, and the next use recounts.
+void leave_global(bpe_ctx *c) {
+    if (!c->rl_global) return;
+    c->rl_global = false;
+    c->rl_delta_pending = false;
+    c->counts_valid = c->sketch_valid = c->best_ready = false;
+    c->cold_exact = false;
+    c->cold_list = false;
 }
 
 void geometry(bpe_ctx *c) {
@@ -208,6 +232,8 @@ int seal_packed(bpe_ctx *c) {
     c->packed = true;
     c->counts_valid = c->carry_valid = false;
     c->cold_exact = false;
+    c->rl_global = c->rl_delta_pending = false;
+    c->cold_list = false;
     geometry(c);
     return BPE_OK;
 }
@@ -257,6 +283,7 @@ static_assert(COLD_GRID * 256 >= HOT_BINS, "k_collect covers the hot bins");
 
 // Empties the cold table: free slots, zero dense counts (the invariant past n_used), n_used = 0.
 int cold_clear(bpe_ctx *c) {
+    c->cold_list = false;
     HIP_TRY(hipMemsetAsync(c->cold.slots, 0xFF, c->cold_cap * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(c->cold.dcounts, 0, c->cold_cap * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, 2 * sizeof(uint32_t), c->stream));
@@ -357,6 +384,21 @@ int settle(bpe_ctx *c);
 int settle_with(bpe_ctx *c, unsigned long long R);
 int maybe_compact(bpe_ctx *c);
 
+// One 160 KiB slab per workgroup of a counting pass (for the current geometry).
+int ensure_partials(bpe_ctx *c) {
+    geometry(c);
+    if (c->G > c->partials_wg) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        dfree(c->d_partials);
+        c->d_partials = nullptr;
+        c->partials_wg = 0;
+        int rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS);
+        if (rc) return rc;
+        c->partials_wg = c->G;
+    }
+    return BPE_OK;
+}
+
 // fused: a merge pass that also refreshes the maintained cold table (MODE_FUSED; the caller
 // invalidates the pairs with a side a or b before it and syncs the dense view after it)
 int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *replaced,
@@ -364,13 +406,8 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
     int rc;
     if (merge && c->pending)
         if ((rc = settle(c))) return rc;
-    geometry(c);
-    if (c->G > c->partials_wg) {   // one 160 KiB slab per workgroup of the pass
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        dfree(c->d_partials);
-        if ((rc = dev_alloc(&c->d_partials, (size_t)c->G * HIST_WORDS))) return rc;
-        c->partials_wg = c->G;
-    }
+    if ((rc = ensure_partials(c))) return rc;
+    c->cold_list = false;   // (fused and incremental passes update the cold table)
     if ((rc = sync_len16(c, c->opt_max_length))) return rc;   // the reduce's max_length filter
     hipStream_t s = c->stream;
     // the spill is zero here: zeroed once at create, then by every k_reduce_table
@@ -508,17 +545,31 @@ int compact(bpe_ctx *c) {
         return fail(BPE_ERR_STATE, "bpe native: compaction lost slots");
     std::swap(c->d_ids, c->d_tmp);
     const bool counts = c->counts_valid, cold_exact = c->cold_exact, sketch = c->sketch_valid;
+    const bool glob = c->rl_global, pend = c->rl_delta_pending, list = c->cold_list;
     if ((rc = seal_packed(c))) return rc;
     c->counts_valid = counts;
     c->sketch_valid = sketch;
     c->cold_exact = cold_exact;
+    c->rl_global = glob;
+    c->rl_delta_pending = pend;
+    c->cold_list = list;
     if (c->stats_on) c->stats.compactions += 1;
     return BPE_OK;
 }
 
+// Dead slots past the compaction threshold.
+bool compaction_due(const bpe_ctx *c);
+
 int maybe_compact(bpe_ctx *c) {
+    if (!compaction_due(c)) return BPE_OK;
+    int rc = compact(c);
+    if (rc) return rc;
+    return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout
+}
+
+bool compaction_due(const bpe_ctx *c) {
     const int64_t slots = c->n_chunks * CHUNK;
-    if (c->packed || slots < (1 << 20)) return BPE_OK;
+    if (c->packed || slots < (1 << 20)) return false;
     // dead slots cost a pass as much as live ones: re-pack once they are 1% of the stream (a
     // compaction costs about three passes; at C3 merge rates that is every ~700 merges; 3% timed
     // 0.8% slower per pass over the full C3 run)
@@ -527,10 +578,7 @@ int maybe_compact(bpe_ctx *c) {
         const int p = v ? atoi(v) : 99;
         return p >= 90 && p <= 99 ? p : 99;
     }();
-    if (c->live_slots * 100 >= slots * keep_pct) return BPE_OK;
-    int rc = compact(c);
-    if (rc) return rc;
-    return run_pass(c, false, 0, 0, 0, nullptr);         // rebuild carries for the new layout
+    return c->live_slots * 100 < slots * keep_pct;
 }
 
 // Exact counts of the cold pairs in the sketch buckets marked in d_heavy, into the sparse table
@@ -712,6 +760,7 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
             int64_t *w) {
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
     int rc;
+    leave_global(c);
     // with a maintained cold table the selection settles a pending merge from the Result it
     // copies back anyway, so the host does not wait for the merge pass before enqueueing it
     const bool deferred = c->pending && c->cold_exact && c->counts_valid;
@@ -768,6 +817,7 @@ int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc);
 
 int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
+    leave_global(c);
     if ((rc = register_merge(c, a, b, cc))) return rc;                 // core.ts:315-318
     if (replaced) *replaced = 0;
     if ((rc = settle(c))) return rc;
@@ -816,7 +866,9 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     int rc;
     *n_done = 0;
     *status = LOOP_DONE;
+    leave_global(c);
     if ((rc = settle(c))) return rc;
+    c->cold_list = false;
     c->opt_max_length = max_length;
     const bool maint = c->cold_exact && c->counts_valid && c->carry_valid &&
                        !getenv("BPE_DEBUG_NO_FUSED");
@@ -825,18 +877,6 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     const int64_t base = (int64_t)c->h_len16.size();
     if ((rc = ensure_len16_cap(c, base + n))) return rc;
-    if (maint) {
-        // this corpus's token counts, for the refresh fit check of each decision
-        if (c->count_cap < c->cap_vocab) {
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            dfree(c->d_count);
-            c->d_count = nullptr;
-            if ((rc = dev_alloc(&c->d_count, c->cap_vocab))) return rc;
-            c->count_cap = c->cap_vocab;
-        }
-        HIP_TRY(hipMemcpyAsync(c->d_count, c->h_count.data(), base * sizeof(long long),
-                               hipMemcpyHostToDevice, c->stream));
-    }
     // the device table must be exact below `base`: k_decide extends it
     if (c->len16_lo < base) {
         HIP_TRY(hipMemcpyAsync(c->d_len16 + c->len16_lo, c->h_len16.data() + c->len16_lo,
@@ -878,7 +918,6 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         // a few microseconds, about 3% of an iteration with all six
         c->span_mute = (c->span_tick++ % SPAN_EVERY) != 0;
         hipEvent_t e_sel = span_begin(c);
-        long long *cnt = maint ? c->d_count : nullptr;
         if (maint) {
             k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res,
                                                     c->d_ctl);
@@ -889,11 +928,9 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
                                                             c->d_res, c->d_cand, c->d_heavy,
                                                             c->d_ctl);
         }
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr,
-                                  cnt);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
         k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr,
-                                  cnt);
+        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr);
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
@@ -1005,18 +1042,49 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
 }
 
 // ---- the device loop on one rank of a sharded corpus ------------------------
-// Per iteration the caller enqueues, on this context's stream: all-reduce(SUM) of `table`,
-// rank_loop_select, all-reduce(MAX) of `tie`, rank_loop_decide, rank_loop_count.  Nothing syncs
-// the host until rank_loop_end, which reads the batch's merges back.
-int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *table,
-                    unsigned long long *tie, int rank) {
+// Per iteration the caller enqueues, on this context's stream: all-reduce(SUM) of the exchange
+// buffer's first *n_words words, rank_loop_select, all-reduce(MAX) of the BPE_TIE_WORDS tie words,
+// rank_loop_decide, rank_loop_count.  Nothing syncs the host until rank_loop_end, which reads the
+// batch's merges back.  Two states, the same on every rank:
+//  - table (the streaming pass's full recount): the exchange is the header + this shard's 81920-bin
+//    table, summed into the global table every rank selects from;
+//  - maintained (after bpe_set_global_counts: skewed corpora, large vocabularies): every rank
+//    holds the global hot and cold tables; a merge (a, b) -> c zeroes the pairs touching a or b
+//    in them, each shard recounts the pairs with a side in {a, b, c} on its own corpus (MODE_INCR)
+//    into delta rows, and the summed rows are added to every rank's tables (k_apply_delta).
+// The header's first word is this shard's replacement count of the merge just applied: summed,
+// it must equal W (checked on the device by the next decision, and for the batch's last merge by
+// the host from the log).
+int carry_pass(bpe_ctx *c);
+
+int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *xchg,
+                    unsigned long long *tie, int rank, int world, int64_t *n_words) {
     int rc;
-    c->cold_exact = false;
     if ((rc = settle(c))) return rc;
-    if ((rc = maybe_compact(c))) return rc;
+    const bool glob = c->rl_global;
     c->opt_max_length = max_length;
-    if (!table_ok(c) || !c->carry_valid)
-        if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    if (glob) {
+        // the global tables stay: a compaction keeps every count, and the carries are rebuilt
+        // without a counting pass (it would write this shard's counts over the global table)
+        if (compaction_due(c)) {
+            if (!c->carry_valid)
+                if ((rc = carry_pass(c))) return rc;
+            if ((rc = compact(c))) return rc;
+        }
+        if (!c->carry_valid)
+            if ((rc = carry_pass(c))) return rc;
+        if (c->rl_delta_pending && xchg != c->rl_table) {
+            // (another exchange buffer: the last merge's delta rows are not in it)
+            leave_global(c);
+            return rank_loop_begin(c, max_length, min_weight, xchg, tie, rank, world, n_words);
+        }
+    } else {
+        c->cold_exact = false;
+        if ((rc = maybe_compact(c))) return rc;
+        if (!table_ok(c) || !c->carry_valid)
+            if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
+    }
+    if ((rc = ensure_partials(c))) return rc;
     const int64_t base = (int64_t)c->h_len16.size();
     if ((rc = ensure_len16_cap(c, base + LOOP_BATCH))) return rc;
     if (c->len16_lo < base) {
@@ -1025,7 +1093,6 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
                                c->stream));
         c->len16_lo = base;
     }
-    geometry(c);
     hipStream_t s = c->stream;
     HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
     LoopCtl *h = c->h_ctl;
@@ -1036,33 +1103,67 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
     h->min_weight = min_weight == 0 ? 2 : min_weight;                   // core.ts:256
     h->sharded = 1;
     h->max_id = BPE_MAX_VOCAB;
+    h->last_rank = rank == world - 1;
+    h->maintained = glob ? 1 : 0;
+    h->cold_cap = c->cold_cap;
+    int64_t nw;
+    if (glob) {
+        // the delta rows of every token id a merge of this batch can see (<= base + LOOP_BATCH)
+        nw = XCHG_HDR + DELTA_ROWS * std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
+        if (c->rl_delta_pending) {
+            // the last batch's last merge: its rows go into this batch's first exchange
+            h->a = c->rl_last_a;
+            h->b = c->rl_last_b;
+            h->c = c->rl_last_c;
+            h->w = c->rl_last_w;
+        } else {
+            HIP_TRY(hipMemsetAsync(xchg, 0, nw * sizeof(unsigned long long), s));
+        }
+    } else {
+        nw = XCHG_HDR + TABLE_BINS;
+        HIP_TRY(hipMemsetAsync(xchg, 0, XCHG_HDR * sizeof(unsigned long long), s));
+        HIP_TRY(hipMemcpyAsync(xchg + XCHG_HDR, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
+                               hipMemcpyDeviceToDevice, s));
+    }
     HIP_TRY(hipMemcpyAsync(c->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
-    // this shard's table, to be summed over the ranks
-    HIP_TRY(hipMemcpyAsync(table, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
-                           hipMemcpyDeviceToDevice, s));
-    c->rl_table = table;
+    c->rl_delta_pending = false;
+    c->cold_list = false;
+    c->rl_table = xchg;
     c->rl_tie = tie;
     c->rl_rank = rank;
+    c->rl_world = world;
     c->rl_base = base;
     c->rl_enqueued = 0;
     c->rl_max_length = max_length;
     c->rl_open = true;
     c->best_ready = false;
+    *n_words = nw;
     return BPE_OK;
 }
 
-// From the all-reduced table: the best key, its pairs, the decision (or the tie pass, whose
-// positions go to `tie` for the all-reduce(MAX)).
+// From the all-reduced exchange: the global table (or the maintained tables after the delta),
+// the best key, its pairs, the proposal (or the tie pass, whose positions go to `tie` with this
+// rank's vote for the all-reduce(MAX)).
 int rank_loop_select(bpe_ctx *c) {
     if (!c->rl_open || c->rl_enqueued >= LOOP_BATCH)
         return fail(BPE_ERR_STATE, "bpe native: rank loop not begun, or its batch is full");
     hipStream_t s = c->stream;
     const int64_t ml = c->rl_max_length;
     hipEvent_t e_sel = span_begin(c);
-    k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->rl_table, c->d_len16, ml, c->d_res, c->d_ctl);
-    k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->rl_table, c->d_len16, ml, c->d_res,
-                                                    c->d_cand, c->d_heavy, c->d_ctl);
-    k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
+    if (c->rl_global) {
+        k_apply_delta<<<COLD_GRID, 256, 0, s>>>(c->rl_table, c->d_hot, c->cold, c->d_ctl);
+        k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, ml, c->d_res, c->d_ctl);
+        k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, ml, c->d_res, c->d_ctl);
+        k_collect<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, ml, c->d_res, c->d_cand,
+                                            c->d_ctl);
+    } else {
+        const unsigned long long *table = c->rl_table + XCHG_HDR;
+        k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(table, c->d_len16, ml, c->d_res, c->d_ctl);
+        k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(table, c->d_len16, ml, c->d_res, c->d_cand,
+                                                        c->d_heavy, c->d_ctl);
+    }
+    k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr,
+                              c->rl_table);
     TieArgs A;
     memset(&A, 0, sizeof A);
     A.ids = c->d_ids;
@@ -1079,42 +1180,61 @@ int rank_loop_select(bpe_ctx *c) {
     return span_end(c, e_sel, 1);
 }
 
-// After the all-reduce(MAX) of `tie`: the decision of a tied iteration.
+// After the all-reduce(MAX) of `tie`: the decision, the same on every rank.
 int rank_loop_decide(bpe_ctx *c) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
     k_decide<<<1, 64, 0, c->stream>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1,
-                                      c->rl_tie);
+                                      c->rl_tie, c->rl_table);
     HIP_TRY(hipGetLastError());
     return BPE_OK;
 }
 
-// Applies the decided merge to this shard and counts it: this shard's table into `table`.
+// Applies the decided merge to this shard and counts it: this shard's table (or delta rows) and
+// its replacement count into the exchange buffer.
 int rank_loop_count(bpe_ctx *c) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
     hipStream_t s = c->stream;
+    unsigned long long *x = c->rl_table;
     hipEvent_t e_step = span_begin(c);
-    k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
-                                    c->d_partials, c->d_spill, c->cold, c->d_sums,
-                                    &c->d_res->replaced);
+    if (c->rl_global) {
+        k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl);
+        k_step_loop<MODE_INCR><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
+                                                   c->d_ctl, c->d_partials, c->d_spill, c->cold,
+                                                   c->d_sums, &c->d_res->replaced, c->d_hot, x);
+    } else {
+        k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
+                                        c->d_partials, c->d_spill, c->cold, c->d_sums,
+                                        &c->d_res->replaced);
+    }
     HIP_TRY(hipGetLastError());
     int rc;
     if ((rc = span_end(c, e_step, 0))) return rc;
     hipEvent_t e_red = span_begin(c);
-    k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
-                                                          c->cold, c->d_heavy, c->d_ctl);
-    k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
-        c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->rl_max_length, nullptr, c->d_ctl);
+    if (c->rl_global) {
+        k_runs<MODE_INCR><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry, c->d_spill,
+                                                             c->cold, c->d_heavy, c->d_ctl, -1, -1,
+                                                             -1, c->d_hot, x);
+        k_reduce_rows<<<4 * INCR_RLIM / 2 / RR_COLS, 256, 0, s>>>(
+            c->d_partials, c->G, c->d_spill, c->d_hot, c->cold, -1, -1, -1, c->d_ctl, x,
+            &c->d_res->replaced);
+    } else {
+        k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
+                                                              c->d_spill, c->cold, c->d_heavy,
+                                                              c->d_ctl);
+        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+            c->d_partials, c->G, c->d_spill, x + XCHG_HDR, c->d_len16, c->rl_max_length, nullptr,
+            c->d_ctl, x, &c->d_res->replaced);
+    }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->rl_table, c->d_hot, TABLE_BINS * sizeof(unsigned long long),
-                           hipMemcpyDeviceToDevice, s));
     c->rl_enqueued += 1;
     return span_end(c, e_red, 1);
 }
 
-// Syncs, reads the batch's merges back (out_abw: (a, b, W) triples) and updates the host tables
-// with this shard's replacement counts.  *status: LOOP_RUN (every enqueued iteration merged),
-// LOOP_DONE (no pair qualifies), LOOP_HOST (the next iteration needs the host protocol).
-int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, int *status) {
+// Syncs, reads the batch's merges back (out_abwr: (a, b, W, this shard's replacement count)
+// quadruples) and updates the host tables with this shard's counts.  *status: LOOP_RUN (every
+// enqueued iteration merged), LOOP_DONE (no pair qualifies), LOOP_HOST (the next iteration needs
+// the host protocol).
+int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *status) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
     c->rl_open = false;
     hipStream_t s = c->stream;
@@ -1124,7 +1244,13 @@ int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, in
     HIP_TRY(hipMemcpyAsync(c->h_log, c->d_log, LOG_WORDS * LOOP_BATCH * sizeof(long long),
                            hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (h->status == LOOP_ERROR) return fail(BPE_ERR_STATE, "bpe native: rank loop: tie pass found no occurrence");
+    const bool glob = c->rl_global;
+    if (h->status == LOOP_ERROR) {
+        leave_global(c);
+        c->counts_valid = false;
+        return fail(BPE_ERR_STATE, "bpe native: rank loop: the shards' replacement counts do not "
+                                   "sum to W, or a tie pass found no occurrence");
+    }
     const int64_t nd = h->n_done;
     if (nd < 0 || nd > c->rl_enqueued) return fail(BPE_ERR_STATE, "bpe native: rank loop: bad merge count");
     const int64_t base = c->rl_base;
@@ -1152,11 +1278,13 @@ int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, in
             c->stats.step_launches += 1;
             c->stats.step_slots += c->n_chunks * CHUNK;
             c->stats.step_live += c->n_live;
+            if (glob) c->stats.fused_passes += 1;
         }
         if (i < cap) {
-            out_abw[3 * i] = a;
-            out_abw[3 * i + 1] = b;
-            out_abw[3 * i + 2] = W;
+            out[4 * i] = a;
+            out[4 * i + 1] = b;
+            out[4 * i + 2] = W;
+            out[4 * i + 3] = R;
         }
     }
     c->len16_lo = base + nd;
@@ -1166,10 +1294,99 @@ int rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_done, in
         c->stats.tie_lone += h->n_lone;
         c->stats.loop_host += h->n_host;
     }
-    c->counts_valid = c->carry_valid = c->sketch_valid = true;   // d_hot: this shard's table
+    c->carry_valid = true;   // (the last pass's carries)
     c->best_ready = false;
+    const bool all = h->status == LOOP_RUN && nd == c->rl_enqueued;
+    if (glob) {
+        if (all && nd > 0) {
+            // the last merge's delta rows wait in the exchange buffer for the next batch's first
+            // all-reduce
+            const long long *m = c->h_log + LOG_WORDS * (nd - 1);
+            c->rl_delta_pending = true;
+            c->rl_last_a = (int32_t)m[0];
+            c->rl_last_b = (int32_t)m[1];
+            c->rl_last_c = (int32_t)(base + nd - 1);
+            c->rl_last_w = m[2];
+        } else if (!all) {
+            leave_global(c);   // (the host path takes over: this shard's counts are recounted)
+        }
+    } else if (all && nd > 0) {
+        // the last count left this shard's table in the exchange buffer, not summed since
+        HIP_TRY(hipMemcpyAsync(c->d_hot, c->rl_table + XCHG_HDR, TABLE_BINS * sizeof(unsigned long long),
+                               hipMemcpyDeviceToDevice, s));
+        c->counts_valid = c->sketch_valid = true;
+    } else if (nd > 0 || !all) {
+        // (the exchange buffer was summed again after the batch ended: recount when needed)
+        c->counts_valid = false;
+    }
     *n_done = nd;
     *status = h->status;
+    return BPE_OK;
+}
+
+// This shard's exact count of every cold pair (an id >= 256), for the global tables of the
+// sharded maintained state: one exact streaming pass (kept: a second call with a bigger buffer
+// exports the same list without another pass).
+int cold_counts(bpe_ctx *c, uint32_t *keys, unsigned long long *counts, int64_t cap, int64_t *n) {
+    int rc;
+    leave_global(c);
+    if ((rc = settle(c))) return rc;
+    if (!c->cold_list) {
+        hipStream_t s = c->stream;
+        if (c->n_live >= 2) {
+            HIP_TRY(hipMemsetAsync(c->d_heavy, 0xFF, HEAVY_WORDS * sizeof(uint32_t), s));
+            if ((rc = exact_pass(c))) return rc;
+        } else {
+            if ((rc = cold_clear(c))) return rc;
+            c->cold_used = 0;
+        }
+        c->cold_list = true;
+    }
+    *n = (int64_t)c->cold_used;
+    if (*n > cap) return BPE_OK;
+    if (*n) {
+        if (!keys || !counts) return fail(BPE_ERR_ARG, "bpe native: null cold buffers");
+        k_export_cold<<<256, 256, 0, c->stream>>>(c->cold, keys, counts);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return BPE_OK;
+}
+
+// Loads the global maintained state of a sharded corpus: the hot bins of the global table and
+// the cold pairs of every shard (duplicates summed).  The next rank loop batch keeps them.
+int set_global_counts(bpe_ctx *c, const unsigned long long *table, const uint32_t *keys,
+                      const unsigned long long *counts, int64_t n) {
+    int rc;
+    leave_global(c);
+    if ((rc = settle(c))) return rc;
+    if (n < 0 || (n && (!keys || !counts))) return fail(BPE_ERR_ARG, "bpe native: bad global counts");
+    hipStream_t s = c->stream;
+    // room for every distinct pair at half fill, and for the claims of the merges to come (the
+    // decisions hand over to the host before 3/4 fill)
+    if ((rc = ensure_cold(c, 0, 4 * (uint64_t)n + 4096))) return rc;
+    for (int attempt = 0;; ++attempt) {
+        if ((rc = cold_clear(c))) return rc;
+        HIP_TRY(hipMemcpyAsync(c->d_hot, table, HOT_BINS * sizeof(unsigned long long),
+                               hipMemcpyDeviceToDevice, s));
+        if (n) k_load_cold<<<1024, 256, 0, s>>>(c->cold, keys, counts, n);
+        HIP_TRY(hipGetLastError());
+        uint32_t flags[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!flags[1] && (uint64_t)flags[0] * 4 <= c->cold_cap) {
+            c->cold_used = flags[0];
+            break;
+        }
+        if (attempt == 2) return fail(BPE_ERR_STATE, "bpe native: global cold table overflow");
+        if ((rc = ensure_cold(c, 0, 2 * c->cold_cap))) return rc;
+    }
+    c->rl_global = true;
+    c->rl_delta_pending = false;
+    c->counts_valid = true;
+    c->sketch_valid = false;
+    c->cold_exact = false;   // (the single-context maintained state is not this one)
+    c->best_ready = false;
     return BPE_OK;
 }
 
@@ -1207,6 +1424,7 @@ int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
 // extra pass.  replaced (may be null) receives each merge's replacement count.
 int replay(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, bool count_after) {
     int rc;
+    leave_global(c);
     if ((rc = settle(c))) return rc;
     const int64_t n_plain = count_after ? n - 1 : n;
     for (int64_t i0 = 0; i0 < n_plain;) {
@@ -1574,6 +1792,7 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     int64_t n = 0;
     const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
     int builds = 0;
+    leave_global(c);
     // Heavy merges first on the stream: a merge costs the index O(W) (plus contention on the
     // new pairs' slots when W is large), the stream one pass whatever W.  While the next merge's
     // W exceeds max(2^16, n_live / 8192) (C3: 131 K against W = 16 K, so never; a skewed corpus's
@@ -1835,7 +2054,7 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
-                    c->d_ctl, c->d_log, c->d_repl, c->d_count};
+                    c->d_ctl, c->d_log, c->d_repl};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
@@ -2079,14 +2298,33 @@ int bpe_apply_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *repla
     return do_apply(c, a, b, cc, replaced);
 }
 
-int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint64_t *table,
-                        uint64_t *tie, int rank) {
+int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint64_t *xchg,
+                        uint64_t *tie, int rank, int world, int64_t *xchg_words) {
     NOT_MULTI;
-    if (!c || !table || !tie || rank < 0) return fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
+    if (!c || !xchg || !tie || rank < 0 || world < 1 || rank >= world || !xchg_words)
+        return fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
     int rc = set_device(c);
     if (rc) return rc;
-    return rank_loop_begin(c, max_length, min_weight, (unsigned long long *)table,
-                           (unsigned long long *)tie, rank);
+    return rank_loop_begin(c, max_length, min_weight, (unsigned long long *)xchg,
+                           (unsigned long long *)tie, rank, world, xchg_words);
+}
+
+int bpe_cold_counts(bpe_ctx *c, uint32_t *keys, uint64_t *counts, int64_t cap, int64_t *n) {
+    NOT_MULTI;
+    if (!c || !n || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return cold_counts(c, keys, (unsigned long long *)counts, cap, n);
+}
+
+int bpe_set_global_counts(bpe_ctx *c, const uint64_t *table, const uint32_t *keys,
+                          const uint64_t *counts, int64_t n) {
+    NOT_MULTI;
+    if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return set_global_counts(c, (const unsigned long long *)table, keys,
+                             (const unsigned long long *)counts, n);
 }
 
 int bpe_rank_loop_select(bpe_ctx *c) {
@@ -2110,12 +2348,12 @@ int bpe_rank_loop_count(bpe_ctx *c) {
     return rc ? rc : rank_loop_count(c);
 }
 
-int bpe_rank_loop_end(bpe_ctx *c, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status) {
+int bpe_rank_loop_end(bpe_ctx *c, int64_t *out_abwr, int64_t cap, int64_t *n_merges, int *status) {
     NOT_MULTI;
-    if (!c || !n_merges || !status || (cap > 0 && !out_abw))
+    if (!c || !n_merges || !status || (cap > 0 && !out_abwr))
         return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
-    return rc ? rc : rank_loop_end(c, out_abw, cap, n_merges, status);
+    return rc ? rc : rank_loop_end(c, out_abwr, cap, n_merges, status);
 }
 
 int bpe_apply_merges(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, int count_after) {
@@ -2226,6 +2464,7 @@ int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
     if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
+    leave_global(c);
     if ((rc = settle(c))) return rc;
     if (!table_ok(c))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
@@ -2241,6 +2480,7 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     if (!c || !table || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
+    leave_global(c);
     if ((rc = settle(c))) return rc;
     if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
@@ -2358,6 +2598,7 @@ int bpe_recount(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
+    leave_global(c);
     if ((rc = settle(c))) return rc;
     return run_pass(c, false, 0, 0, 0, nullptr);
 }

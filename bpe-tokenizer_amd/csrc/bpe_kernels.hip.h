@@ -169,8 +169,16 @@ struct LoopCtl {
     // the maintained cold-pair table (skewed corpora): selection reads it instead of the sketch,
     // each merge pass refreshes it (MODE_FUSED); cold_cap = its capacity (for the fill limits)
     int32_t maintained;
-    int32_t pad_;
+    // sharded: this rank holds the corpus tail (the tie pass's tail window scans it alone)
+    int32_t last_rank;
     unsigned long long cold_cap;
+    // sharded: this rank asks the others to hand the iteration to the host (its copy of the
+    // maintained tables is too full, or dead, or the merge's refresh might not fit: facts that
+    // differ between ranks, so they travel through the tie all-reduce(MAX) before any decision)
+    int32_t vote;
+    // sharded: the single candidate chosen before the vote (tie == 3)
+    int32_t pend_a, pend_b;
+    int32_t pad_;
 };
 
 // Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
@@ -307,7 +315,31 @@ struct Sink {
     // (global u64 [4 * INCR_RLIM])
     unsigned long long *hot;
     unsigned long long *rspill;
+    // MODE_INCR on a rank of a sharded corpus: the touched pairs' counts go to this shard's delta
+    // rows (summed over the ranks, then added to every rank's copy of the global tables by
+    // k_apply_delta) instead of straight into the tables
+    unsigned long long *delta;
 };
+
+// Delta rows of the sharded maintained state (include/bpe.h BPE_XCHG_*): the pairs a merge
+// (a, b) -> c can change, at HDR + 6 * other + row, rows in precedence order (a, .) (b, .)
+// (., a) (., b) (c, .) (., c).  Every touched pair has a side in {a, b, c}: each maps to one slot.
+constexpr int XCHG_HDR = 8;
+constexpr int DELTA_ROWS = 6;
+constexpr int XCHG_WORDS = XCHG_HDR + DELTA_ROWS * 55296;   // BPE_MAX_VOCAB
+static_assert(XCHG_WORDS >= XCHG_HDR + TABLE_BINS, "exchange buffer holds the table too");
+
+__device__ __forceinline__ uint32_t delta_slot(int32_t x, int32_t y, int32_t a, int32_t b,
+                                                int32_t c) {
+    int row, other;
+    if (x == a) { row = 0; other = y; }
+    else if (x == b) { row = 1; other = y; }
+    else if (y == a) { row = 2; other = x; }
+    else if (y == b) { row = 3; other = x; }
+    else if (x == c) { row = 4; other = y; }
+    else { row = 5; other = x; }
+    return (uint32_t)(XCHG_HDR + DELTA_ROWS * other + row);
+}
 
 template <int MODE>
 __device__ __forceinline__ bool exact_wanted(const Sink &k, int32_t x, int32_t y) {
@@ -328,6 +360,10 @@ __device__ __forceinline__ bool incr_touched(const Sink &k, int32_t x, int32_t y
 // MODE_INCR: n occurrences of a touched pair straight into the maintained tables.
 __device__ __forceinline__ void incr_global_add(const Sink &k, int32_t x, int32_t y,
                                                 unsigned long long n) {
+    if (k.delta) {
+        atomicAdd(&k.delta[delta_slot(x, y, k.ma, k.mb, k.mc)], n);
+        return;
+    }
     if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT)
         atomicAdd(&k.hot[hot_bin((uint32_t)x, (uint32_t)y)], n);
     else
@@ -1205,8 +1241,10 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                                           const uint32_t *__restrict__ heavy_g,
                                           RegionSum *__restrict__ sums,
                                           unsigned long long *__restrict__ replaced,
-                                          unsigned long long *__restrict__ hot_g = nullptr) {
-    // (MODE_INCR: `spill` holds the rows' spill, 4 * INCR_RLIM u64; hot_g the maintained table)
+                                          unsigned long long *__restrict__ hot_g = nullptr,
+                                          unsigned long long *__restrict__ delta = nullptr) {
+    // (MODE_INCR: `spill` holds the rows' spill, 4 * INCR_RLIM u64; hot_g the maintained table;
+    // delta: a sharded rank's delta rows, which then take the touched pairs instead of the tables)
     unsigned long long *rspill = spill;
     if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
         // (MODE_FUSED: the LDS hash's keys start EMPTY; one store per dword, so no two threads
@@ -1244,6 +1282,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.mc = mc;
     k.hot = hot_g;
     k.rspill = rspill;
+    k.delta = delta;
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6)));
     if (r < R) {
@@ -1450,16 +1489,17 @@ k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
             const RegionCarry *__restrict__ carry, const LoopCtl *__restrict__ ctl,
             uint32_t *__restrict__ partials, unsigned long long *__restrict__ spill, ColdTable ct,
             RegionSum *__restrict__ sums, unsigned long long *__restrict__ replaced,
-            unsigned long long *__restrict__ hot_g = nullptr) {
+            unsigned long long *__restrict__ hot_g = nullptr,
+            unsigned long long *__restrict__ delta = nullptr) {
     __shared__ __attribute__((aligned(16))) uint32_t hist[HIST_WORDS];
     if (ctl->status != LOOP_RUN) return;
     const int32_t ma = ctl->a, mb = ctl->b, mc = ctl->c;
     if (ma == mb)
         step_body<MERGE_XX, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
-                                  ct, nullptr, sums, replaced, hot_g);
+                                  ct, nullptr, sums, replaced, hot_g, delta);
     else
         step_body<MERGE_XY, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
-                                  ct, nullptr, sums, replaced, hot_g);
+                                  ct, nullptr, sums, replaced, hot_g, delta);
 }
 
 __device__ __forceinline__ int prev_nonempty(const RegionSum *s, int q) {
@@ -1483,7 +1523,8 @@ template <int MODE>
 __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__restrict__ carry,
                        unsigned long long *__restrict__ spill, ColdTable ct,
                        const uint32_t *__restrict__ heavy, const LoopCtl *ctl, int32_t ma = -1,
-                       int32_t mb = -1, int32_t mc = -1, unsigned long long *hot = nullptr) {
+                       int32_t mb = -1, int32_t mc = -1, unsigned long long *hot = nullptr,
+                       unsigned long long *delta = nullptr) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R || loop_off(ctl)) return;
     if ((MODE == MODE_FUSED || MODE == MODE_INCR) && ctl) {   // (device loop: the merge applied)
@@ -1501,6 +1542,7 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.mc = mc;
     k.hot = hot;
     k.rspill = nullptr;
+    k.delta = delta;
     const int p = prev_nonempty(s, r - 1);
     const int nx = next_nonempty(s, r + 1, R);
     RegionCarry rc;
@@ -1569,10 +1611,14 @@ __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len
 __global__ void __launch_bounds__(256)
 k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ spill,
                unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
-               int64_t max_length, Result *res, const LoopCtl *ctl) {
+               int64_t max_length, Result *res, const LoopCtl *ctl,
+               unsigned long long *__restrict__ hdr = nullptr,
+               const unsigned long long *__restrict__ rep = nullptr) {
     __shared__ uint32_t s_sum[8][32][8];
     if (loop_off(ctl)) return;
     const int t = threadIdx.x;
+    // (sharded: the exchange header carries this shard's replacement count, summed with the table)
+    if (hdr && rep && blockIdx.x == 0 && t == 0) hdr[0] = *rep;
     const int wl = t & 31, grp = t >> 5;
     const int w0 = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * wl;   // first of my 4 words
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                 // < 2^23 each: G <= 256 x 2^15
@@ -1809,21 +1855,27 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
 }
 
 // The device loop's decision: do_find's selection tail (core.ts:294-318) without leaving the GPU.
-// phase 0, after k_select_multi: checks the previous merge's replacement count against its W, then
-// ends the batch (no pair or W < min_weight: LOOP_DONE; heavy sketch buckets or more than MAX_CAND
-// candidates: LOOP_HOST, the host path takes that iteration), waits for the tie pass (several
-// candidates), or decides.  phase 1, after k_tie: the candidate whose last counted occurrence is
-// earliest (rule R3).  A decision logs (a, b, W), registers the new token's UTF-16 length
-// (core.ts:318) and clears the Result for the next pass.  One thread.
+// phase 0, after the selection kernels: checks the previous merge's replacement count against its
+// W, then ends the batch (no pair or W < min_weight: LOOP_DONE; heavy sketch buckets or more than
+// MAX_CAND candidates: LOOP_HOST, the host path takes that iteration), waits for the tie pass
+// (several candidates), or decides.  phase 1, after k_tie: the candidate whose last counted
+// occurrence is earliest (rule R3).  A decision logs (a, b, W), registers the new token's UTF-16
+// length (core.ts:318) and clears the Result for the next pass.  One thread.
 //
 // With a maintained cold table (ctl->maintained) the selection read that table, not the sketch:
 // the batch hands over to the host when the table overflowed, is 3/4 full, is more than half dead
 // claims (it is then rebuilt), or when the refresh of the chosen merge might not fit (2 claims
-// per replacement at most).  count: this corpus's per-token occurrence counts, kept up to date
-// here with W (the host reads them back at the batch end).
+// per replacement at most).
+//
+// One rank of a sharded corpus (ctl->sharded): the replacement count checked is the SUM over the
+// ranks (the exchange header `hdr`, all-reduced with the table or the delta rows).  Phase 0 only
+// proposes (ctl->tie: 1 / 2 tie pass in the tail window / over the whole shard, 3 one candidate,
+// 4 no merge, 5 the host path) and votes: the reasons above that depend on this rank's copy of the
+// maintained tables (fill, dead claims, room) differ between ranks, so they ride in the tie
+// all-reduce(MAX) (tie_pos[MAX_CAND]) and phase 1 decides on every rank alike.
 __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
                          long long *log, int phase, const unsigned long long *__restrict__ tie_pos,
-                         long long *__restrict__ count = nullptr) {
+                         const unsigned long long *__restrict__ hdr = nullptr) {
     if (threadIdx.x != 0) return;
     // Snapshots of the control block and the Result (their loads issue together: one memory
     // latency instead of a chain of dependent ones); the fields are written back one by one.
@@ -1849,36 +1901,38 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
     };
     if (phase == 0) {
         if (C.w >= 0) {
-            // the previous merge's replacement count: == W on the whole corpus, logged per shard
-            if (!C.sharded && R.replaced != (unsigned long long)C.w) {
+            // the previous merge's replacement count: == W on the whole corpus (sharded: summed
+            // over the ranks in the exchange header); this corpus's own count is logged
+            const unsigned long long total = C.sharded && hdr ? hdr[0] : R.replaced;
+            if ((C.sharded && !hdr) || total != (unsigned long long)C.w) {
                 ctl->status = LOOP_ERROR;
                 return;
             }
-            log[LOG_WORDS * (C.n_done - 1) + 3] = (long long)R.replaced;
+            // (a sharded batch may open on the last batch's last merge: not in this log)
+            if (C.n_done > 0) log[LOG_WORDS * (C.n_done - 1) + 3] = (long long)R.replaced;
         }
         ctl->w = -1;
+        int vote = 0;
         if (C.maintained) {
             const unsigned long long used = R.cold_flags & 0xFFFFFFFFull;
             if ((R.cold_flags >> 32) || used * 4 > C.cold_cap * 3 ||
-                2 * R.cold_dead > used + 65536) {
-                to_host();
-                return;
-            }
-        } else if (R.n_heavy) {
+                2 * R.cold_dead > used + 65536)
+                vote = 1;
+        }
+        if (!room()) vote = 1;
+        // the proposal: LOOP_DONE (4), the host path (5), a tie pass (1, 2) or one candidate (3)
+        int prop;
+        if (vote && !C.sharded) {
+            prop = 5;
+        } else if (!C.maintained && R.n_heavy) {
             // a heavy sketch bucket may hold a cold pair above the best hot one (even when no
             // hot pair exists at all): only the host path's exact counts can tell
-            to_host();
-            return;
-        }
-        if (best == 0 || W < C.min_weight) {                      // core.ts:312-313
-            ctl->status = LOOP_DONE;
-            return;
-        }
-        if (n == 0 || n > (unsigned)MAX_CAND || C.next_id >= C.max_id) {
-            to_host();
-            return;
-        }
-        if (n > 1) {
+            prop = 5;
+        } else if (best == 0 || W < C.min_weight) {                  // core.ts:312-313
+            prop = 4;
+        } else if (n == 0 || n > (unsigned)MAX_CAND || C.next_id >= C.max_id) {
+            prop = 5;
+        } else if (n > 1) {
             // the same candidate order on every rank (the collection order is not): by (a, b)
             for (unsigned j = 1; j < n; ++j) {
                 const int2 v = cand[j];
@@ -1887,55 +1941,89 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
                     cand[i] = cand[i - 1];
                 cand[i] = v;
             }
-            // X Y candidates only (one corpus): the tail window first; else the full pass
-            int all_xy = !C.sharded;
+            // X Y candidates only: the corpus tail window first (a sharded corpus's tail is the
+            // last rank's); else the full pass
+            int all_xy = 1;
             for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
             for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
-            ctl->tie = all_xy ? 1 : 2;
             ctl->n_tie = C.n_tie + 1;
-            return;
+            prop = all_xy ? 1 : 2;
+        } else {
+            prop = 3;
         }
-        a = cand0.x;
-        b = cand0.y;
-        if (!room()) {
-            to_host();
+        if (!C.sharded) {
+            if (prop == 4) {
+                ctl->status = LOOP_DONE;
+                return;
+            }
+            if (prop == 5) {
+                to_host();
+                return;
+            }
+            if (prop != 3) {
+                ctl->tie = prop;
+                return;
+            }
+            a = cand0.x;
+            b = cand0.y;
+        } else {
+            ctl->tie = prop;
+            ctl->vote = vote;
+            ctl->pend_a = cand0.x;
+            ctl->pend_b = cand0.y;
             return;
         }
     } else {
         if (!C.tie) return;
-        unsigned long long bp = ~0ull;
-        unsigned missing = 0;
-        for (unsigned j = 0; j < n; ++j) {
-            const unsigned long long p = tie_pos ? tie_pos[j] : R.last[j];
-            if (p && p < bp) {
-                bp = p;
-                a = cand[j].x;
-                b = cand[j].y;
-            }
-            missing += p == 0;
-        }
-        if (C.tie == 1 && missing) {
-            if (missing > 1) {
-                // two or more occur only before the tail window: the host path's full pass
+        if (C.sharded) {
+            ctl->tie = 0;
+            if (tie_pos[MAX_CAND] || C.tie == 5) {   // some rank voted for the host path
                 to_host();
                 return;
             }
-            // the only one missing occurs only earlier: its last occurrence is the earliest
-            for (unsigned j = 0; j < n; ++j)
-                if ((tie_pos ? tie_pos[j] : R.last[j]) == 0) {
+            if (C.tie == 4) {
+                ctl->status = LOOP_DONE;
+                return;
+            }
+        }
+        if (C.tie == 3) {
+            a = C.pend_a;
+            b = C.pend_b;
+        } else {
+            unsigned long long bp = ~0ull;
+            unsigned missing = 0;
+            for (unsigned j = 0; j < n; ++j) {
+                const unsigned long long p = tie_pos ? tie_pos[j] : R.last[j];
+                if (p && p < bp) {
+                    bp = p;
                     a = cand[j].x;
                     b = cand[j].y;
                 }
-            ctl->n_lone = C.n_lone + 1;
-        }
-        if (C.tie == 1) ctl->n_tail = C.n_tail + 1;
-        if (a < 0) {
-            ctl->status = LOOP_ERROR;
-            return;
-        }
-        if (!room()) {
-            to_host();
-            return;
+                missing += p == 0;
+            }
+            if (C.tie == 1 && missing) {
+                if (missing > 1) {
+                    // two or more occur only before the tail window: the host path's full pass
+                    to_host();
+                    return;
+                }
+                // the only one missing occurs only earlier: its last occurrence is the earliest
+                for (unsigned j = 0; j < n; ++j)
+                    if ((tie_pos ? tie_pos[j] : R.last[j]) == 0) {
+                        a = cand[j].x;
+                        b = cand[j].y;
+                    }
+                ctl->n_lone = C.n_lone + 1;
+            }
+            if (C.tie == 1) ctl->n_tail = C.n_tail + 1;
+            if (a < 0) {
+                ctl->status = LOOP_ERROR;
+                return;
+            }
+            if (!C.sharded && !room()) {
+                to_host();
+                return;
+            }
         }
         ctl->tie = 0;
     }
@@ -1952,11 +2040,6 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
     ctl->w = W;
     ctl->next_id = c + 1;
     ctl->n_done = i + 1;
-    if (count) {   // (replacements == W exactly on one corpus)
-        count[a] -= W;
-        count[b] -= W;
-        count[c] = W;
-    }
     res->best = 0;
     res->n_cand = 0;
     res->n_heavy = 0;
@@ -2110,6 +2193,40 @@ __global__ void k_incr_invalidate(ColdTable ct, unsigned long long *__restrict__
     }
 }
 
+// Sharded maintained state, at the start of the next selection: the delta rows summed over the
+// ranks (the recount of every pair the last merge (a, b) -> c touched, which k_incr_invalidate
+// zeroed before the pass) into this rank's copy of the global tables, and the rows zeroed for the
+// next merge.  Each touched pair has exactly one slot (delta_slot), so a hot bin gets one add.
+__global__ void __launch_bounds__(256) k_apply_delta(unsigned long long *__restrict__ xchg,
+                                                     unsigned long long *__restrict__ hot,
+                                                     ColdTable ct, const LoopCtl *ctl) {
+    if (loop_off(ctl) || ctl->w < 0) return;   // (w < 0: no merge applied yet in this batch)
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    const uint32_t n = (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);   // other tokens <= c
+    unsigned long long *d = xchg + XCHG_HDR;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned long long v = d[i];
+        if (!v) continue;
+        d[i] = 0;
+        const uint32_t row = i % DELTA_ROWS;
+        const int32_t o = (int32_t)(i / DELTA_ROWS);
+        const int32_t m = row == 0 || row == 2 ? a : row == 1 || row == 3 ? b : c;
+        const bool left = row == 0 || row == 1 || row == 4;   // (m, o), else (o, m)
+        const int32_t x = left ? m : o, y = left ? o : m;
+        if (((uint32_t)x | (uint32_t)y) < (uint32_t)HOT) hot[hot_bin((uint32_t)x, (uint32_t)y)] += v;
+        else cold_add(ct, pair_key(x, y), v);
+    }
+}
+
+// bpe_set_global_counts: (key, count) entries of every shard, duplicates summed, into the cleared
+// cold table (holes, key EMPTY or count 0, skipped).
+__global__ void k_load_cold(ColdTable ct, const uint32_t *__restrict__ keys,
+                            const unsigned long long *__restrict__ counts, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (counts[i] && keys[i] != EMPTY) cold_add(ct, keys[i], counts[i]);
+}
+
 // MODE_INCR after the pass: sums the G slabs' rows (+ their spill, zeroed here) and adds each
 // nonzero count to its pair in the maintained tables.  A block owns 32 row dwords (64 counters):
 // its 8 lane groups each sum every 8th slab, eight loads in flight, then combine in LDS.
@@ -2117,7 +2234,8 @@ constexpr int RR_COLS = 32;
 __global__ void __launch_bounds__(256)
 k_reduce_rows(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ rspill,
               unsigned long long *__restrict__ hot, ColdTable ct, int32_t a, int32_t b, int32_t c,
-              const LoopCtl *ctl = nullptr) {
+              const LoopCtl *ctl = nullptr, unsigned long long *__restrict__ delta = nullptr,
+              const unsigned long long *__restrict__ rep = nullptr) {
     __shared__ uint32_t s_lo[8][RR_COLS], s_hi[8][RR_COLS];
     if (loop_off(ctl)) return;
     if (ctl) {
@@ -2125,6 +2243,8 @@ k_reduce_rows(const uint32_t *__restrict__ partials, int G, unsigned long long *
         b = ctl->b;
         c = ctl->c;
     }
+    // (sharded: the exchange header carries this shard's replacement count, summed with the rows)
+    if (delta && rep && blockIdx.x == 0 && threadIdx.x == 0) delta[0] = *rep;
     const int vl = incr_vlim(c);
     const int d0 = blockIdx.x * RR_COLS;   // first of the block's dwords (4 rows x INCR_RLIM / 2)
     const int row = d0 / (INCR_RLIM / 2);
@@ -2170,6 +2290,10 @@ k_reduce_rows(const uint32_t *__restrict__ partials, int G, unsigned long long *
         Sink k;
         k.hot = hot;
         k.ct = ct;
+        k.delta = delta;
+        k.ma = a;
+        k.mb = b;
+        k.mc = c;
         incr_global_add(k, x, y, n);
     }
 }
@@ -2304,9 +2428,12 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     int n = A.n_cand;
     int tail = 0;
     if (A.ctl) {
-        if (A.ctl->status != LOOP_RUN || !A.ctl->tie) return;
+        const int tie = A.ctl->tie;
+        if (A.ctl->status != LOOP_RUN || (tie != 1 && tie != 2)) return;
         n = (int)A.res->n_cand;
-        tail = A.ctl->tie == 1;
+        tail = tie == 1;
+        // (a sharded corpus's tail window lies on the last rank: the others find nothing there)
+        if (tail && A.ctl->sharded && !A.ctl->last_rank) return;
     }
     TieState ts;
     ts.n = min(n, MAX_CAND);
@@ -2412,15 +2539,24 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
 }
 
 // Sharded loop: this shard's last tie positions as corpus-wide ones (rank << 40 | position; 0:
-// none) for the all-reduce(MAX) that follows.  One thread per candidate slot.
+// none), and this rank's vote for the host path at [MAX_CAND], for the all-reduce(MAX) that
+// follows.  One thread per slot.
 constexpr int RANK_SHIFT = 40;
+constexpr int TIE_WORDS = 32;   // include/bpe.h BPE_TIE_WORDS
+static_assert(TIE_WORDS > MAX_CAND, "tie exchange: positions + vote");
 __global__ void k_tie_export(const LoopCtl *ctl, const Result *res, unsigned long long *tie_pos,
                              int rank) {
     const int j = threadIdx.x;
-    if (j >= MAX_CAND) return;
+    if (j >= TIE_WORDS) return;
+    const bool run = ctl->status == LOOP_RUN;
+    const int tie = ctl->tie;
     unsigned long long v = 0;
-    if (ctl->status == LOOP_RUN && ctl->tie == 2 && res->last[j])
-        v = ((unsigned long long)rank << RANK_SHIFT) | res->last[j];
+    if (j < MAX_CAND) {
+        if (run && (tie == 1 || tie == 2) && res->last[j])
+            v = ((unsigned long long)rank << RANK_SHIFT) | res->last[j];
+    } else if (j == MAX_CAND) {
+        v = run && ctl->vote ? 1 : 0;
+    }
     tie_pos[j] = v;
 }
 

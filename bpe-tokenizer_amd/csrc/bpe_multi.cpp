@@ -54,12 +54,17 @@ struct bpe_multi {
     std::vector<bpe_ctx *> sh;
     std::vector<hipStream_t> st;
     std::vector<unsigned long long *> d_table, d_tie;   // per shard, on its device
+    std::vector<unsigned long long *> d_xchg;            // per shard: the rank loop's exchange
     std::vector<uint32_t *> d_keys;                      // per shard: exact cold-pair lists
     std::vector<unsigned long long *> d_counts;
     int64_t cold_cap = 0;
-    unsigned long long *h_buf = nullptr, *h_sum = nullptr;   // pinned, BPE_TABLE_BINS each
+    unsigned long long *h_buf = nullptr, *h_sum = nullptr;   // pinned, BPE_XCHG_WORDS each
     std::vector<std::vector<int32_t>> staged;            // samples not yet on a device
     bool distributed = false;
+    // the maintained state (every shard holds the global tables, bpe_set_global_counts), and the
+    // host-protocol iterations in a row that needed exact cold counts (two: enter that state)
+    bool maintained = false;
+    int heavy_streak = 0;
     std::vector<ncclComm_t> comms;
     Rccl rccl;
 };
@@ -204,6 +209,7 @@ int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
     m->st.assign(n, nullptr);
     m->d_table.assign(n, nullptr);
     m->d_tie.assign(n, nullptr);
+    m->d_xchg.assign(n, nullptr);
     m->d_keys.assign(n, nullptr);
     m->d_counts.assign(n, nullptr);
     for (int r = 0; r < n; ++r) {
@@ -214,11 +220,12 @@ int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
         m->st[r] = (hipStream_t)s;
         if (hipSetDevice(m->dev[r]) != hipSuccess ||
             hipMalloc((void **)&m->d_table[r], BPE_TABLE_BINS * 8) != hipSuccess ||
-            hipMalloc((void **)&m->d_tie[r], BPE_MAX_CAND * 8) != hipSuccess)
+            hipMalloc((void **)&m->d_xchg[r], BPE_XCHG_WORDS * 8) != hipSuccess ||
+            hipMalloc((void **)&m->d_tie[r], BPE_TIE_WORDS * 8) != hipSuccess)
             return bail(bpe_fail(BPE_ERR_OOM, "bpe native: multi-device buffers"));
     }
-    if (hipHostMalloc((void **)&m->h_buf, BPE_TABLE_BINS * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&m->h_sum, BPE_TABLE_BINS * 8, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void **)&m->h_buf, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&m->h_sum, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_OOM, "bpe native: pinned host buffers"));
     if (reduce == BPE_REDUCE_RCCL && n > 1) {
         int rc = load_rccl(m->rccl);
@@ -241,7 +248,7 @@ int multi_destroy(bpe_multi *m) {
     for (int r = 0; r < (int)m->sh.size(); ++r) {
         (void)hipSetDevice(m->dev[r]);
         if (m->sh[r]) bpe_destroy(m->sh[r]);
-        void *ptrs[] = {m->d_table[r], m->d_tie[r], m->d_keys[r], m->d_counts[r]};
+        void *ptrs[] = {m->d_table[r], m->d_tie[r], m->d_xchg[r], m->d_keys[r], m->d_counts[r]};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
     }
@@ -263,19 +270,36 @@ int multi_set_token_len16(bpe_multi *m, int32_t id, int32_t len16) {
     return BPE_OK;
 }
 
+int check_vocab(bpe_multi *m, int32_t *n_tokens);
+
 int multi_num_tokens(bpe_multi *m, int32_t *n) { return bpe_num_tokens(m->sh[0], n); }
 
 int multi_add_sample(bpe_multi *m, const int32_t *ids, int64_t n) {
-    if (m->distributed) return bpe_add_sample(m->sh.back(), ids, n);   // (corpus order kept)
     for (int64_t i = 0; i < n; ++i)
         if (ids[i] < 0 || ids[i] >= BPE_MAX_VOCAB)
             return bpe_fail(BPE_ERR_ARG, "bpe native: token id out of range in sample");
+    // every shard knows every token before any shard sees it: a new id grows the vocabulary of
+    // all of them alike, so the next merge numbers its token the same on every shard
     int32_t mx = -1;
     for (int64_t i = 0; i < n; ++i) mx = std::max(mx, ids[i]);
     int32_t nt = 0;
     MTRY(bpe_num_tokens(m->sh[0], &nt));
     for (int32_t id = nt; id <= mx; ++id) MTRY(multi_set_token_len16(m, id, 1));
+    if (m->distributed) return bpe_add_sample(m->sh.back(), ids, n);   // (corpus order kept)
     m->staged.emplace_back(ids, ids + n);
+    return BPE_OK;
+}
+
+// The shards' vocabularies must agree (every new id is numbered by the vocabulary size).
+int check_vocab(bpe_multi *m, int32_t *n_tokens) {
+    int32_t n0 = 0;
+    MTRY(bpe_num_tokens(m->sh[0], &n0));
+    for (int r = 1; r < m->n; ++r) {
+        int32_t nr = 0;
+        MTRY(bpe_num_tokens(m->sh[r], &nr));
+        if (nr != n0) return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the vocabulary size");
+    }
+    if (n_tokens) *n_tokens = n0;
     return BPE_OK;
 }
 
@@ -315,6 +339,8 @@ int multi_add_latin1(bpe_multi *m, const uint8_t *bytes, int64_t n, int64_t samp
 int multi_clear_corpus(bpe_multi *m) {
     m->staged.clear();
     m->distributed = false;
+    m->maintained = false;
+    m->heavy_streak = 0;
     for (auto s : m->sh) MTRY(bpe_clear_corpus(s));
     return BPE_OK;
 }
@@ -422,9 +448,20 @@ int multi_read_samples(bpe_multi *m, const int64_t *idx, int64_t n, int32_t *ids
 // ---- the hot path -----------------------------------------------------------------------------------
 // findNextMerge over the shards (core.ts:247-326): the host protocol (sharded.py
 // exchange_and_select, in C++).
+int find_next_merge_host(bpe_multi *m, int64_t max_length, int64_t min_weight, int32_t *a,
+                         int32_t *b, int64_t *w, bool *heavy_out);
+
 int multi_find_next_merge(bpe_multi *m, int64_t max_length, int64_t min_weight, int32_t *a,
                           int32_t *b, int64_t *w) {
+    bool heavy = false;
+    return find_next_merge_host(m, max_length, min_weight, a, b, w, &heavy);
+}
+
+// The host protocol of one iteration; *heavy_out: some sketch bucket needed exact cold counts.
+int find_next_merge_host(bpe_multi *m, int64_t max_length, int64_t min_weight, int32_t *a,
+                         int32_t *b, int64_t *w, bool *heavy_out) {
     MTRY(distribute(m));
+    m->maintained = false;   // (the shards recount their own tables below)
     for (int r = 0; r < m->n; ++r) MTRY(bpe_export_counts(m->sh[r], (uint64_t *)m->d_table[r]));
     MTRY(all_reduce(m, m->d_table, BPE_TABLE_BINS, false));
     // exact counts of the cold pairs whose global sketch bucket could still win (every shard
@@ -443,6 +480,7 @@ int multi_find_next_merge(bpe_multi *m, int64_t max_length, int64_t min_weight, 
         if (rc < 0) return rc;
         if (nc < 0) continue;
         heavy = true;
+        *heavy_out = true;
         if (nc == 0) continue;
         std::vector<uint32_t> k(nc);
         std::vector<uint64_t> v(nc);
@@ -500,6 +538,7 @@ int multi_find_next_merge(bpe_multi *m, int64_t max_length, int64_t min_weight, 
 
 int multi_apply_merge(bpe_multi *m, int32_t a, int32_t b, int32_t c, int64_t *replaced) {
     MTRY(distribute(m));
+    m->maintained = false;
     int64_t tot = 0;
     for (auto s : m->sh) {
         int64_t r = 0;
@@ -513,6 +552,7 @@ int multi_apply_merge(bpe_multi *m, int32_t a, int32_t b, int32_t c, int64_t *re
 int multi_apply_merges(bpe_multi *m, const int32_t *abc, int64_t n, int64_t *replaced,
                        int count_after) {
     MTRY(distribute(m));
+    m->maintained = false;
     std::vector<int64_t> rep(std::max<int64_t>(n, 1));
     if (replaced) std::fill(replaced, replaced + n, 0);
     for (auto s : m->sh) {
@@ -523,13 +563,55 @@ int multi_apply_merges(bpe_multi *m, const int32_t *abc, int64_t n, int64_t *rep
     return BPE_OK;
 }
 
+// The maintained state over the shards: the global table (all-reduced) and every shard's exact
+// cold-pair list, gathered through the host, loaded into every shard (bpe_set_global_counts).
+int enter_maintained(bpe_multi *m) {
+    for (int r = 0; r < m->n; ++r) MTRY(bpe_export_counts(m->sh[r], (uint64_t *)m->d_table[r]));
+    MTRY(all_reduce(m, m->d_table, BPE_TABLE_BINS, false));
+    std::vector<int64_t> cnt(m->n, 0);
+    int64_t total = 0;
+    for (int r = 0; r < m->n; ++r) {
+        MTRY(bpe_cold_counts(m->sh[r], nullptr, nullptr, 0, &cnt[r]));   // (the pass; kept)
+        total += cnt[r];
+    }
+    MTRY(ensure_cold_bufs(m, std::max<int64_t>(total, 1)));
+    std::vector<uint32_t> keys(total);
+    std::vector<uint64_t> vals(total);
+    int64_t o = 0;
+    for (int r = 0; r < m->n; ++r) {
+        int64_t nr = 0;
+        MTRY(bpe_cold_counts(m->sh[r], m->d_keys[r], (uint64_t *)m->d_counts[r], m->cold_cap, &nr));
+        if (nr != cnt[r]) return bpe_fail(BPE_ERR_STATE, "bpe native: cold list changed size");
+        if (nr) {
+            MHIP(hipSetDevice(m->dev[r]));
+            MHIP(hipMemcpy(keys.data() + o, m->d_keys[r], nr * 4, hipMemcpyDeviceToHost));
+            MHIP(hipMemcpy(vals.data() + o, m->d_counts[r], nr * 8, hipMemcpyDeviceToHost));
+        }
+        o += nr;
+    }
+    for (int r = 0; r < m->n; ++r) {
+        if (total) {
+            MHIP(hipSetDevice(m->dev[r]));
+            MHIP(hipMemcpy(m->d_keys[r], keys.data(), total * 4, hipMemcpyHostToDevice));
+            MHIP(hipMemcpy(m->d_counts[r], vals.data(), total * 8, hipMemcpyHostToDevice));
+        }
+        MTRY(bpe_set_global_counts(m->sh[r], (const uint64_t *)m->d_table[r], m->d_keys[r],
+                                   (const uint64_t *)m->d_counts[r], total));
+    }
+    m->maintained = true;
+    m->heavy_streak = 0;
+    return BPE_OK;
+}
+
 // mergeUntil (core.ts:365-383) over the shards: batches of the device-resident rank loop, the
-// host protocol for the iterations it hands back.
+// host protocol for the iterations it hands back.  Two host iterations in a row that needed exact
+// cold counts (the cold pairs outgrow the sketch: skewed corpora, large vocabularies) move the
+// shards to the maintained state, where the batches keep the global tables with delta rows.
 int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                       int64_t max_iterations, int64_t *out_abw, int64_t cap, int64_t *n_merges) {
     MTRY(distribute(m));
     int64_t n = 0, batch = BPE_LOOP_BATCH;
-    std::vector<std::vector<int64_t>> abw(m->n, std::vector<int64_t>(3 * BPE_LOOP_BATCH));
+    std::vector<std::vector<int64_t>> log(m->n, std::vector<int64_t>(4 * BPE_LOOP_BATCH));
     auto put = [&](int32_t a, int32_t b, int64_t w) {
         if (n < cap) {
             out_abw[3 * n] = a;
@@ -540,18 +622,26 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
     };
     while (!max_iterations || n < max_iterations) {
         int32_t nt = 0;
-        MTRY(bpe_num_tokens(m->sh[0], &nt));
+        MTRY(check_vocab(m, &nt));
         int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)nt);
         if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
         int status = 2;
+        bool batch_maintained = false;
         if (want > 0) {
-            for (int r = 0; r < m->n; ++r)
-                MTRY(bpe_rank_loop_begin(m->sh[r], max_length, min_weight,
-                                         (uint64_t *)m->d_table[r], (uint64_t *)m->d_tie[r], r));
+            if (!m->maintained && m->heavy_streak >= 2) MTRY(enter_maintained(m));
+            batch_maintained = m->maintained;
+            int64_t nw = -1;
+            for (int r = 0; r < m->n; ++r) {
+                int64_t w_r = 0;
+                MTRY(bpe_rank_loop_begin(m->sh[r], max_length, min_weight, (uint64_t *)m->d_xchg[r],
+                                         (uint64_t *)m->d_tie[r], r, m->n, &w_r));
+                if (nw >= 0 && w_r != nw) return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the exchange");
+                nw = w_r;
+            }
             for (int64_t i = 0; i < want; ++i) {
-                MTRY(all_reduce(m, m->d_table, BPE_TABLE_BINS, false));
+                MTRY(all_reduce(m, m->d_xchg, (size_t)nw, false));
                 for (auto s : m->sh) MTRY(bpe_rank_loop_select(s));
-                MTRY(all_reduce(m, m->d_tie, BPE_MAX_CAND, true));
+                MTRY(all_reduce(m, m->d_tie, BPE_TIE_WORDS, true));
                 for (auto s : m->sh) MTRY(bpe_rank_loop_decide(s));
                 for (auto s : m->sh) MTRY(bpe_rank_loop_count(s));
             }
@@ -559,14 +649,23 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
             for (int r = 0; r < m->n; ++r) {
                 int64_t k = 0;
                 int st = 0;
-                MTRY(bpe_rank_loop_end(m->sh[r], abw[r].data(), BPE_LOOP_BATCH, &k, &st));
-                if ((nd >= 0 && (k != nd || st != status)) ||
-                    (r > 0 && !std::equal(abw[r].begin(), abw[r].begin() + 3 * k, abw[0].begin())))
-                    return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the merges");
+                MTRY(bpe_rank_loop_end(m->sh[r], log[r].data(), BPE_LOOP_BATCH, &k, &st));
+                bool same = nd < 0 || (k == nd && st == status);
+                for (int64_t i = 0; same && r > 0 && i < k; ++i)
+                    same = std::equal(log[r].begin() + 4 * i, log[r].begin() + 4 * i + 3,
+                                      log[0].begin() + 4 * i);
+                if (!same) return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the merges");
                 nd = k;
                 status = st;
             }
-            for (int64_t i = 0; i < nd; ++i) put((int32_t)abw[0][3 * i], (int32_t)abw[0][3 * i + 1], abw[0][3 * i + 2]);
+            for (int64_t i = 0; i < nd; ++i) {
+                // every merge: the shards' replacement counts sum to W (core.ts:356-359)
+                int64_t tot = 0;
+                for (int r = 0; r < m->n; ++r) tot += log[r][4 * i + 3];
+                if (tot != log[0][4 * i + 2]) return bpe_fail(BPE_ERR_STATE, "bpe native: replacement count != W");
+                put((int32_t)log[0][4 * i], (int32_t)log[0][4 * i + 1], log[0][4 * i + 2]);
+            }
+            if (status != 0) m->maintained = false;   // (the shards left the global state)
             if (status == 1) break;                                        // no pair qualifies
             if (status == 0) {
                 batch = std::min<int64_t>(BPE_LOOP_BATCH, 2 * batch);
@@ -575,13 +674,17 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
             batch = std::max<int64_t>(1, std::min<int64_t>(BPE_LOOP_BATCH, 2 * nd));
             if (max_iterations && n >= max_iterations) break;
         }
-        // the host protocol for this iteration (or the vocabulary limit, reported by the apply)
+        // the host protocol for this iteration (or the vocabulary limit, reported by the apply).
+        // After a maintained batch hands over, one more iteration with exact counts re-enters it.
+        const bool was_maintained = batch_maintained && status == 2;
         int32_t a, b;
         int64_t w;
-        int rc = multi_find_next_merge(m, max_length, min_weight, &a, &b, &w);
+        bool heavy = false;
+        int rc = find_next_merge_host(m, max_length, min_weight, &a, &b, &w, &heavy);
         if (rc == BPE_NO_MERGE) break;
         if (rc) return rc;
-        MTRY(bpe_num_tokens(m->sh[0], &nt));
+        m->heavy_streak = heavy ? std::max(m->heavy_streak + 1, was_maintained ? 2 : 1) : 0;
+        MTRY(check_vocab(m, &nt));
         int64_t rep = 0;
         MTRY(multi_apply_merge(m, a, b, nt, &rep));
         if (rep != w) return bpe_fail(BPE_ERR_STATE, "bpe native: replacement count != W");

@@ -261,9 +261,12 @@ __device__ __forceinline__ void pix_bmax_dirty(const PixTable &t, const PixBufs 
 }
 
 __global__ void __launch_bounds__(256) k_pix_sbmax(PixTable t, PixBufs B, PixCtl *ctl, int all) {
-    const uint32_t ns = all ? t.nsuper : min(ctl->n_dsuper, t.nsuper);
-    if (!all && ctl->status != PIX_RUN) return;
     __shared__ unsigned long long red[4];
+    __shared__ uint32_t s_ns;
+    if (threadIdx.x == 0)   // (read once and broadcast: the loop around the barriers is uniform)
+        s_ns = all ? t.nsuper : (ctl->status != PIX_RUN ? 0u : min(ctl->n_dsuper, t.nsuper));
+    __syncthreads();
+    const uint32_t ns = s_ns;
     for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
         const uint32_t sb = all ? i : B.dsuper[i];
         const uint32_t blk = sb * PIX_SB + threadIdx.x;
@@ -294,14 +297,24 @@ __global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long
 __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixCtl *ctl) {
     __shared__ unsigned long long red[16];
     __shared__ uint32_t lst[64];
-    __shared__ uint32_t n_lst, n_blk;
-    __shared__ uint32_t blks[64];
+    __shared__ uint32_t n_lst, n_blk, n_cs;
+    __shared__ uint32_t blks[64], cs[MAX_CAND];
+    __shared__ uint32_t s_go, s_nd;
+    __shared__ long long s_mw;
     const int tid = threadIdx.x;
-    if (ctl->status != PIX_RUN) return;
+    // (every control value a branch below depends on is read by one thread and broadcast through
+    // LDS, so the whole block takes the same path: each barrier is reached by all of its threads)
+    if (tid == 0) {
+        s_go = ctl->status != PIX_RUN ? 0u : ctl->n_done >= ctl->n_want ? 1u : 2u;
+        s_nd = min(ctl->n_dsuper, t.nsuper);
+        s_mw = ctl->min_weight;
+    }
+    __syncthreads();
+    if (s_go == 0) return;
     {
         // the superblocks the previous merge may have lowered (one wave each)
         const int lane = tid & 63, wv = tid >> 6;
-        const uint32_t nd = min(ctl->n_dsuper, t.nsuper);
+        const uint32_t nd = s_nd;
         for (uint32_t q = wv; q < nd; q += 16) {
             const uint32_t sb = B.dsuper[q];
             unsigned long long m = 0;
@@ -316,8 +329,11 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
                 t.sbdirty[sb] = 0;
             }
         }
-        __threadfence_block();
+        // (their new maxima are read below by other waves: made visible at agent scope, L1
+        // invalidated after the barrier)
+        __threadfence();
         __syncthreads();
+        __threadfence();
     }
     if (tid == 0) {
         // counters of the previous merge (nothing else reads them now)
@@ -327,9 +343,9 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         ctl->tie_done = 0;
         ctl->n_check = 0;
         for (int q = 0; q < MAX_CAND; ++q) ctl->last[q] = 0;
-        n_lst = n_blk = 0;
+        n_lst = n_blk = n_cs = 0;
     }
-    if (ctl->n_done >= ctl->n_want) {
+    if (s_go == 1) {
         if (tid == 0) ctl->status = PIX_PAUSE;
         return;
     }
@@ -343,7 +359,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
 #pragma unroll
     for (int i = 0; i < 16; ++i) best = max(best, red[i]);
     const long long W = (long long)(best >> 17);
-    if (best == 0 || W < ctl->min_weight) {                           // core.ts:312-313
+    if (best == 0 || W < s_mw) {                                      // core.ts:312-313
         if (tid == 0) ctl->status = PIX_DONE;
         return;
     }
@@ -363,19 +379,24 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         }
     }
     __syncthreads();
+    // the candidates gather in LDS; thread 0 publishes them (a global counter that other waves of
+    // this block add to while thread 0 has just stored it, then reads back, is not ordered by the
+    // barrier: a candidate could be lost, and a tie with it)
     const uint32_t nbk = min(n_blk, 64u);
     for (uint32_t q = 0; q < nbk; ++q) {
         if (tid < PIX_B) {
             const uint32_t s = blks[q] * PIX_B + tid;
             if (pix_sel(t, s) == best) {
-                const uint32_t k = atomicAdd(&ctl->n_cand, 1u);
-                if (k < MAX_CAND) ctl->cand_slot[k] = s;
+                const uint32_t k = atomicAdd(&n_cs, 1u);
+                if (k < MAX_CAND) cs[k] = s;
             }
         }
     }
     __syncthreads();
     if (tid == 0) {
-        const uint32_t nc = ctl->n_cand;
+        const uint32_t nc = n_cs;
+        ctl->n_cand = nc;
+        for (uint32_t j = 0; j < min(nc, (uint32_t)MAX_CAND); ++j) ctl->cand_slot[j] = cs[j];
         if (n_lst > 64 || n_blk > 64 || nc > (uint32_t)MAX_CAND || nc == 0) {
             ctl->status = PIX_HOST;
             ctl->err = nc == 0 ? 10 : 4;
@@ -411,28 +432,36 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
 // offset of its run) and decides.
 constexpr int PIX_TIE_SPLIT = 16;
 __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
-    if (ctl->status != PIX_RUN || !ctl->tie) return;
-    const uint32_t j = blockIdx.x / PIX_TIE_SPLIT, part = blockIdx.x % PIX_TIE_SPLIT;
-    const uint32_t nc = ctl->n_cand;
     __shared__ unsigned long long red[4];
     __shared__ bool last_block;
+    __shared__ uint32_t s_run, s_nc;
+    // (the control block is read by one thread and broadcast, so every branch around a barrier
+    // below is uniform by construction, whatever the compiler can prove)
+    if (threadIdx.x == 0) {
+        s_run = ctl->status == PIX_RUN && ctl->tie;
+        s_nc = ctl->n_cand;
+    }
+    __syncthreads();
+    if (!s_run) return;
+    const uint32_t j = blockIdx.x / PIX_TIE_SPLIT, part = blockIdx.x % PIX_TIE_SPLIT;
+    const uint32_t nc = s_nc;
+    unsigned long long m = 0;
     if (j < nc) {
         const uint32_t s = ctl->cand_slot[j];
         const int32_t u = (int32_t)(t.keys[s] >> 16), v = (int32_t)(t.keys[s] & 0xFFFF);
         const uint32_t off = t.off[s], len = t.len[s];
-        unsigned long long m = 0;
         for (uint32_t i = part * 256 + threadIdx.x; i < len; i += PIX_TIE_SPLIT * 256) {
             const uint32_t p = B.pool[off + i];
             if (C.tok[p] == u && pix_tok_is(C, C.nxt[p], v)) m = max(m, (unsigned long long)p + 1);
         }
+    }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            m = max(max(red[0], red[1]), max(red[2], red[3]));
-            if (m) atomicMax(&ctl->last[j], m);
-        }
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0 && j < nc) {
+        m = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (m) atomicMax(&ctl->last[j], m);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -576,10 +605,16 @@ __device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uin
 // odd), so (l, a) -> (l, c) on the left, (a, r) -> (c, r) on the right when L is even, (c, a)
 // when L is odd, and floor(m/2) pairs (c, c) for the m c's.
 __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
-    if (ctl->status != PIX_RUN) return;
+    __shared__ uint32_t s_run, s_len;
+    if (threadIdx.x == 0) {   // (read once and broadcast: the loop around the barriers is uniform)
+        s_run = ctl->status == PIX_RUN;
+        s_len = s_run ? t.len[ctl->pair_slot] : 0u;
+    }
+    __syncthreads();
+    if (!s_run) return;
     const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
     const uint32_t s = ctl->pair_slot;
-    const uint32_t off = t.off[s], len = t.len[s];
+    const uint32_t off = t.off[s], len = s_len;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // every (a, b) is merged (no count change below touches the pair itself)
         t.cnt[s] = 0;
@@ -676,10 +711,14 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
 // Segments for this merge's new pairs, from their owner entries (one pool atomic per block), and
 // the new pairs' maxima: their counts are final now.
 __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
-    if (ctl->status != PIX_RUN) return;
     __shared__ unsigned long long wsum[4], wown[4], base_s;
+    __shared__ uint32_t s_ne;
+    if (threadIdx.x == 0)   // (read once and broadcast: the loop around the barriers is uniform)
+        s_ne = ctl->status != PIX_RUN ? 0u
+                                      : min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
+    __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t ne = min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
+    const uint32_t ne = s_ne;
     for (uint32_t i0 = blockIdx.x * 256; i0 < ne; i0 += gridDim.x * 256) {
         const uint32_t i = i0 + threadIdx.x;
         uint2 e = make_uint2(PIX_NONE, 0);

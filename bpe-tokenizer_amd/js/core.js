@@ -93,13 +93,17 @@ class BPETokenizer {
     if (!this._engine) {
       let n = loadNative()
       let devices = null
-      if (process.env.BPE_DEVICES) devices = process.env.BPE_DEVICES.split(',').map(Number)
-      else if (+process.env.BPE_NUM_GPUS > 1) {
+      if (process.env.BPE_DEVICES) {
+        devices = process.env.BPE_DEVICES.split(',').map(s => Number(s.trim()))
+        if (devices.some(d => !Number.isInteger(d) || d < 0))
+          throw new Error('bpe native: BPE_DEVICES must list device indices, e.g. "0,1,2,3"')
+      } else if (+process.env.BPE_NUM_GPUS > 1) {
         devices = []
         for (let i = 0; i < +process.env.BPE_NUM_GPUS; i++) devices.push(i)
       }
       let reduce = process.env.BPE_REDUCE === 'host' ? 1 : 0
-      this._engine = devices && devices.length > 1 ? n.createEngine(0, Int32Array.from(devices), reduce) : n.createEngine(0)
+      if (devices && devices.length > 1) this._engine = n.createEngine(0, Int32Array.from(devices), reduce)
+      else this._engine = n.createEngine(devices ? devices[0] : 0)
       this._registered = 0
     }
     this.flushMerges()

@@ -383,7 +383,8 @@ class BPETokenizerDB {
   }
 
   dropEngine() {
-    if (this._engine) loadNative().clearCorpus(this._engine)
+    // (the context and its device memory go now, not when the garbage collector finds the handle)
+    if (this._engine) loadNative().destroyEngine(this._engine)
     this._engine = null
     this._rows = []
     this._lens = []

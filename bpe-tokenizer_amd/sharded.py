@@ -19,6 +19,10 @@ bpe_rank_loop_*): per iteration the table all-reduce(SUM), the selection kernels
 all-reduce(MAX), the decision and the fused apply+count pass are enqueued in order on the
 engine's HIP stream, with no host sync until the end of a batch of BPE_LOOP_BATCH iterations.
 Only an iteration with heavy sketch buckets or too many tied pairs takes the host protocol above.
+When two host iterations in a row needed exact cold counts (skewed corpora, large vocabularies),
+the ranks move to the maintained state: every rank holds the global hot and cold tables (the
+all-reduced table + every rank's exact cold-pair list, all-gathered), and each iteration exchanges
+only the delta rows of the pairs the merge touched (bpe_set_global_counts, include/bpe.h).
 
 The protocol only needs a `shard` object with export()/select()/tie_positions()/apply(); GpuShard
 wraps libbpe on a HIP device, and tests/test_sharded_gloo.py drives the same protocol on CPU
@@ -100,9 +104,10 @@ class GpuShard:
         return self.engine.apply_merge(a, b, c, sync=False)
 
 
-def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
+def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0, info=None):
     """The per-iteration collective protocol.  Returns (a, b, W) or None, identical on every rank.
-    Collectives run on the tables' device (RCCL); with the gloo backend on host copies."""
+    Collectives run on the tables' device (RCCL); with the gloo backend on host copies.
+    info (a dict): receives 'heavy', whether exact cold counts were needed."""
     import torch
     table = shard.export()
     dev = torch.device('cpu') if dist.get_backend() == 'gloo' else table.device
@@ -111,6 +116,8 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0):
     dist.all_reduce(table)
     gtable = table.to(sdev)
     heavy = shard.heavy(gtable, max_length)                  # identical decision on every rank
+    if info is not None:
+        info['heavy'] = heavy is not None
     m = 0
     if heavy is not None:
         keys, counts = heavy
@@ -166,7 +173,11 @@ class ShardedTrainer:
         self.n_tokens = n_tokens          # token_table.length (next new id, core.ts:315)
         self.live = live_global           # live corpus tokens over all ranks
         self.merges = []
-        self._rl = None                   # rank loop buffers (table, tie, stream)
+        self._rl = None                   # rank loop buffers (exchange, tie, stream)
+        # the maintained state (every rank holds the global tables: bpe_set_global_counts), and the
+        # host iterations in a row that needed exact cold counts (two: enter that state)
+        self._maintained = False
+        self._heavy_streak = 0
 
     @classmethod
     def synthetic(cls, device, rank, world, bytes_per_rank, sample_bytes, seed, alphabet, base,
@@ -225,18 +236,8 @@ class ShardedTrainer:
             return ms
         return self.run_rank_loop(n, max_length, min_weight)
 
-    def run_rank_loop(self, n, max_length=0, min_weight=0):
-        """n iterations across the ranks with the exchange on the device (bpe_rank_loop_*): no
-        host sync inside a batch of LOOP_BATCH iterations.  Returns the merges [(a, b, W)]."""
-        import torch
+    def _collectives(self):
         dist = self.dist
-        eng = self.engine
-        if self._rl is None:
-            dev = self.shard.device
-            self._rl = (torch.zeros(TABLE_BINS, dtype=torch.int64, device=dev),
-                        torch.zeros(MAX_CAND, dtype=torch.int64, device=dev),
-                        torch.cuda.ExternalStream(eng.stream(), device=dev))
-        table, tie, stream = self._rl
         gloo = dist.get_backend() == 'gloo'
 
         def all_reduce(t, op):
@@ -246,39 +247,114 @@ class ShardedTrainer:
                 t.copy_(h)
             else:              # RCCL, ordered after the stream's kernels by events
                 dist.all_reduce(t, op=op)
+        return gloo, all_reduce
 
+    def enter_maintained(self):
+        """The maintained state over the ranks (skewed corpora, large vocabularies): the global
+        table, and every rank's exact cold-pair list all-gathered, become every rank's global
+        tables (bpe_cold_counts / bpe_set_global_counts); the rank loop then keeps them with
+        delta rows instead of exchanging whole tables."""
+        import torch
+        dist, eng = self.dist, self.engine
+        gloo, all_reduce = self._collectives()
+        dev = self.shard.device
+        table = self.shard.export().clone()
+        all_reduce(table, dist.ReduceOp.SUM)
+        n = eng.cold_counts(None, None, 0)                     # (the pass; kept for the export)
+        cap = max(1, n)
+        keys = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        counts = torch.zeros(cap, dtype=torch.int64, device=dev)
+        eng.cold_counts(keys.data_ptr(), counts.data_ptr(), cap)
+        cdev = torch.device('cpu') if gloo else dev
+        size = torch.tensor([n], dtype=torch.int64, device=cdev)
+        sizes = [torch.zeros_like(size) for _ in range(self.world)]
+        dist.all_gather(sizes, size)
+        sizes = [int(x.item()) for x in sizes]
+        m = max(1, max(sizes))
+        kp = torch.full((m,), -1, dtype=torch.int32, device=cdev)
+        cp = torch.zeros(m, dtype=torch.int64, device=cdev)
+        kp[:n] = keys[:n].to(cdev)
+        cp[:n] = counts[:n].to(cdev)
+        gk = [torch.empty_like(kp) for _ in range(self.world)]
+        gc = [torch.empty_like(cp) for _ in range(self.world)]
+        dist.all_gather(gk, kp)
+        dist.all_gather(gc, cp)
+        all_k = torch.cat([g[:z] for g, z in zip(gk, sizes)] + [kp[:0]]).to(dev).contiguous()
+        all_c = torch.cat([g[:z] for g, z in zip(gc, sizes)] + [cp[:0]]).to(dev).contiguous()
+        total = all_k.numel()
+        eng.set_global_counts(table.data_ptr(), all_k.data_ptr() if total else None,
+                              all_c.data_ptr() if total else None, total)
+        torch.cuda.synchronize(dev)
+        self._maintained = True
+        self._heavy_streak = 0
+
+    def run_rank_loop(self, n, max_length=0, min_weight=0):
+        """n iterations across the ranks with the exchange on the device (bpe_rank_loop_*): no
+        host sync inside a batch of LOOP_BATCH iterations.  Returns the merges [(a, b, W)]."""
+        import torch
+        dist = self.dist
+        eng = self.engine
+        if self._rl is None:
+            dev = self.shard.device
+            self._rl = (torch.zeros(pkg.XCHG_WORDS, dtype=torch.int64, device=dev),
+                        torch.zeros(pkg.TIE_WORDS, dtype=torch.int64, device=dev),
+                        torch.cuda.ExternalStream(eng.stream(), device=dev))
+        xchg, tie, stream = self._rl
+        gloo, all_reduce = self._collectives()
         ms = []
         batch = LOOP_BATCH      # (as bpe_merge_until: about twice what an early-ended batch did)
         while len(ms) < n:
             k = min(batch, n - len(ms))
+            if not self._maintained and self._heavy_streak >= 2:
+                self.enter_maintained()
+            batch_maintained = self._maintained
             with torch.cuda.stream(stream):
-                eng.rank_loop_begin(max_length, min_weight, table.data_ptr(), tie.data_ptr(),
-                                    self.rank)
+                nw = eng.rank_loop_begin(max_length, min_weight, xchg.data_ptr(), tie.data_ptr(),
+                                         self.rank, self.world)
+                view = xchg[:nw]
                 for _ in range(k):
-                    all_reduce(table, dist.ReduceOp.SUM)
+                    all_reduce(view, dist.ReduceOp.SUM)
                     eng.rank_loop_select()
                     all_reduce(tie, dist.ReduceOp.MAX)
                     eng.rank_loop_decide()
                     eng.rank_loop_count()
-                got, status = eng.rank_loop_end()
+                got, reps, status = eng.rank_loop_end()
+            if got:
+                # every merge: the ranks' replacement counts sum to W (core.ts:356-359)
+                r = torch.tensor(reps, dtype=torch.int64,
+                                 device=torch.device('cpu') if gloo else self.shard.device)
+                dist.all_reduce(r)
+                if [int(v) for v in r.cpu().tolist()] != [m[2] for m in got]:
+                    raise RuntimeError('bpe sharded: replacement counts do not sum to W')
             for m in got:
                 self.n_tokens += 1
                 self.live -= m[2]
             self.merges += got
             ms += got
+            if status != 0:
+                self._maintained = False      # (the engines left the global state)
             if status == 1:
                 break
             batch = min(LOOP_BATCH, 2 * batch) if status == 0 else max(1, 2 * len(got))
             if status == 2 and len(ms) < n:
-                m = self.step(max_length, min_weight)     # the host protocol for this iteration
+                info = {}
+                m = self.step(max_length, min_weight, info)     # the host protocol for this iteration
+                heavy = info.get('heavy', False)
+                self._heavy_streak = (max(self._heavy_streak + 1, 2 if batch_maintained else 1)
+                                      if heavy else 0)
                 if m is None:
                     break
                 ms.append(m)
         return ms
 
-    def step(self, max_length=0, min_weight=0):
+    def step(self, max_length=0, min_weight=0, info=None):
         """One findNextMerge + applyMerge on every rank; returns (a, b, W) or None."""
-        m = self.find_next_merge(max_length, min_weight)
+        self._maintained = False
+        if self.world == 1:
+            m = self.engine.find_next_merge(max_length, min_weight)
+        else:
+            m = exchange_and_select(self.shard, self.dist, self.rank, self.world, max_length,
+                                    min_weight, info)
         if m is None:
             return None
         a, b, w = m

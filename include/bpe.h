@@ -183,28 +183,57 @@ int bpe_select_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *cold_
 int bpe_tie_positions(bpe_ctx *ctx, const int32_t *cand, int64_t n, uint64_t *last);
 
 /* ---- the device-resident loop on one rank of a sharded corpus ---------------------------------
- * mergeUntil (core.ts:365-383) over shards with no host sync per iteration.  `table`
- * (BPE_TABLE_BINS u64) and `tie` (BPE_MAX_CAND u64) are DEVICE buffers the caller all-reduces IN
+ * mergeUntil (core.ts:365-383) over shards with no host sync per iteration.  `xchg`
+ * (BPE_XCHG_WORDS u64) and `tie` (BPE_TIE_WORDS u64) are DEVICE buffers the caller all-reduces IN
  * ORDER on this context's stream (bpe_get_stream; e.g. RCCL on that stream).  Per iteration:
- *   all-reduce(SUM, table); bpe_rank_loop_select; all-reduce(MAX, tie); bpe_rank_loop_decide;
- *   bpe_rank_loop_count
+ *   all-reduce(SUM, xchg[0 .. *xchg_words)); bpe_rank_loop_select;
+ *   all-reduce(MAX, tie[0 .. BPE_TIE_WORDS)); bpe_rank_loop_decide; bpe_rank_loop_count
  * at most BPE_LOOP_BATCH times between bpe_rank_loop_begin and bpe_rank_loop_end.  Every rank takes
  * the same decisions from the same global tables, so all ranks run the same collectives; an
  * iteration after the batch has ended is a no-op (its collectives still run).
- * bpe_rank_loop_begin writes this shard's table into `table`; `rank` orders the tie positions
- * (rank r's occurrences come after rank r-1's, rule R3).  bpe_rank_loop_end syncs and writes the
- * batch's merges as (a, b, W) triples into host out_abw (capacity cap triples), *status:
+ * The exchange holds a header (BPE_XCHG_HDR words; word 0: this shard's replacement count of the
+ * merge just applied, so that the sum checked against W covers every shard) and either
+ *   - this shard's pair table (BPE_TABLE_BINS words), summed into the global table, or
+ *   - after bpe_set_global_counts (the maintained state: every rank holds the GLOBAL hot and cold
+ *     tables and keeps them merge by merge), BPE_DELTA_ROWS delta rows per token id: this shard's
+ *     recount of every pair the merge (a, b) -> c touched, at HDR + 6 * other + row, rows
+ *     (a, .) (b, .) (., a) (., b) (c, .) (., c) in this order of precedence.
+ * tie: the tied candidates' last positions (rank << 40 | position, rule R3: rank r's occurrences
+ * come after rank r-1's) in words 0..15, and word 16 this rank's vote for the host path (facts of
+ * its own copy of the maintained tables: fill, dead claims, room).  A tie between pairs X Y is
+ * decided from the corpus tail, which only the last rank (world - 1) scans.
+ * bpe_rank_loop_begin writes this shard's part of the first exchange and *xchg_words (the words to
+ * all-reduce per iteration of this batch: the same on every rank).  bpe_rank_loop_end syncs and
+ * writes the batch's merges as (a, b, W, this shard's replacement count) quadruples into host
+ * out_abwr (capacity cap quadruples; sum the counts over the shards: == W), *status:
  * 0 = every enqueued iteration merged, 1 = no pair qualifies (stop), 2 = the next iteration needs
- * the host protocol (heavy sketch buckets or more than BPE_MAX_CAND tied pairs: export / heavy /
- * select / tie_positions above). */
+ * the host protocol (heavy sketch buckets, more than BPE_MAX_CAND tied pairs, a vote: export /
+ * heavy / select / tie_positions above).  A batch of the maintained state that ran to its end
+ * leaves its last merge's delta rows in xchg for the next batch's first exchange: pass the same
+ * buffer again. */
 #define BPE_MAX_CAND 16
 #define BPE_LOOP_BATCH 64
-int bpe_rank_loop_begin(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, uint64_t *table,
-                        uint64_t *tie, int rank);
+#define BPE_XCHG_HDR 8
+#define BPE_DELTA_ROWS 6
+#define BPE_XCHG_WORDS (BPE_XCHG_HDR + BPE_DELTA_ROWS * BPE_MAX_VOCAB)
+#define BPE_TIE_WORDS 32
+int bpe_rank_loop_begin(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, uint64_t *xchg,
+                        uint64_t *tie, int rank, int world, int64_t *xchg_words);
 int bpe_rank_loop_select(bpe_ctx *ctx);
 int bpe_rank_loop_decide(bpe_ctx *ctx);
 int bpe_rank_loop_count(bpe_ctx *ctx);
-int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abw, int64_t cap, int64_t *n_merges, int *status);
+int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abwr, int64_t cap, int64_t *n_merges, int *status);
+
+/* The maintained state of a sharded corpus (skewed corpora, large vocabularies: the cold pairs
+ * outgrow the sketch).  Every rank: bpe_cold_counts (its exact count of every pair with an id >=
+ * 256, one streaming pass; *n > cap: nothing written, call again with room, no second pass), then
+ * the lists of ALL ranks gathered (e.g. all-gather) and bpe_set_global_counts with the global table
+ * (all-reduced bpe_export_counts) and the gathered lists (device pointers; duplicate keys summed).
+ * The next rank loop batches keep those global tables up to date with delta rows (above); any
+ * per-shard entry point (find/apply/export/...) drops the state. */
+int bpe_cold_counts(bpe_ctx *ctx, uint32_t *keys, uint64_t *counts, int64_t cap, int64_t *n);
+int bpe_set_global_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *keys,
+                          const uint64_t *counts, int64_t n);
 
 /* ---- modes -------------------------------------------------------------------------------------
  * BPE_MODE_STREAM (default): every merge is one fused streaming pass over the corpus (apply the

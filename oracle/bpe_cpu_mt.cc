@@ -201,11 +201,37 @@ extern "C" {
 
 /* A corpus (flat ids + n_samples + 1 offsets), the UTF-16 length of each of n_tokens tokens, room
  * for `extra` more tokens, `threads` OpenMP threads (<= 0: all). */
+cpu_bpe *cpu_setup(cpu_bpe *c, const int64_t *off, int64_t n_samples, const int32_t *len16,
+                   int32_t n_tokens, int64_t extra, int threads);
+
 cpu_bpe *cpu_create(const int32_t *ids, const int64_t *off, int64_t n_samples, const int32_t *len16,
                     int32_t n_tokens, int64_t extra, int threads) {
     cpu_bpe *c = new cpu_bpe();
+    c->ids.assign(ids, ids + off[n_samples]);
+    return cpu_setup(c, off, n_samples, len16, n_tokens, extra, threads);
+}
+
+/* The same from latin1 bytes (byte b -> token map256[b]) cut into samples of sample_bytes (the
+ * last one shorter), without a host copy of the int32 ids: the config-5 corpus (16 GiB of text)
+ * is 64 GiB of ids.  Every token has UTF-16 length 1. */
+cpu_bpe *cpu_create_latin1(const uint8_t *bytes, int64_t n, int64_t sample_bytes,
+                           const int32_t *map256, int32_t n_tokens, int64_t extra, int threads) {
+    cpu_bpe *c = new cpu_bpe();
+    c->ids.resize(n);
+    int32_t *ids = c->ids.data();
+#pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : omp_get_max_threads())
+    for (int64_t i = 0; i < n; ++i) ids[i] = map256[bytes[i]];
+    if (sample_bytes <= 0 || sample_bytes > n) sample_bytes = n > 0 ? n : 1;
+    const int64_t n_samples = (n + sample_bytes - 1) / sample_bytes;
+    std::vector<int64_t> off(n_samples + 1);
+    for (int64_t k = 0; k <= n_samples; ++k) off[k] = std::min(n, k * sample_bytes);
+    std::vector<int32_t> len16(std::max<int32_t>(n_tokens, 1), 1);
+    return cpu_setup(c, off.data(), n_samples, len16.data(), n_tokens, extra, threads);
+}
+
+cpu_bpe *cpu_setup(cpu_bpe *c, const int64_t *off, int64_t n_samples, const int32_t *len16,
+                   int32_t n_tokens, int64_t extra, int threads) {
     const int64_t total = off[n_samples];
-    c->ids.assign(ids, ids + total);
     c->begin.resize(n_samples);
     c->len.resize(n_samples);
     for (int64_t s = 0; s < n_samples; ++s) {

@@ -189,6 +189,9 @@ def lib_mt():
         L.cpu_create.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int32, ctypes.c_int64,
                                  ctypes.c_int]
         L.cpu_create.restype = vp
+        L.cpu_create_latin1.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, i32p, ctypes.c_int32,
+                                        ctypes.c_int64, ctypes.c_int]
+        L.cpu_create_latin1.restype = vp
         L.cpu_destroy.argtypes = [vp]
         L.cpu_destroy.restype = None
         L.cpu_live.argtypes = [vp]
@@ -224,6 +227,19 @@ class CpuMT:
         self._h = lib_mt().cpu_create(_p(ids, ctypes.c_int32), _p(off, ctypes.c_int64),
                                       self.n_samples, _p(l16, ctypes.c_int32), n_tokens, extra,
                                       threads)
+
+    @classmethod
+    def from_latin1(cls, data, sample_bytes, char_to_id, n_tokens, threads=0, extra=1 << 16):
+        """The corpus from latin1 bytes (byte b -> char_to_id[b]) in samples of sample_bytes,
+        mapped natively (no host int32 copy: bpe_cpu_mt.cc cpu_create_latin1)."""
+        self = cls.__new__(cls)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        cmap = np.ascontiguousarray(char_to_id, dtype=np.int32)
+        self.n_samples = (len(data) + sample_bytes - 1) // sample_bytes if len(data) else 1
+        self.n_tokens = n_tokens
+        self._h = lib_mt().cpu_create_latin1(data.ctypes.data, len(data), sample_bytes,
+                                             _p(cmap, ctypes.c_int32), n_tokens, extra, threads)
+        return self
 
     def close(self):
         if self._h:

@@ -31,7 +31,7 @@ def test_addon_builds_and_exports():
     out = subprocess.check_output([NODE, '-e', "const a=require(process.argv[1]);"
                                    "console.log(Object.keys(a).sort().join(','))",
                                    os.path.join(ADDON_DIR, 'bpe_napi.node')], text=True)
-    assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEngine,'
+    assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEngine,destroyEngine,'
                            'deviceCount,encodeMerges,findNextMerge,mergeUntil,readCorpus,'
                            'readSamples,sampleLengths,setTokenLen16')
 

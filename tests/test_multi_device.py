@@ -123,6 +123,34 @@ def test_samples_added_after_merging_go_to_the_last_shard():
     assert e.samples() == st2.samples()
 
 
+def test_sample_with_new_ids_after_merging_grows_every_shard():
+    """A later sample brings ids the shards never saw (the C-ABI caller registers nothing): every
+    shard's vocabulary grows alike, so the next merges number their tokens alike and match the
+    oracle on the whole corpus."""
+    rng = random.Random(21)
+    V = 12
+    first = [np.array([rng.randrange(V) for _ in range(3000)], np.int32) for _ in range(6)]
+    e = multi_engine(first, [1] * V, 3)
+    m1 = e.merge_until(0, 2, 8)
+    nt = e.num_tokens()
+    assert nt == V + 8
+    # ids nt .. nt+4 are brand new (never registered); the sample mixes them with old ones
+    later = np.array([rng.choice([nt, nt + 1, nt + 4, 0, 1]) for _ in range(5000)], np.int32)
+    e.add_sample(later)
+    assert e.num_tokens() == nt + 5
+    m2 = e.merge_until(0, 2, 12)
+    st = OracleState(np.concatenate(first), np.concatenate([[0], np.cumsum([len(s) for s in first])]),
+                     [1] * V, V)
+    assert m1 == st.merge_until(0, 2, 8)
+    ids = np.concatenate([st.ids, later])
+    off = np.concatenate([st.off, [st.off[-1] + len(later)]])
+    l16 = list(st.len16[:st.n_tokens]) + [1] * 5
+    st2 = OracleState(ids, off, l16, nt + 5)
+    assert m2 == st2.merge_until(0, 2, 12)
+    assert e.samples() == st2.samples()
+    e.close()
+
+
 def test_per_shard_entry_points_refuse_a_multi_context():
     e = pkg.Engine(devices=[0, 0], reduce='host')
     with pytest.raises(pkg.BpeError, match='multi-device'):
@@ -137,3 +165,55 @@ def test_rccl_exchange_over_two_devices():
     two = pkg.Engine(devices=[0, 1], reduce='rccl')
     two.add_latin1(data, sample_bytes=1 << 20)
     assert two.merge_until(0, 2, 300) == one.merge_until(0, 2, 300)
+
+
+@pytest.mark.parametrize('shards,mib,n,max_length', [(3, 6, 900, 0), (4, 4, 600, 5)])
+def test_maintained_state_over_shards_on_zipf_words(shards, mib, n, max_length):
+    """A skewed corpus over several shards: the cold pairs outgrow the sketch, the shards move to
+    the maintained state (global tables on every shard, delta rows exchanged per merge) and stay
+    in the device loop.  Same merges and corpus as one context."""
+    data = pkg.synth_zipf(mib << 20, seed=12345)
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    want = one.merge_until(max_length, 2, n)
+    ids1, off1 = one.read_corpus()
+    one.close()
+    multi = pkg.Engine(devices=[0] * shards, reduce='host')
+    multi.add_latin1(data, sample_bytes=1 << 20)
+    multi.stats_enable(True)
+    got = multi.merge_until(max_length, 2, n)
+    st = multi.stats()
+    assert got == want
+    ids, off = multi.read_corpus()
+    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    assert st['fused_passes'] > n // 2, st      # (summed over the shards)
+    assert st['loop_host'] <= 12, st
+    multi.close()
+
+
+@pytest.mark.slow
+def test_eight_shards_to_the_32k_vocabulary():
+    """8 shards of the C5 stream on one device (host-copy exchange, the same rank loop as RCCL
+    over 8 GPUs) taken to the 32k-token vocabulary: past the sketch's reach the shards keep the
+    global tables themselves (maintained state), so the iterations stay in the device loop
+    (few host hand-offs); merges and final corpus equal one context's."""
+    n = 512 << 20
+    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    one = pkg.Engine(0)
+    _, nt, _ = one.add_latin1(data, sample_bytes=1 << 20)
+    want = one.merge_until(0, 2, 32768 - nt)
+    ids1, _ = one.read_corpus()
+    one.close()
+    multi = pkg.Engine(devices=[0] * 8, reduce='host')
+    multi.add_latin1(data, sample_bytes=1 << 20)
+    del data
+    multi.stats_enable(True)
+    got = multi.merge_until(0, 2, 32768 - nt)
+    st = multi.stats()
+    assert len(got) == len(want) == 32768 - nt
+    assert got == want
+    ids, _ = multi.read_corpus()
+    assert np.array_equal(ids, ids1)
+    assert st['loop_host'] <= 24, st
+    assert st['fused_passes'] > 8 * 10000, st   # (summed over the 8 shards)
+    multi.close()

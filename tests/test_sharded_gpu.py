@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
-           mib=3):
+           mib=3, corpus='uniform'):
     import importlib
     import sys
     import torch
@@ -25,7 +25,9 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
         torch.cuda.set_device(0)
         tr = sharded.ShardedTrainer.synthetic(device=0, rank=rank, world=world,
                                               bytes_per_rank=mib << 20, sample_bytes=1 << 20,
-                                              seed=seed, alphabet=A, base=base, dist=dist)
+                                              seed=seed, alphabet=A, base=base, dist=dist,
+                                              corpus=corpus)
+        tr.engine.stats_enable(True)
         if mode == 'step':
             for _ in range(n):
                 if tr.step(max_length, 2) is None:
@@ -33,7 +35,7 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
         else:
             tr.run(n, max_length, 2)     # the device-resident rank loop
         ids, off = tr.engine.read_corpus()
-        q.put((rank, tr.merges, ids.tolist(), off.tolist()))
+        q.put((rank, tr.merges, ids.tolist(), off.tolist(), tr.engine.stats()))
     finally:
         dist.destroy_process_group()
 
@@ -56,9 +58,12 @@ def run_ranks(world, **kw):
     return res
 
 
-def single_engine(world, n=60, max_length=0, seed=777, A=40, base=60, mib=3, **_):
+def single_engine(world, n=60, max_length=0, seed=777, A=40, base=60, mib=3, corpus='uniform', **_):
     from bpe_amd import pkg
-    data = pkg.synth_latin1((mib * world) << 20, seed=seed, A=A, base=base)
+    if corpus == 'zipf':
+        data = pkg.synth_zipf((mib * world) << 20, seed=seed, sample_bytes=1 << 20)
+    else:
+        data = pkg.synth_latin1((mib * world) << 20, seed=seed, A=A, base=base)
     e = pkg.Engine(0)
     e.add_latin1(data, sample_bytes=1 << 20)
     want = e.merge_until(max_length, 2, n)
@@ -73,6 +78,7 @@ def check(world, **kw):
     for r in range(world):
         assert [tuple(m) for m in res[r][0]] == want, 'rank %d merges' % r
     assert sum((res[r][1] for r in range(world)), []) == ids
+    return [res[r][3] for r in range(world)]
 
 
 def test_two_ranks_on_one_gpu_match_single_engine():
@@ -88,3 +94,19 @@ def test_rank_loop_two_ranks_match_single_engine():
 
 def test_rank_loop_three_ranks_max_length():
     check(3, mode='loop', n=200, max_length=3, seed=4242, A=12, base=97, mib=2)
+
+
+def test_rank_loop_maintained_state_on_zipf_words():
+    """A skewed corpus (Zipf words): the cold pairs outgrow the sketch, so the ranks move to the
+    maintained state (every rank holds the global tables; each merge exchanges only the delta
+    rows of the pairs it touched, bpe_set_global_counts) and stay there: most merges in that
+    state, few host iterations, the same merges and corpus as one engine."""
+    st = check(2, mode='loop', n=700, corpus='zipf', mib=4, seed=12345)
+    for s in st:
+        assert s['fused_passes'] > 300, s
+        assert s['loop_host'] <= 12, s
+
+
+def test_rank_loop_maintained_state_three_ranks_max_length():
+    st = check(3, mode='loop', n=400, corpus='zipf', mib=2, seed=99, max_length=6)
+    assert all(s['fused_passes'] > 100 for s in st), st

@@ -10,6 +10,6 @@ for spec in "$@"; do
   envs=""
   [[ "$spec" == *:* ]] && envs=${spec#*:}
   name=$(basename "$lib" .so)${envs:+_${envs//[=,]/_}}
-  env BPE_LIB=$lib ${envs//,/ } timeout -k 10 300 python3 bench.py --steps $STEPS --no-cpu-baseline --no-incremental > "$OUT/$name.json"
+  env BPE_LIB=$lib ${envs//,/ } timeout -k 10 300 python3 bench.py --steps $STEPS --no-cpu-baseline > "$OUT/$name.json"
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; b=d['breakdown_ms_per_step']; print(sys.argv[2], 'ms/step %.4f k_step %.4f frac %.3f value %.4g compactions %d' % (d['ms_per_step'], r['kernel_avg_ms'], r['frac'], d['value'], b['compactions']))" "$OUT/$name.json" "$name"
 done

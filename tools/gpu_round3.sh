@@ -1,18 +1,17 @@
 #!/bin/bash
-# One GPU-box pass of round 2: GPU parity tests, smoke, the default bench line, the rocprofv3
-# kernel-trace stats of the same bench command, FETCH_SIZE / WRITE_SIZE and two SQ counter passes
-# (each its own run, no trace domains), the JS drop-in bench.
-# Usage (repo root, on the GPU box): tools/gpu_round2.sh TAG [what...]
-#   what ∈ tests smoke bench prof pmc sq js
+# One GPU-box pass of round 3.  Usage (repo root, on the GPU box): tools/gpu_round3.sh TAG [what...]
+#   what ∈ tests smoke driver bench prof pmc sq pixab slow
+#   driver: the driver's exact bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
+#   pixab:  the incremental mode's parity tests on the -structurizecfg-skip-uniform-regions build
 set -eo pipefail
-TAG=${1:-r02}; shift || true
-WHAT=${*:-tests smoke bench prof pmc sq js}
+TAG=${1:-r03}; shift || true
+WHAT=${*:-tests smoke driver bench prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 has() { [[ " $WHAT " == *" $1 "* ]]; }
 if has tests; then
-  timeout -k 10 1000 python3 -u -m pytest tests -m gpu -v --maxfail=5 --timeout 400 \
+  timeout -k 10 1100 python3 -u -m pytest tests -m gpu -v --maxfail=5 --timeout 400 ${PYTEST_EXTRA} \
       --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
   tail -3 "$OUT/pytest_gpu.log"
 fi
@@ -20,14 +19,18 @@ if has smoke; then
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
   cat "$OUT/smoke.log"
 fi
+if has driver; then
+  /usr/bin/time -v timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver.jsonl" 2> "$OUT/driver.err"
+  cat "$OUT/driver.jsonl"; grep "Elapsed" "$OUT/driver.err"
+fi
 if has bench; then
-  timeout -k 10 600 python3 bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
+  timeout -k 10 600 python3 bench.py --incremental > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
   cat "$OUT/bench.jsonl"
 fi
 if has prof; then
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
-      -- python3 bench.py > "$OUT/trace.log" 2>&1
-  find "$OUT/trace" -name '*kernel_stats.csv' -exec head -12 {} \;
+      -- python3 bench.py --no-cpu-baseline > "$OUT/trace.log" 2>&1
+  find "$OUT/trace" -name '*kernel_stats.csv' -exec head -14 {} \;
 fi
 PMC_BENCH="bench.py --steps 300 --warmup 5 --no-cpu-baseline"
 if has pmc; then
@@ -44,11 +47,11 @@ if has sq; then
       -d "$OUT/sq2" -o run --output-format csv -- python3 $PMC_BENCH > "$OUT/sq2.log" 2>&1
   python3 tools/sq_loop_summary.py "$OUT" > "$OUT/sq_summary.txt" && cat "$OUT/sq_summary.txt"
 fi
-if has js; then
-  timeout -k 10 300 node tools/bench_js.js 64 1000 5 > "$OUT/bench_js.json" 2> "$OUT/bench_js.err"
-  cat "$OUT/bench_js.json"
-  timeout -k 10 300 python3 tools/loop_bench.py 64 1000 5 > "$OUT/bench_py64.json"
-  cat "$OUT/bench_py64.json"
+if has pixab; then
+  BPE_LIB=gpurun_exp/sk.so timeout -k 10 600 python3 -u -m pytest tests/test_incremental.py tests/test_gpu_parity.py \
+      -m gpu -k "pix or incremental" -v --timeout 300 --timeout-method thread > "$OUT/pixab.log" 2>&1 \
+      || { tail -40 "$OUT/pixab.log"; exit 1; }
+  tail -3 "$OUT/pixab.log"
 fi
 # keep the merged-back output small (the raw per-dispatch CSVs are tens of MB)
 find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
     -- python3 bench.py --corpus zipf --steps $STEPS --no-cpu-baseline > "$OUT/trace.log" 2>&1
 find "$OUT/trace" -name '*kernel_stats.csv' -exec head -16 {} \;
-PMC="bench.py --corpus zipf --steps 600 --warmup 2000 --no-cpu-baseline --no-incremental"
+PMC="bench.py --corpus zipf --steps 600 --warmup 2000 --no-cpu-baseline"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 $PMC > "$OUT/fetch.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 $PMC > "$OUT/write.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
