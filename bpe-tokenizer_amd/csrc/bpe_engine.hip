@@ -10,7 +10,6 @@
 // so a mergeUntil iteration streams the corpus exactly once.
 #include "bpe_kernels.hip.h"
 #include "bpe_pix.hip.h"
-#include "bpe_pixlib.h"
 #include "bpe.h"
 #include "bpe_multi.h"
 #include "bpe_tools.h"
@@ -1634,8 +1633,10 @@ int pix_alloc(PixState *P, T **out, size_t n) {
 }
 
 // The index of the current corpus: the slot array is the compacted corpus itself (d_ids, n live
-// slots), links i -> i+1, and one radix sort of (pair key, slot) gives every pair's list; counts
-// follow from the run offsets (an inclusive max-scan of run starts).
+// slots), links i -> i +- 1, and every pair's list from a counting scatter into the pair table
+// (bpe_pix.hip.h, index build): run starts per block and their carries, then per position its
+// pair's slot, list length and count, a pool segment per pair, and the positions into the
+// segments.  A table that fills past a quarter is built again four times larger.
 int pix_build(bpe_ctx *c, int64_t max_length) {
     int rc;
     if ((rc = settle(c))) return rc;
@@ -1658,51 +1659,23 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
     const uint64_t pool_cap = std::min<uint64_t>(0xFFFFFFF0ull, (uint64_t)N + std::max<uint64_t>(N / 2, 1u << 22));
     PixBufs &B = P->B;
     if ((rc = pix_alloc(P, &B.pool, pool_cap))) return rc;
-    {
-        Scratch t;
-        uint32_t *A, *Bk, *V, *D, *R, *d_nruns;
-        int32_t *runmark, *run_start;
-        if ((rc = t.get(&A, N)) || (rc = t.get(&Bk, N)) || (rc = t.get(&V, N)) || (rc = t.get(&D, N)) ||
-            (rc = t.get(&R, N)) || (rc = t.get(&d_nruns, 2)))
-            return rc;
-        runmark = reinterpret_cast<int32_t *>(R);
-        run_start = reinterpret_cast<int32_t *>(D);
-        k_pix_build_keys<<<4096, 256, 0, s>>>(C, A, V, runmark);
-        HIP_TRY(hipGetLastError());
-        // temp storage for every library call below
-        size_t tb = 0, t1 = 0;
-        HIP_TRY(pixlib_sort_pairs(nullptr, t1, A, Bk, V, B.pool, N, s));
-        tb = std::max(tb, t1);
-        HIP_TRY(pixlib_max_scan(nullptr, t1, runmark, run_start, N, s));
-        tb = std::max(tb, t1);
-        HIP_TRY(pixlib_reduce_by_key(nullptr, t1, Bk, V, A, R, d_nruns, N, s));
-        tb = std::max(tb, t1);
-        HIP_TRY(pixlib_run_lengths(nullptr, t1, Bk, A, D, d_nruns + 1, N, s));
-        tb = std::max(tb, t1);
-        HIP_TRY(pixlib_exclusive_sum(nullptr, t1, D, Bk, N, s));
-        tb = std::max(tb, t1);
-        void *tmp;
-        if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
-        HIP_TRY(pixlib_max_scan(tmp, tb, runmark, run_start, N, s));
-        HIP_TRY(pixlib_sort_pairs(tmp, tb, A, Bk, V, B.pool, N, s));
-        // A: counted flags in sorted order; then per pair (V: keys, R: counts)
-        k_pix_build_counted<<<4096, 256, 0, s>>>(C, B.pool, run_start, A);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(pixlib_reduce_by_key(tmp, tb, Bk, V, A, R, d_nruns, N, s));
-        // (A: keys again, D: list lengths, Bk: list offsets)
-        HIP_TRY(pixlib_run_lengths(tmp, tb, Bk, A, D, d_nruns + 1, N, s));
-        uint32_t nruns[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(nruns, d_nruns, sizeof nruns, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (nruns[0] != nruns[1] || nruns[0] == 0 || nruns[0] > N)
-            return fail(BPE_ERR_STATE, "bpe native: position index: bad pair runs");
-        HIP_TRY(pixlib_exclusive_sum(tmp, tb, D, Bk, nruns[0], s));
-        // the pair table: room for the current pairs and the ones merges will add
-        uint64_t cap = 1u << 20;
-        while (cap < 4ull * nruns[0] || cap < (uint64_t)N / 8) cap <<= 1;
+    const uint32_t nblk = (N + PB - 1) / PB;
+    int32_t *carry;
+    if ((rc = pix_alloc(P, &carry, nblk))) return rc;
+    k_pix_build_links<<<4096, 256, 0, s>>>(C, carry);
+    k_pix_scan_max<<<1, 1024, 0, s>>>(carry, nblk);
+    HIP_TRY(hipGetLastError());
+    if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
+    HIP_TRY(hipHostMalloc((void **)&P->h_ctl, sizeof(PixCtl), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&P->h_log, 3 * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
+    // the pair table: room for the current pairs and the ones merges will add
+    uint64_t cap = 1u << 20;
+    while (cap < (uint64_t)N / 8) cap <<= 1;
+    PixTable &T = P->T;
+    for (int attempt = 0;; ++attempt) {
         if (cap > (1ull << 31)) return PIX_NOT_ELIGIBLE;
         P->cap = cap;
-        PixTable &T = P->T;
+        T = PixTable{};
         T.mask = (uint32_t)(cap - 1);
         T.len16 = c->d_len16;
         T.ml = max_length;
@@ -1719,34 +1692,45 @@ int pix_build(bpe_ctx *c, int64_t max_length) {
         HIP_TRY(hipMemsetAsync(T.len, 0, cap * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(T.bdirty, 0, T.nblocks * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(T.sbdirty, 0, T.nsuper * sizeof(uint32_t), s));
-        // per-merge buffers
-        B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
-        B.ent_cap = 2 * B.site_cap + 16;
-        if ((rc = pix_alloc(P, &B.sites, B.site_cap)) || (rc = pix_alloc(P, &B.ent, B.ent_cap)) ||
-            (rc = pix_alloc(P, &B.dblocks, T.nblocks)) ||
-            (rc = pix_alloc(P, &B.dsuper, T.nsuper)))
-            return rc;
-        if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
-        HIP_TRY(hipHostMalloc((void **)&P->h_ctl, sizeof(PixCtl), hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc((void **)&P->h_log, 3 * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
         PixCtl *h = P->h_ctl;
         memset(h, 0, sizeof *h);
         h->status = PIX_RUN;
         h->max_length = max_length;
         h->max_id = BPE_MAX_VOCAB;
         h->next_id = (int32_t)c->h_len16.size();
-        h->pool_top = N;
         h->pool_cap = pool_cap;
         h->used_cap = cap / 10 * 7;
         HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
-        k_pix_build_insert<<<4096, 256, 0, s>>>(T, P->d_ctl, A, R, D, Bk, d_nruns);
-        k_pix_bmax_all<<<4096, 256, 0, s>>>(T);
-        k_pix_sbmax<<<1024, 256, 0, s>>>(T, B, P->d_ctl, 1);
+        k_pix_build_count<<<4096, 256, 0, s>>>(C, T, P->d_ctl, carry);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));   // (before the scratch goes)
-        if (h->status != PIX_RUN) return fail(BPE_ERR_STATE, "bpe native: position index: pair table full");
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!h->err && h->used * 4 <= cap) break;
+        // too full to probe well: a table four times larger
+        for (void *q : {(void *)T.keys, (void *)T.cnt, (void *)T.off, (void *)T.len, (void *)T.fill,
+                        (void *)T.bmax, (void *)T.sbmax, (void *)T.bdirty, (void *)T.sbdirty}) {
+            P->owned.erase(std::find(P->owned.begin(), P->owned.end(), q));
+            dfree(q);
+        }
+        cap <<= 2;
+        if (attempt == 3) return PIX_NOT_ELIGIBLE;
     }
+    k_pix_build_alloc<<<4096, 256, 0, s>>>(T, P->d_ctl, (uint32_t)cap);
+    k_pix_build_fill<<<4096, 256, 0, s>>>(C, T, B);
+    // per-merge buffers
+    B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
+    B.ent_cap = 2 * B.site_cap + 16;
+    if ((rc = pix_alloc(P, &B.sites, B.site_cap)) || (rc = pix_alloc(P, &B.ent, B.ent_cap)) ||
+        (rc = pix_alloc(P, &B.dblocks, T.nblocks)) || (rc = pix_alloc(P, &B.dsuper, T.nsuper)))
+        return rc;
+    k_pix_bmax_all<<<4096, 256, 0, s>>>(T);
+    k_pix_sbmax<<<1024, 256, 0, s>>>(T, B, P->d_ctl, 1);
+    HIP_TRY(hipGetLastError());
+    PixCtl *h = P->h_ctl;
+    HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->status != PIX_RUN) return fail(BPE_ERR_STATE, "bpe native: position index: pair table full");
+    if (h->pool_top > (uint64_t)N) return fail(BPE_ERR_STATE, "bpe native: position index: bad pair lists");
     c->counts_valid = c->carry_valid = c->best_ready = false;
     c->cold_exact = false;
     if (c->stats_on) c->stats.pix_builds += 1;
@@ -1762,19 +1746,17 @@ int pix_finish(bpe_ctx *c) {
     const uint32_t N = P->C.n;
     {
         Scratch t;
-        uint8_t *flag;
-        uint32_t *d_nsel;
+        uint32_t *cnt, *d_total;
+        const uint32_t nblk = (N + PB - 1) / PB;
         int rc;
-        if ((rc = t.get(&flag, N)) || (rc = t.get(&d_nsel, 1))) return rc;
-        k_pix_live_flags<<<4096, 256, 0, s>>>(c->d_ids, N, flag);
-        size_t tb = 0;
-        HIP_TRY(pixlib_select_flagged(nullptr, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
-        void *tmp;
-        if ((rc = t.get(reinterpret_cast<uint8_t **>(&tmp), tb))) return rc;
+        if ((rc = t.get(&cnt, nblk)) || (rc = t.get(&d_total, 1))) return rc;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
-        HIP_TRY(pixlib_select_flagged(tmp, tb, c->d_ids, flag, c->d_tmp, d_nsel, N, s));
+        k_pix_live_count<<<4096, 256, 0, s>>>(c->d_ids, N, cnt);
+        k_pix_scan_sum<<<1, 1024, 0, s>>>(cnt, nblk, d_total);
+        k_pix_live_scatter<<<4096, 256, 0, s>>>(c->d_ids, N, cnt, c->d_tmp);
+        HIP_TRY(hipGetLastError());
         uint32_t nsel = 0;
-        HIP_TRY(hipMemcpyAsync(&nsel, d_nsel, sizeof nsel, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&nsel, d_total, sizeof nsel, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if ((int64_t)nsel != c->live_slots)
             return fail(BPE_ERR_STATE, "bpe native: position index: live slots lost");

@@ -980,6 +980,16 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             return;
         }
     }
+#ifdef BPE_PROBE_NOCOUNT
+    if (MODE == MODE_TABLE) {   // (timing probe only: the ring and its bookkeeping, no counting)
+        s.first_tok = s.n_live ? s.first_tok : w.first;
+        s.par = 0;
+        s.prev = w.last;
+        s.n_live += len;
+        s.in_lead = 0;
+        return;
+    }
+#endif
     const int32_t t0 = w.t[0], t1 = w.t[1], t2 = w.t[2], t3 = w.t[3];
     // lane 63's bit when the chunk is partial (an integer mask, not a boolean: uniform booleans
     // cost a lane-mask round trip per use)
@@ -1137,6 +1147,14 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
                                             int32_t mc, uint32_t key,
                                             const __amdgpu_buffer_rsrc_t rs, int c, int lane,
                                             Apply &ap) {
+#ifdef BPE_PROBE_NOAPPLY
+    if (lane >= 0) {   // (timing probe only: no merge detection or rewrite)
+        ap.prev = w.last;
+        ap.par = 0;
+        ap.match = 0;
+        return;
+    }
+#endif
     // The common case, no (a, b) in the chunk: four packed (slot, right neighbour) compares.  In a
     // partial chunk lane 63's slot 3 (dead) stands in for the last live slot, paired with nxt.
     // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)

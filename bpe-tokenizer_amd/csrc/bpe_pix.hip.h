@@ -182,45 +182,200 @@ __device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32
     return p != PIX_NONE && C.tok[p] == x;
 }
 
-// ---- index build ------------------------------------------------------------------------------
-__global__ void k_pix_build_keys(PixCorpus C, uint32_t *keys, uint32_t *vals, int32_t *runmark) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < C.n; i += gridDim.x * blockDim.x) {
-        const int32_t t = C.tok[i];
-        const int32_t u = i + 1 < C.n ? C.tok[i + 1] : SEP;
-        keys[i] = (t >= 0 && u >= 0) ? pix_key(t, u) : PIX_NONE;
-        vals[i] = i;
-        runmark[i] = (i == 0 || C.tok[i - 1] != t) ? (int32_t)i : 0;
-        C.nxt[i] = i + 1 < C.n ? i + 1 : PIX_NONE;
-        C.prv[i] = i > 0 ? i - 1 : PIX_NONE;
-    }
+// ---- index build: a counting scatter of every pair's positions into its segment -------------
+// (no sort: the pair table itself is the histogram)
+//   k_pix_build_links  links i -> i +- 1, and per block of PB positions its last run start
+//   k_pix_scan_max     the run start each block's first position continues (exclusive max-scan)
+//   k_pix_build_count  per valid pair position: its table slot (claimed on first sight), list
+//                      length + 1, count + 1 when counted (a pair (x, x) at an odd offset of its
+//                      run is not, core.ts:285-290)
+//   k_pix_build_alloc  a pool segment per pair (one pool atomic per wave)
+//   k_pix_build_fill   every position into its pair's segment
+constexpr int PB = 4096;          // positions per build block (256 threads x 16)
+constexpr int PB_PER = PB / 256;
+
+__device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t *red) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    return v;
 }
 
-// counted[j] for the sorted position pool[j]: 1, except a pair (x, x) at an odd offset of its run
-__global__ void k_pix_build_counted(PixCorpus C, const uint32_t *pool, const int32_t *run_start,
-                                    uint32_t *counted) {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < C.n; j += gridDim.x * blockDim.x) {
-        const uint32_t i = pool[j];
-        uint32_t k = 1;
-        if (i + 1 < C.n && C.tok[i] == C.tok[i + 1]) k = ((i - (uint32_t)run_start[i]) & 1u) ? 0u : 1u;
-        counted[j] = k;
-    }
-}
-
-__global__ void k_pix_build_insert(PixTable t, PixCtl *ctl, const uint32_t *uniq,
-                                   const uint32_t *counts, const uint32_t *lens,
-                                   const uint32_t *offs, const uint32_t *n_runs) {
-    const uint32_t n = *n_runs;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        if (uniq[j] == PIX_NONE) continue;
-        const uint32_t s = pix_slot(t, ctl, uniq[j], true, true);
-        if (s == PIX_NONE) {
-            ctl->err = 9;
-            ctl->status = PIX_ERROR;
-            continue;
+__global__ void __launch_bounds__(256) k_pix_build_links(PixCorpus C, int32_t *__restrict__ blast) {
+    __shared__ int32_t red[4];
+    const uint32_t nblk = (C.n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint32_t i0 = blk * PB, i1 = min(i0 + PB, C.n);
+        int32_t m = -1;
+        for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) {
+            const int32_t t = C.tok[i];
+            if (i == 0 || C.tok[i - 1] != t) m = (int32_t)i;   // (i grows: the last one wins)
+            C.nxt[i] = i + 1 < C.n ? i + 1 : PIX_NONE;
+            C.prv[i] = i > 0 ? i - 1 : PIX_NONE;
         }
-        t.cnt[s] = counts[j];
-        t.len[s] = lens[j];
-        t.off[s] = offs[j];
+        m = block_max_i32(m, red);
+        if (threadIdx.x == 0) blast[blk] = m;
+    }
+}
+
+// In place: v[b] <- max(v[0 .. b-1]) (-1 for b = 0).  One block of 1024.
+__global__ void __launch_bounds__(1024) k_pix_scan_max(int32_t *__restrict__ v, uint32_t n) {
+    __shared__ int32_t part[1024];
+    const uint32_t per = (n + 1023) / 1024, t = threadIdx.x;
+    int32_t acc = -1;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t i = t * per + k;
+        if (i < n) acc = max(acc, v[i]);
+    }
+    part[t] = acc;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const int32_t o = t >= d ? part[t - d] : -1;
+        __syncthreads();
+        part[t] = max(part[t], o);
+        __syncthreads();
+    }
+    int32_t run = t ? part[t - 1] : -1;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t i = t * per + k;
+        if (i < n) {
+            const int32_t x = v[i];
+            v[i] = run;
+            run = max(run, x);
+        }
+    }
+}
+
+// In place: v[b] <- v[0] + ... + v[b-1] (u32).  One block of 1024.
+__global__ void __launch_bounds__(1024) k_pix_scan_sum(uint32_t *__restrict__ v, uint32_t n,
+                                                       uint32_t *__restrict__ total) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (n + 1023) / 1024, t = threadIdx.x;
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t i = t * per + k;
+        if (i < n) acc += v[i];
+    }
+    part[t] = acc;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t o = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += o;
+        __syncthreads();
+    }
+    uint32_t run = t ? part[t - 1] : 0;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t i = t * per + k;
+        if (i < n) {
+            const uint32_t x = v[i];
+            v[i] = run;
+            run += x;
+        }
+    }
+    if (t == 1023 && total) *total = part[1023];
+}
+
+// The block's PB positions (+ the next one) staged in LDS; per thread 16 consecutive ones with
+// their run starts: a block max-scan of the threads' last run starts, seeded with the block's
+// carry (the run start its first position continues).
+struct BuildSpan {
+    uint32_t i0;     // first position of the thread
+    int32_t rs;      // run start of the position before i0 (carry into the thread)
+};
+
+__device__ __forceinline__ BuildSpan build_span(const PixCorpus &C, int32_t *tk, int32_t *sc,
+                                                uint32_t blk, int32_t carry) {
+    const uint32_t b0 = blk * PB;
+    for (uint32_t k = threadIdx.x; k <= (uint32_t)PB; k += 256) {
+        const uint32_t i = b0 + k;
+        tk[k] = i < C.n ? C.tok[i] : SEP;
+    }
+    __syncthreads();
+    const uint32_t l0 = threadIdx.x * PB_PER;
+    int32_t last = -1;
+    for (int k = 0; k < PB_PER; ++k) {
+        const uint32_t l = l0 + k, i = b0 + l;
+        if (i < C.n && (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != tk[l])) last = (int32_t)i;
+    }
+    sc[threadIdx.x] = last;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const int32_t o = (int)threadIdx.x >= d ? sc[threadIdx.x - d] : -1;
+        __syncthreads();
+        sc[threadIdx.x] = max(sc[threadIdx.x], o);
+        __syncthreads();
+    }
+    BuildSpan sp;
+    sp.i0 = b0 + l0;
+    sp.rs = max(carry, threadIdx.x ? sc[threadIdx.x - 1] : -1);
+    return sp;
+}
+
+__global__ void __launch_bounds__(256) k_pix_build_count(PixCorpus C, PixTable t, PixCtl *ctl,
+                                                         const int32_t *__restrict__ carry) {
+    __shared__ int32_t tk[PB + 1];
+    __shared__ int32_t sc[256];
+    const uint32_t nblk = (C.n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const BuildSpan sp = build_span(C, tk, sc, blk, carry[blk]);
+        int32_t rs = sp.rs;
+        const uint32_t l0 = threadIdx.x * PB_PER;
+        for (int k = 0; k < PB_PER; ++k) {
+            const uint32_t l = l0 + k, i = sp.i0 + k;
+            if (i >= C.n) break;
+            const int32_t x = tk[l], y = i + 1 < C.n ? tk[l + 1] : SEP;
+            if (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != x) rs = (int32_t)i;
+            if ((x | y) < 0) continue;
+            const uint32_t s = pix_slot(t, ctl, pix_key(x, y), true, true);
+            if (s == PIX_NONE) {
+                atomicOr(&ctl->err, 9);   // (the table is too full: the host builds a bigger one)
+                continue;
+            }
+            atomicAdd(&t.len[s], 1u);
+            if (x != y || !((i - (uint32_t)rs) & 1u)) atomicAdd(&t.cnt[s], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pix_build_alloc(PixTable t, PixCtl *ctl, uint32_t cap) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t s0 = (blockIdx.x * blockDim.x) & ~63u; s0 < cap; s0 += gridDim.x * blockDim.x) {
+        const uint32_t s = s0 + lane + (threadIdx.x & ~63u);
+        const uint32_t len = s < cap ? t.len[s] : 0u;
+        uint32_t incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        const uint32_t tot = __shfl(incl, 63);
+        unsigned long long base = 0;
+        if (lane == 0 && tot) base = atomicAdd(&ctl->pool_top, (unsigned long long)tot);
+        base = __shfl(base, 0);
+        if (len) {
+            t.off[s] = (uint32_t)(base + incl - len);
+            t.fill[s] = 0;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pix_build_fill(PixCorpus C, PixTable t, PixBufs B) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i + 1 < C.n;
+         i += gridDim.x * blockDim.x) {
+        const int32_t x = C.tok[i], y = C.tok[i + 1];
+        if ((x | y) < 0) continue;
+        const uint32_t key = pix_key(x, y);
+        uint32_t s = pix_hash(key) & t.mask;
+        // (present: claimed by the count, within its probe bound)
+        for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
+        if (t.keys[s] != key) continue;
+        const uint32_t k = atomicAdd(&t.fill[s], 1u);
+        B.pool[t.off[s] + k] = i;
     }
 }
 
@@ -809,10 +964,48 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
     }
 }
 
-// dense corpus back from the slot array: live slots (tokens and SEPs) in order
-__global__ void k_pix_live_flags(const int32_t *tok, uint32_t n, uint8_t *flag) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        flag[i] = tok[i] >= SEP;
+// The dense corpus back from the slot array: its live slots (tokens and SEPs) in order.  Per
+// block of PB slots the live count (k_pix_live_count), an exclusive sum over the blocks
+// (k_pix_scan_sum), then each block writes its live slots at its offset (k_pix_live_scatter).
+__global__ void __launch_bounds__(256) k_pix_live_count(const int32_t *__restrict__ tok, uint32_t n,
+                                                        uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t red[4];
+    const uint32_t nblk = (n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        uint32_t c = 0;
+        for (uint32_t i = blk * PB + threadIdx.x; i < min(blk * PB + PB, n); i += 256)
+            c += tok[i] >= SEP;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) cnt[blk] = red[0] + red[1] + red[2] + red[3];
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restrict__ tok, uint32_t n,
+                                                          const uint32_t *__restrict__ off,
+                                                          int32_t *__restrict__ out) {
+    __shared__ uint32_t wsum[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t nblk = (n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        uint32_t o = off[blk];
+        for (uint32_t j0 = blk * PB; j0 < min(blk * PB + PB, n); j0 += 256) {
+            const uint32_t i = j0 + threadIdx.x;
+            const int32_t v = i < n ? tok[i] : TOMB;
+            const bool live = v >= SEP;
+            const unsigned long long m = __ballot(live);
+            if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t b = o;
+            for (int w = 0; w < wv; ++w) b += wsum[w];
+            if (live) out[b + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = v;
+            o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            __syncthreads();
+        }
+    }
 }
 
 }  // namespace bpe

@@ -115,6 +115,12 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0, in
     table = table.to(dev, copy=True)
     dist.all_reduce(table)
     gtable = table.to(sdev)
+
+    def sync():
+        # (collectives and copies run on torch's stream, the engine reads on its own)
+        if getattr(gtable, 'is_cuda', False):
+            torch.cuda.synchronize(gtable.device)
+    sync()
     heavy = shard.heavy(gtable, max_length)                  # identical decision on every rank
     if info is not None:
         info['heavy'] = heavy is not None
@@ -144,7 +150,9 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0, in
     else:
         ukeys = torch.zeros(0, dtype=torch.int32, device=dev)
         ucounts = torch.zeros(0, dtype=torch.int64, device=dev)
-    sel = shard.select(gtable, ukeys.to(sdev), ucounts.to(sdev), max_length, min_weight)
+    ukeys, ucounts = ukeys.to(sdev), ucounts.to(sdev)
+    sync()
+    sel = shard.select(gtable, ukeys, ucounts, max_length, min_weight)
     if sel is None:
         return None
     w, cands = sel
@@ -258,12 +266,15 @@ class ShardedTrainer:
         dist, eng = self.dist, self.engine
         gloo, all_reduce = self._collectives()
         dev = self.shard.device
+        # (torch's work here runs on its own stream: synchronized before each engine call that
+        # reads or writes a tensor made there, which the engine's stream would otherwise race)
         table = self.shard.export().clone()
         all_reduce(table, dist.ReduceOp.SUM)
         n = eng.cold_counts(None, None, 0)                     # (the pass; kept for the export)
         cap = max(1, n)
         keys = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         counts = torch.zeros(cap, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
         eng.cold_counts(keys.data_ptr(), counts.data_ptr(), cap)
         cdev = torch.device('cpu') if gloo else dev
         size = torch.tensor([n], dtype=torch.int64, device=cdev)
@@ -282,9 +293,9 @@ class ShardedTrainer:
         all_k = torch.cat([g[:z] for g, z in zip(gk, sizes)] + [kp[:0]]).to(dev).contiguous()
         all_c = torch.cat([g[:z] for g, z in zip(gc, sizes)] + [cp[:0]]).to(dev).contiguous()
         total = all_k.numel()
+        torch.cuda.synchronize(dev)
         eng.set_global_counts(table.data_ptr(), all_k.data_ptr() if total else None,
                               all_c.data_ptr() if total else None, total)
-        torch.cuda.synchronize(dev)
         self._maintained = True
         self._heavy_streak = 0
 
@@ -335,7 +346,7 @@ class ShardedTrainer:
                 self._maintained = False      # (the engines left the global state)
             if status == 1:
                 break
-            batch = min(LOOP_BATCH, 2 * batch) if status == 0 else max(1, 2 * len(got))
+            batch = min(LOOP_BATCH, 2 * batch if status == 0 else max(1, 2 * len(got)))
             if status == 2 and len(ms) < n:
                 info = {}
                 m = self.step(max_length, min_weight, info)     # the host protocol for this iteration
