@@ -123,7 +123,8 @@ def incremental_mode(args, stream_merges):
             'ms_per_step': dt * 1e3 / max(1, len(got)), 'seconds': dt,
             'equiv_pair_scans_per_s': scans / dt, 'speedup_vs_stream_loop': None,
             'merges': len(got), 'identical_merges_to_stream': same,
-            'index_builds': st['pix_builds'], 'merges_on_index': st['pix_merges'],
+            'index_builds': st['pix_builds'], 'index_build_ms': st['pix_build_ms'],
+            'merges_on_index': st['pix_merges'],
             'handed_to_stream': st['pix_host']}
 
 

@@ -15,6 +15,7 @@
 #include "bpe_tools.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
@@ -147,6 +148,8 @@ struct bpe_ctx {
     // device-resident mergeUntil loop: control block + merge log (pinned host mirrors)
     LoopCtl *d_ctl = nullptr, *h_ctl = nullptr;
     long long *d_log = nullptr, *h_log = nullptr;
+    unsigned int *d_ticket = nullptr;   // last-block tickets (k_tie_fused, k_select_maint; zero between launches)
+    BlockBest *d_brec = nullptr;        // k_select_maint's per-block bests
     // apply-only replay: per-merge replacement counts
     unsigned long long *d_repl = nullptr, *h_repl = nullptr;
     // sharded device loop (one rank): the caller's all-reduced exchange buffer (include/bpe.h
@@ -885,7 +888,10 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     }
     geometry(c);
     hipStream_t s = c->stream;
-    if (c->best_ready && c->best_ml == max_length) {
+    if (maint) {
+        // (k_select_maint takes the best over the hot bins itself)
+        HIP_TRY(hipMemsetAsync(c->d_res, 0, sizeof(Result), s));
+    } else if (c->best_ready && c->best_ml == max_length) {
         // keep the reduce's best key, clear the rest of the Result
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(Result) - offsetof(Result, n_cand), s));
     } else {
@@ -918,18 +924,17 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         c->span_mute = (c->span_tick++ % SPAN_EVERY) != 0;
         hipEvent_t e_sel = span_begin(c);
         if (maint) {
-            k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, max_length, c->d_res,
-                                                    c->d_ctl);
-            k_collect<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length,
-                                                c->d_res, c->d_cand, c->d_ctl);
+            // best key over the hot bins and the cold table, its pairs, the table's flags
+            k_select_maint<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length,
+                                                     c->d_res, c->d_cand, c->d_brec, c->d_ticket,
+                                                     c->d_ctl);
         } else {
             k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length,
                                                             c->d_res, c->d_cand, c->d_heavy,
                                                             c->d_ctl);
         }
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 0, nullptr);
-        k_tie<<<(c->R + 3) / 4, 256, 0, s>>>(A);
-        k_decide<<<1, 64, 0, s>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1, nullptr);
+        // the decision, the R3 tie pass when tied, and its commit: one launch
+        k_tie_fused<<<(c->R + 3) / 4, 256, 0, s>>>(A, c->d_len16, c->d_log, c->d_ticket);
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
@@ -959,8 +964,6 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
                                                                  c->d_ctl, -1, -1, -1, c->d_hot);
             k_reduce_rows<<<4 * INCR_RLIM / 2 / RR_COLS, 256, 0, s>>>(
                 c->d_partials, c->G, c->d_spill, c->d_hot, c->cold, -1, -1, -1, c->d_ctl);
-            k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length, c->d_res,
-                                                        c->d_ctl);
         } else {
             if (maint)
                 k_runs<MODE_FUSED><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
@@ -1030,8 +1033,9 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         c->stats.loop_host += h->n_host;
     }
     c->last_replaced = nd ? c->h_log[LOG_WORDS * (nd - 1) + 2] : c->last_replaced;
-    // every early-ended batch leaves the last reduce's best key in the Result
-    c->best_ready = true;
+    // every early-ended batch of the table state leaves the last reduce's best key in the Result
+    // (the maintained state selects with k_select_maint: nothing is left ready)
+    c->best_ready = !maint;
     c->best_ml = max_length;
     c->counts_valid = c->carry_valid = true;
     if (!maint) c->sketch_valid = true;
@@ -1116,7 +1120,9 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
             h->c = c->rl_last_c;
             h->w = c->rl_last_w;
         } else {
-            HIP_TRY(hipMemsetAsync(xchg, 0, nw * sizeof(unsigned long long), s));
+            // all of it: the rows past this batch's words must be zero when later batches reach
+            // them (k_apply_delta only zeroes the rows it consumes; the buffer may hold anything)
+            HIP_TRY(hipMemsetAsync(xchg, 0, XCHG_WORDS * sizeof(unsigned long long), s));
         }
     } else {
         nw = XCHG_HDR + TABLE_BINS;
@@ -1245,10 +1251,29 @@ int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *s
     HIP_TRY(hipStreamSynchronize(s));
     const bool glob = c->rl_global;
     if (h->status == LOOP_ERROR) {
+        const bool was_global = glob;
+        static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
+        if (dbg) {
+            HIP_TRY(hipMemcpy(c->h_log, c->d_log, LOG_WORDS * LOOP_BATCH * sizeof(long long),
+                              hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < h->n_done && i < LOOP_BATCH; ++i)
+                fprintf(stderr, "[bpe debug] rank %d batch merge %lld: (%lld, %lld) W %lld rep %lld\n",
+                        c->rl_rank, (long long)i, c->h_log[4 * i], c->h_log[4 * i + 1],
+                        c->h_log[4 * i + 2], c->h_log[4 * i + 3]);
+            fprintf(stderr, "[bpe debug] rank %d ctl: a %d b %d c %d w %lld tie %d vote %d base %lld\n",
+                    c->rl_rank, h->a, h->b, h->c, (long long)h->w, h->tie, h->vote, (long long)c->rl_base);
+        }
         leave_global(c);
         c->counts_valid = false;
-        return fail(BPE_ERR_STATE, "bpe native: rank loop: the shards' replacement counts do not "
-                                   "sum to W, or a tie pass found no occurrence");
+        char msg[256];
+        if (h->err == 1)
+            snprintf(msg, sizeof msg, "bpe native: rank loop: the shards' replacement counts sum to "
+                     "%llu, not W = %llu (merge %lld of the batch, %s state)", h->err_got, h->err_want,
+                     (long long)h->n_done, was_global ? "maintained" : "table");
+        else
+            snprintf(msg, sizeof msg, "bpe native: rank loop: a tie pass found no occurrence (merge "
+                     "%lld of the batch, %s state)", (long long)h->n_done, was_global ? "maintained" : "table");
+        return fail(BPE_ERR_STATE, msg);
     }
     const int64_t nd = h->n_done;
     if (nd < 0 || nd > c->rl_enqueued) return fail(BPE_ERR_STATE, "bpe native: rank loop: bad merge count");
@@ -1637,7 +1662,18 @@ int pix_alloc(PixState *P, T **out, size_t n) {
 // (bpe_pix.hip.h, index build): run starts per block and their carries, then per position its
 // pair's slot, list length and count, a pool segment per pair, and the positions into the
 // segments.  A table that fills past a quarter is built again four times larger.
+int pix_build_timed(bpe_ctx *c, int64_t max_length);
+
 int pix_build(bpe_ctx *c, int64_t max_length) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = pix_build_timed(c, max_length);
+    if (c->stats_on && rc == BPE_OK)
+        c->stats.pix_build_ms +=
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int pix_build_timed(bpe_ctx *c, int64_t max_length) {
     int rc;
     if ((rc = settle(c))) return rc;
     if (!c->packed)
@@ -1985,6 +2021,10 @@ int bpe_create(bpe_ctx **out, int device) {
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_ticket, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_brec, COLD_GRID))) return bail(rc);
+    if (hipMemset(c->d_ticket, 0, sizeof(unsigned int)) != hipSuccess)
+        return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
     if ((rc = dev_alloc(&c->d_repl, REPLAY_BATCH))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_repl, REPLAY_BATCH * sizeof(unsigned long long),
                       hipHostMallocDefault) != hipSuccess)
@@ -2036,7 +2076,7 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
-                    c->d_ctl, c->d_log, c->d_repl};
+                    c->d_ctl, c->d_log, c->d_repl, c->d_ticket, c->d_brec};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_cand) (void)hipHostFree(c->h_cand);
@@ -2479,6 +2519,7 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     if ((rc = exact_pass(c))) return rc;
     uint32_t nu = 0;
     HIP_TRY(hipMemcpy(&nu, c->cold.n_used, sizeof nu, hipMemcpyDeviceToHost));
+    nu = std::min<uint32_t>(nu, c->cold.mask + 1);
     *n_cold = nu;
     if ((int64_t)nu > cap) return fail(BPE_ERR_ARG, "bpe native: export buffer too small");
     if (nu) {
@@ -2583,6 +2624,29 @@ int bpe_recount(bpe_ctx *c) {
     leave_global(c);
     if ((rc = settle(c))) return rc;
     return run_pass(c, false, 0, 0, 0, nullptr);
+}
+
+// (debug: BPE_DEBUG_GLOBAL, bpe_multi.cpp) this context's maintained tables: the hot bins
+// (HOT_BINS u64 into hot) and the cold table's dense entries (up to cap; *n = n_used)
+int bpe_debug_tables(bpe_ctx *c, uint64_t *hot, uint32_t *keys, uint64_t *counts, int64_t cap,
+                     int64_t *n) {
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(hot, c->d_hot, HOT_BINS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    uint32_t nu = 0;
+    HIP_TRY(hipMemcpy(&nu, c->cold.n_used, sizeof nu, hipMemcpyDeviceToHost));
+    uint32_t of = 0;
+    HIP_TRY(hipMemcpy(&of, c->cold.overflow, sizeof of, hipMemcpyDeviceToHost));
+    if (of) fprintf(stderr, "[bpe debug] cold table overflow (n_used %u, capacity %u)\n", nu, c->cold.mask + 1);
+    nu = std::min<uint32_t>(nu, c->cold.mask + 1);
+    *n = nu;
+    const int64_t k = std::min<int64_t>(nu, cap);
+    if (k) {
+        HIP_TRY(hipMemcpy(keys, c->cold.dkeys, k * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(counts, c->cold.dcounts, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    return BPE_OK;
 }
 
 int bpe_get_stream(bpe_ctx *c, void **stream) {

@@ -62,6 +62,11 @@ static_assert(WAVES_PER_WG * RING * 256 < 49152, "ring depth vs the LDS overflow
 #ifndef BPE_LOAD_AUX
 #define BPE_LOAD_AUX 2
 #endif
+// Merge detection of the streaming pass: 0 packed (slot, neighbour) words (v_perm + compare per
+// plane), 1 compares into wave masks (slot == a, slot == b) combined on the scalar unit
+#ifndef BPE_APPLY_MASKS
+#define BPE_APPLY_MASKS 0
+#endif
 
 // f(integral_constant<I>) for I = 0 .. N-1, unrolled in the source (the ring's slot indices must be
 // compile-time constants, or the ring is moved to scratch memory)
@@ -178,7 +183,10 @@ struct LoopCtl {
     int32_t vote;
     // sharded: the single candidate chosen before the vote (tie == 3)
     int32_t pend_a, pend_b;
-    int32_t pad_;
+    // LOOP_ERROR: 1 the replacement count (sum) != W, 2 a tie pass found no occurrence
+    int32_t err;
+    // (err 1: the count found and the W expected)
+    unsigned long long err_got, err_want;
 };
 
 // Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
@@ -265,6 +273,13 @@ __device__ __forceinline__ void cold_add(const ColdTable &ct, uint32_t key, unsi
         h = (h + 1) & ct.mask;
     }
     atomicOr(ct.overflow, 1u);
+}
+
+// Claimed dense entries to scan: a claim past the capacity bumps n_used before it sees the
+// overflow, so n_used alone can point past the dense arrays.
+__device__ __forceinline__ uint32_t cold_used(const ColdTable &ct) {
+    const uint32_t n = *ct.n_used;
+    return n <= ct.mask ? n : ct.mask + 1;
 }
 
 // entries per thread and sweep of the cold-table scans (their loads in flight together)
@@ -1155,6 +1170,27 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
         return;
     }
 #endif
+#if BPE_APPLY_MASKS
+    // The common case, no (a, b) in the chunk: eight compares into wave masks (slot == a, slot ==
+    // b), the matches M[e] = A[e] & B[e + 1] on the scalar unit (dead slots and tail tags are
+    // negative: never a or b), the last live slot's pair (last, nxt) as a scalar test.
+    const unsigned long long A0 = __ballot(w.t[0] == ma), A1 = __ballot(w.t[1] == ma),
+                             A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
+    const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
+                             B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
+    {
+        const unsigned long long H = (A0 & B1) | (A1 & B2) | (A2 & B3) | (A3 & (B0 >> 1));
+        const uint32_t m_l = ((uint32_t)(w.last ^ ma) | (uint32_t)(nxt ^ mb)) == 0u;
+        unsigned long long T = H | (unsigned long long)(m_l | (uint32_t)ap.match);
+        if (MERGE == MERGE_XX) T |= (unsigned long long)(uint32_t)(w.last == ma);
+        if (T == 0ull) {
+            ap.prev = w.last;
+            ap.par = 0;
+            ap.match = 0;
+            return;
+        }
+    }
+#else
     // The common case, no (a, b) in the chunk: four packed (slot, right neighbour) compares.  In a
     // partial chunk lane 63's slot 3 (dead) stands in for the last live slot, paired with nxt.
     // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)
@@ -1180,6 +1216,7 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
                              A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
     const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
                              B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
+#endif
     unsigned long long M0 = A0 & B1, M1 = A1 & B2, M2 = A2 & B3, M3 = A3 & (B0 >> 1);
     // the last live slot's neighbour is nxt
     int m_last = ((uint32_t)(w.last ^ ma) | (uint32_t)(nxt ^ mb)) == 0u;
@@ -1751,7 +1788,7 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
     __shared__ unsigned long long s_best[4];
     __shared__ unsigned s_live;
     if (loop_off(ctl)) return;
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = cold_used(ct);
     if (blockIdx.x == 0 && threadIdx.x == 0)   // (rides along with the Result's copy to the host)
         res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n;
     if (threadIdx.x == 0) s_live = 0;
@@ -1791,6 +1828,127 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
         if (best) atomicMax(&res->best, best);
         if (s_live) atomicAdd(&res->cold_dead, (unsigned long long)s_live);
     }
+}
+
+// The maintained state's selection in one launch (the single-corpus device loop; was k_argmax_hot
+// + k_argmax_cold + k_collect): the best key over the hot bins and the cold table's dense entries,
+// and every pair holding it.  Each thread keeps its best key, its first entry holding it and how
+// many of its entries hold it; each block its best and the entries holding it (a rescan only by
+// the threads with several); a global atomicMax settles the best, and the last block to finish
+// (a ticket) gathers the entries of the blocks whose best is the global one.  Also the cold
+// table's flags and its dead claims (count 0, key set), as k_argmax_cold.  res->best and
+// res->n_cand are zero on entry (k_decide / k_tie_fused clear them).
+constexpr int SEL_MAX = MAX_CAND + 1;   // (more than MAX_CAND candidates: the host path)
+struct BlockBest {
+    unsigned long long key;
+    uint32_t n;
+    uint32_t pad_;
+    int2 cand[SEL_MAX];
+};
+
+__global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *__restrict__ hot,
+                                                      ColdTable ct, const int32_t *__restrict__ len16,
+                                                      int64_t max_length, Result *res, int2 *cand,
+                                                      BlockBest *rec, unsigned int *ticket,
+                                                      const LoopCtl *ctl) {
+    __shared__ unsigned long long s_best[4];
+    __shared__ unsigned s_dead, s_n;
+    __shared__ int2 s_c[SEL_MAX];
+    __shared__ bool s_last;
+    if (loop_off(ctl)) return;
+    const uint32_t n_cold = cold_used(ct);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    if (tid == 0) res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n_cold;
+    if (threadIdx.x == 0) s_dead = s_n = 0;
+    // this thread's elements: hot bins tid, tid + stride, ... then cold entries likewise
+    unsigned long long best = 0;
+    int2 first = make_int2(-1, -1);
+    uint32_t cnt = 0;
+    unsigned dead = 0;
+    auto see = [&](unsigned long long k, int32_t a, int32_t b) {
+        if (k > best) {
+            best = k;
+            first = make_int2(a, b);
+            cnt = 1;
+        } else if (k && k == best) {
+            ++cnt;
+        }
+    };
+    for (uint32_t bin = tid; bin < (uint32_t)HOT_BINS; bin += stride) {
+        const int32_t a = bin_a(bin), b = bin_b(bin);
+        if (pair_ok(a, b, len16, max_length)) see(pack_key(hot[bin], a, b), a, b);
+    }
+    for (uint32_t i0 = tid; i0 < n_cold; i0 += COLD_ILP * stride) {
+        unsigned long long v[COLD_ILP];
+        uint32_t kk[COLD_ILP];
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            const uint32_t i = i0 + q * stride;
+            v[q] = i < n_cold ? ct.dcounts[i] : 0ull;
+            kk[q] = i < n_cold ? ct.dkeys[i] : EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < COLD_ILP; ++q) {
+            dead += (v[q] == 0) & (kk[q] != EMPTY);
+            const int32_t a = (int32_t)(kk[q] >> 16), b = (int32_t)(kk[q] & 0xFFFFu);
+            if (v[q] && pair_ok(a, b, len16, max_length)) see(pack_key(v[q], a, b), a, b);
+        }
+    }
+    unsigned long long bb = wave_max_u64(best);
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = bb;
+    if (dead) atomicAdd(&s_dead, dead);
+    __syncthreads();
+    bb = max(max(s_best[0], s_best[1]), max(s_best[2], s_best[3]));
+    if (bb && best == bb) {
+        if (cnt == 1) {
+            const unsigned k = atomicAdd(&s_n, 1u);
+            if (k < SEL_MAX) s_c[k] = first;
+        } else {
+            // (rare: several entries of this thread hold the block's best) the thread's elements again
+            for (uint32_t bin = tid; bin < (uint32_t)HOT_BINS; bin += stride) {
+                const int32_t a = bin_a(bin), b = bin_b(bin);
+                if (pair_ok(a, b, len16, max_length) && pack_key(hot[bin], a, b) == bb) {
+                    const unsigned k = atomicAdd(&s_n, 1u);
+                    if (k < SEL_MAX) s_c[k] = make_int2(a, b);
+                }
+            }
+            for (uint32_t i = tid; i < n_cold; i += stride) {
+                const unsigned long long v = ct.dcounts[i];
+                const uint32_t kk = ct.dkeys[i];
+                const int32_t a = (int32_t)(kk >> 16), b = (int32_t)(kk & 0xFFFFu);
+                if (v && pair_ok(a, b, len16, max_length) && pack_key(v, a, b) == bb) {
+                    const unsigned k = atomicAdd(&s_n, 1u);
+                    if (k < SEL_MAX) s_c[k] = make_int2(a, b);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        BlockBest &r = rec[blockIdx.x];
+        r.key = bb;
+        r.n = s_n;
+        for (unsigned k = 0; k < min(s_n, (unsigned)SEL_MAX); ++k) r.cand[k] = s_c[k];
+        if (bb) atomicMax(&res->best, bb);
+        if (s_dead) atomicAdd(&res->cold_dead, (unsigned long long)s_dead);
+        __threadfence();
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    *ticket = 0;
+    const unsigned long long g = __hip_atomic_load(&res->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned total = 0;
+    if (g)
+        for (unsigned q = 0; q < gridDim.x; ++q) {
+            const BlockBest &r = rec[q];
+            if (r.key != g) continue;
+            for (unsigned k = 0; k < min(r.n, (unsigned)SEL_MAX) && total + k < (unsigned)SEL_MAX; ++k)
+                cand[total + k] = r.cand[k];
+            total += r.n;
+        }
+    res->n_cand = total;
 }
 
 // One workgroup: best hot key (wave + LDS max), the hot pairs sharing it, and the heavy sketch
@@ -1891,160 +2049,88 @@ __global__ void __launch_bounds__(256) k_select_multi(const unsigned long long *
 // 4 no merge, 5 the host path) and votes: the reasons above that depend on this rank's copy of the
 // maintained tables (fill, dead claims, room) differ between ranks, so they ride in the tie
 // all-reduce(MAX) (tie_pos[MAX_CAND]) and phase 1 decides on every rank alike.
-__global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
-                         long long *log, int phase, const unsigned long long *__restrict__ tie_pos,
-                         const unsigned long long *__restrict__ hdr = nullptr) {
-    if (threadIdx.x != 0) return;
-    // Snapshots of the control block and the Result (their loads issue together: one memory
-    // latency instead of a chain of dependent ones); the fields are written back one by one.
-    const LoopCtl C = *ctl;
-    const Result R = *res;
-    const int2 cand0 = cand[0];
-    if (C.status != LOOP_RUN) return;
+// ---- the decision's parts (k_decide, and k_tie_fused's last block) ----
+// Room in the maintained table for the refresh of the merge: every pair the merge creates has
+// the new token c as a side, and c occurs W times, so it claims at most 2 W new slots.
+__device__ __forceinline__ bool decide_room(const LoopCtl &C, const Result &R) {
+    if (!C.maintained) return true;
+    const long long W = (long long)(R.best >> 17);
+    const unsigned long long V = (unsigned long long)C.next_id + 1;
+    const unsigned long long claims = 2 * (unsigned long long)W < V * V ? 2 * W : V * V;
+    return (R.cold_flags & 0xFFFFFFFFull) + claims + 64 <= C.cold_cap / 4 * 3;
+}
+
+// Phase 0's proposal from the snapshots: 4 no merge (LOOP_DONE), 5 the host path, 1 / 2 a tie
+// pass over the corpus tail window / the whole corpus, 3 one candidate.  *vote: this corpus's
+// own reasons for the host path (a sharded rank votes; one corpus proposes 5).  Sorts
+// cand[0 .. n) by (a, b) when tied (the same order on every rank).
+__device__ int decide_propose(const LoopCtl &C, const Result &R, int2 *cand, int &vote) {
     const unsigned long long best = R.best;
     const long long W = (long long)(best >> 17);
     const unsigned n = R.n_cand;
-    int32_t a = -1, b = -1;
-    auto to_host = [&]() {
-        ctl->status = LOOP_HOST;
-        ctl->n_host = C.n_host + 1;
-    };
-    // room in the maintained table for the refresh of the merge: every pair the merge creates
-    // has the new token c as a side, and c occurs W times, so it claims at most 2 W new slots
-    auto room = [&]() -> bool {
-        if (!C.maintained) return true;
-        const unsigned long long V = (unsigned long long)C.next_id + 1;
-        const unsigned long long claims = 2 * (unsigned long long)W < V * V ? 2 * W : V * V;
-        return (R.cold_flags & 0xFFFFFFFFull) + claims + 64 <= C.cold_cap / 4 * 3;
-    };
-    if (phase == 0) {
-        if (C.w >= 0) {
-            // the previous merge's replacement count: == W on the whole corpus (sharded: summed
-            // over the ranks in the exchange header); this corpus's own count is logged
-            const unsigned long long total = C.sharded && hdr ? hdr[0] : R.replaced;
-            if ((C.sharded && !hdr) || total != (unsigned long long)C.w) {
-                ctl->status = LOOP_ERROR;
-                return;
-            }
-            // (a sharded batch may open on the last batch's last merge: not in this log)
-            if (C.n_done > 0) log[LOG_WORDS * (C.n_done - 1) + 3] = (long long)R.replaced;
-        }
-        ctl->w = -1;
-        int vote = 0;
-        if (C.maintained) {
-            const unsigned long long used = R.cold_flags & 0xFFFFFFFFull;
-            if ((R.cold_flags >> 32) || used * 4 > C.cold_cap * 3 ||
-                2 * R.cold_dead > used + 65536)
-                vote = 1;
-        }
-        if (!room()) vote = 1;
-        // the proposal: LOOP_DONE (4), the host path (5), a tie pass (1, 2) or one candidate (3)
-        int prop;
-        if (vote && !C.sharded) {
-            prop = 5;
-        } else if (!C.maintained && R.n_heavy) {
-            // a heavy sketch bucket may hold a cold pair above the best hot one (even when no
-            // hot pair exists at all): only the host path's exact counts can tell
-            prop = 5;
-        } else if (best == 0 || W < C.min_weight) {                  // core.ts:312-313
-            prop = 4;
-        } else if (n == 0 || n > (unsigned)MAX_CAND || C.next_id >= C.max_id) {
-            prop = 5;
-        } else if (n > 1) {
-            // the same candidate order on every rank (the collection order is not): by (a, b)
-            for (unsigned j = 1; j < n; ++j) {
-                const int2 v = cand[j];
-                unsigned i = j;
-                for (; i > 0 && (cand[i - 1].x > v.x || (cand[i - 1].x == v.x && cand[i - 1].y > v.y)); --i)
-                    cand[i] = cand[i - 1];
-                cand[i] = v;
-            }
-            // X Y candidates only: the corpus tail window first (a sharded corpus's tail is the
-            // last rank's); else the full pass
-            int all_xy = 1;
-            for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
-            for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
-            ctl->n_tie = C.n_tie + 1;
-            prop = all_xy ? 1 : 2;
-        } else {
-            prop = 3;
-        }
-        if (!C.sharded) {
-            if (prop == 4) {
-                ctl->status = LOOP_DONE;
-                return;
-            }
-            if (prop == 5) {
-                to_host();
-                return;
-            }
-            if (prop != 3) {
-                ctl->tie = prop;
-                return;
-            }
-            a = cand0.x;
-            b = cand0.y;
-        } else {
-            ctl->tie = prop;
-            ctl->vote = vote;
-            ctl->pend_a = cand0.x;
-            ctl->pend_b = cand0.y;
-            return;
-        }
-    } else {
-        if (!C.tie) return;
-        if (C.sharded) {
-            ctl->tie = 0;
-            if (tie_pos[MAX_CAND] || C.tie == 5) {   // some rank voted for the host path
-                to_host();
-                return;
-            }
-            if (C.tie == 4) {
-                ctl->status = LOOP_DONE;
-                return;
-            }
-        }
-        if (C.tie == 3) {
-            a = C.pend_a;
-            b = C.pend_b;
-        } else {
-            unsigned long long bp = ~0ull;
-            unsigned missing = 0;
-            for (unsigned j = 0; j < n; ++j) {
-                const unsigned long long p = tie_pos ? tie_pos[j] : R.last[j];
-                if (p && p < bp) {
-                    bp = p;
-                    a = cand[j].x;
-                    b = cand[j].y;
-                }
-                missing += p == 0;
-            }
-            if (C.tie == 1 && missing) {
-                if (missing > 1) {
-                    // two or more occur only before the tail window: the host path's full pass
-                    to_host();
-                    return;
-                }
-                // the only one missing occurs only earlier: its last occurrence is the earliest
-                for (unsigned j = 0; j < n; ++j)
-                    if ((tie_pos ? tie_pos[j] : R.last[j]) == 0) {
-                        a = cand[j].x;
-                        b = cand[j].y;
-                    }
-                ctl->n_lone = C.n_lone + 1;
-            }
-            if (C.tie == 1) ctl->n_tail = C.n_tail + 1;
-            if (a < 0) {
-                ctl->status = LOOP_ERROR;
-                return;
-            }
-            if (!C.sharded && !room()) {
-                to_host();
-                return;
-            }
-        }
-        ctl->tie = 0;
+    vote = 0;
+    if (C.maintained) {
+        const unsigned long long used = R.cold_flags & 0xFFFFFFFFull;
+        if ((R.cold_flags >> 32) || used * 4 > C.cold_cap * 3 || 2 * R.cold_dead > used + 65536)
+            vote = 1;
     }
+    if (!decide_room(C, R)) vote = 1;
+    if (vote && !C.sharded) return 5;
+    // a heavy sketch bucket may hold a cold pair above the best hot one (even when no hot pair
+    // exists at all): only the host path's exact counts can tell
+    if (!C.maintained && R.n_heavy) return 5;
+    if (best == 0 || W < C.min_weight) return 4;                     // core.ts:312-313
+    if (n == 0 || n > (unsigned)MAX_CAND || C.next_id >= C.max_id) return 5;
+    if (n == 1) return 3;
+    for (unsigned j = 1; j < n; ++j) {
+        const int2 v = cand[j];
+        unsigned i = j;
+        for (; i > 0 && (cand[i - 1].x > v.x || (cand[i - 1].x == v.x && cand[i - 1].y > v.y)); --i)
+            cand[i] = cand[i - 1];
+        cand[i] = v;
+    }
+    // X Y candidates only: the corpus tail window first (a sharded corpus's tail is the last
+    // rank's); else the full pass
+    int all_xy = 1;
+    for (unsigned j = 0; j < n; ++j) all_xy &= cand[j].x != cand[j].y;
+    return all_xy ? 1 : 2;
+}
+
+// Rule R3 from the last positions (0: none): the candidate whose last counted occurrence comes
+// first.  Tail window (tie == 1): one candidate missing there occurs only earlier, so it wins;
+// two or more missing need the host path's full pass.  Returns 0 (a, b set), 1 (host), 2 (no
+// occurrence at all: an error).
+__device__ int decide_r3(int tie, unsigned n, const unsigned long long *pos, const int2 *cand,
+                         int32_t &a, int32_t &b, int &lone) {
+    unsigned long long bp = ~0ull;
+    unsigned missing = 0;
+    a = b = -1;
+    lone = 0;
+    for (unsigned j = 0; j < n; ++j) {
+        const unsigned long long p = pos[j];
+        if (p && p < bp) {
+            bp = p;
+            a = cand[j].x;
+            b = cand[j].y;
+        }
+        missing += p == 0;
+    }
+    if (tie == 1 && missing) {
+        if (missing > 1) return 1;
+        for (unsigned j = 0; j < n; ++j)
+            if (pos[j] == 0) {
+                a = cand[j].x;
+                b = cand[j].y;
+            }
+        lone = 1;
+    }
+    return a < 0 ? 2 : 0;
+}
+
+// The decision's writes: the log entry (a, b, W), the new token's UTF-16 length (core.ts:318),
+// the merge the next pass applies, and a Result cleared for the next selection.
+__device__ void decide_commit(LoopCtl *ctl, Result *res, const LoopCtl &C, long long W, int32_t a,
+                              int32_t b, int32_t *len16, long long *log) {
     const int32_t c = C.next_id;
     len16[c] = len16[a] + len16[b];
     const long long i = C.n_done;
@@ -2065,6 +2151,112 @@ __global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int
     res->cold_dead = 0;
 }
 
+// Phase 0's check of the previous merge's replacement count: == W on the whole corpus (sharded:
+// summed over the ranks in the exchange header); this corpus's own count is logged.
+__device__ bool decide_check_replaced(LoopCtl *ctl, const LoopCtl &C, const Result &R,
+                                      const unsigned long long *hdr, long long *log) {
+    if (C.w < 0) return true;
+    const unsigned long long total = C.sharded && hdr ? hdr[0] : R.replaced;
+    if ((C.sharded && !hdr) || total != (unsigned long long)C.w) {
+        ctl->status = LOOP_ERROR;
+        ctl->err = 1;
+        ctl->err_got = total;
+        ctl->err_want = (unsigned long long)C.w;
+        return false;
+    }
+    // (a sharded batch may open on the last batch's last merge: not in this log)
+    if (C.n_done > 0) log[LOG_WORDS * (C.n_done - 1) + 3] = (long long)R.replaced;
+    return true;
+}
+
+__global__ void k_decide(LoopCtl *ctl, Result *res, int2 *__restrict__ cand, int32_t *len16,
+                         long long *log, int phase, const unsigned long long *__restrict__ tie_pos,
+                         const unsigned long long *__restrict__ hdr = nullptr) {
+    if (threadIdx.x != 0) return;
+    // Snapshots of the control block and the Result (their loads issue together: one memory
+    // latency instead of a chain of dependent ones); the fields are written back one by one.
+    const LoopCtl C = *ctl;
+    const Result R = *res;
+    if (C.status != LOOP_RUN) return;
+    const long long W = (long long)(R.best >> 17);
+    const unsigned n = R.n_cand;
+    auto to_host = [&]() {
+        ctl->status = LOOP_HOST;
+        ctl->n_host = C.n_host + 1;
+    };
+    int32_t a = -1, b = -1;
+    if (phase == 0) {
+        if (!decide_check_replaced(ctl, C, R, hdr, log)) return;
+        ctl->w = -1;
+        int vote = 0;
+        const int prop = decide_propose(C, R, cand, vote);
+        if (prop == 1 || prop == 2) {
+            for (int j = 0; j < MAX_CAND; ++j) res->last[j] = 0;
+            ctl->n_tie = C.n_tie + 1;
+        }
+        if (C.sharded) {
+            ctl->tie = prop;
+            ctl->vote = vote;
+            ctl->pend_a = cand[0].x;
+            ctl->pend_b = cand[0].y;
+            return;
+        }
+        if (prop == 4) {
+            ctl->status = LOOP_DONE;
+            return;
+        }
+        if (prop == 5) {
+            to_host();
+            return;
+        }
+        if (prop != 3) {
+            ctl->tie = prop;
+            return;
+        }
+        a = cand[0].x;
+        b = cand[0].y;
+    } else {
+        if (!C.tie) return;
+        if (C.sharded) {
+            ctl->tie = 0;
+            if (tie_pos[MAX_CAND] || C.tie == 5) {   // some rank voted for the host path
+                to_host();
+                return;
+            }
+            if (C.tie == 4) {
+                ctl->status = LOOP_DONE;
+                return;
+            }
+        }
+        if (C.tie == 3) {
+            a = C.pend_a;
+            b = C.pend_b;
+        } else {
+            unsigned long long pos[MAX_CAND];
+            for (unsigned j = 0; j < n && j < (unsigned)MAX_CAND; ++j) pos[j] = tie_pos ? tie_pos[j] : R.last[j];
+            int lone = 0;
+            const int r3 = decide_r3(C.tie, n, pos, cand, a, b, lone);
+            if (r3 == 1) {
+                to_host();
+                return;
+            }
+            if (lone) ctl->n_lone = C.n_lone + 1;
+            if (C.tie == 1) ctl->n_tail = C.n_tail + 1;
+            if (r3 == 2) {
+                ctl->status = LOOP_ERROR;
+                ctl->err = 2;
+                return;
+            }
+            if (!C.sharded && !decide_room(C, R)) {
+                to_host();
+                return;
+            }
+        }
+        ctl->tie = 0;
+    }
+    decide_commit(ctl, res, C, W, a, b, len16, log);
+}
+
 __device__ __forceinline__ void push_cand(Result *res, int2 *cand, int32_t a, int32_t b) {
     const unsigned int i = atomicAdd(&res->n_cand, 1u);
     if (i < CAND_CAP) cand[i] = make_int2(a, b);
@@ -2083,7 +2275,7 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
         if (pair_ok(a, b, len16, max_length) && pack_key(hot_counts[tid], a, b) == best)
             push_cand(res, cand, a, b);
     }
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = cold_used(ct);
     const unsigned long long w = best >> 17;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i0 = tid; i0 < n; i0 += COLD_ILP * stride) {
@@ -2106,7 +2298,7 @@ __global__ void k_collect(const unsigned long long *__restrict__ hot_counts, Col
 
 // ---- sharded selection over caller-provided (global) tables ----------------------------------
 __global__ void k_export_cold(ColdTable ct, uint32_t *keys, unsigned long long *counts) {
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = cold_used(ct);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         keys[i] = ct.dkeys[i];
         counts[i] = ct.dcounts[i];   // (a hole exports count 0)
@@ -2160,7 +2352,7 @@ __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b, const Loop
         a = ctl->a;
         b = ctl->b;
     }
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = cold_used(ct);
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += COLD_ILP * stride) {
         uint32_t kk[COLD_ILP];   // (loads issued together, as in k_argmax_cold)
@@ -2193,7 +2385,7 @@ __global__ void k_incr_invalidate(ColdTable ct, unsigned long long *__restrict__
         const int32_t m = (t >> 8) & 1 ? b : a, o = t & 255;
         if (m < HOT) hot[(t >> 9) ? hot_bin((uint32_t)m, (uint32_t)o) : hot_bin((uint32_t)o, (uint32_t)m)] = 0;
     }
-    const uint32_t n = *ct.n_used;
+    const uint32_t n = cold_used(ct);
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i0 = t; i0 < n; i0 += COLD_ILP * stride) {
         uint32_t kk[COLD_ILP];
@@ -2440,19 +2632,11 @@ __device__ __forceinline__ void tie_chunk(const Chunk &w, int32_t nxt, int c, in
 // not found there occurs only earlier, so it wins if it is the only one missing (k_decide).
 constexpr int TIE_TAIL_PER_WAVE = 2;
 
-__global__ void __launch_bounds__(256) k_tie(TieArgs A) {
+// One wave's share of the tie pass: n candidates cand[0 .. n) (any memory), over the corpus tail
+// window (tail) or the wave's region; the last positions go to A.res->last[j] (atomicMax).
+__device__ __forceinline__ void tie_body(const TieArgs &A, int n, int tail, const int2 *cand) {
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    int n = A.n_cand;
-    int tail = 0;
-    if (A.ctl) {
-        const int tie = A.ctl->tie;
-        if (A.ctl->status != LOOP_RUN || (tie != 1 && tie != 2)) return;
-        n = (int)A.res->n_cand;
-        tail = tie == 1;
-        // (a sharded corpus's tail window lies on the last rank: the others find nothing there)
-        if (tail && A.ctl->sharded && !A.ctl->last_rank) return;
-    }
     TieState ts;
     ts.n = min(n, MAX_CAND);
     ts.xx = 0;
@@ -2460,7 +2644,7 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
     for (int j = 0; j < MAX_CAND; ++j) {
         ts.pos[j] = 0;
         // unused slots get a key no chunk word has (slot values >= 0xFF01 in both halves)
-        const int2 cj = j < ts.n ? A.cand[j] : make_int2(-1, -1);
+        const int2 cj = j < ts.n ? cand[j] : make_int2(-1, -1);
         ts.key[j] = __builtin_amdgcn_readfirstlane(pack_pair_s(cj.x, cj.y));
         ts.xx |= (uint32_t)((j < ts.n) & (cj.x == cj.y)) << j;
     }
@@ -2554,6 +2738,94 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
             if (j < ts.n && ts.pos[j])
                 atomicMax(&A.res->last[j], (unsigned long long)(c0 * CHUNK + ts.pos[j]));
     }
+}
+
+__global__ void __launch_bounds__(256) k_tie(TieArgs A) {
+    int n = A.n_cand;
+    int tail = 0;
+    if (A.ctl) {
+        const int tie = A.ctl->tie;
+        if (A.ctl->status != LOOP_RUN || (tie != 1 && tie != 2)) return;
+        n = (int)A.res->n_cand;
+        tail = tie == 1;
+        // (a sharded corpus's tail window lies on the last rank: the others find nothing there)
+        if (tail && A.ctl->sharded && !A.ctl->last_rank) return;
+    }
+    tie_body(A, n, tail, A.cand);
+}
+
+// The single-corpus device loop's selection tail in one launch (k_decide phase 0, k_tie, k_decide
+// phase 1): every block takes the same proposal from the same snapshot of the control block, the
+// Result and the candidates (nothing writes them during the launch); with a tie the blocks scan
+// for rule R3; the last block to finish (a ticket) commits the decision, with the positions every
+// block left.  `ticket` is zero between launches.
+__global__ void __launch_bounds__(256) k_tie_fused(TieArgs A, int32_t *len16, long long *log,
+                                                   unsigned int *ticket) {
+    __shared__ LoopCtl sC;
+    __shared__ Result sR;
+    __shared__ int2 sc[MAX_CAND];
+    __shared__ int s_prop;
+    __shared__ bool s_last;
+    if (threadIdx.x == 0) {
+        sC = *A.ctl;
+        sR = *A.res;
+        const unsigned n = min(sR.n_cand, (unsigned)MAX_CAND);
+        for (unsigned j = 0; j < n; ++j) sc[j] = A.cand[j];
+        int vote = 0;
+        s_prop = sC.status == LOOP_RUN ? decide_propose(sC, sR, sc, vote) : 0;
+    }
+    __syncthreads();
+    const int prop = s_prop;
+    if (prop == 0) return;   // (the batch has ended: every block, no ticket)
+    if (prop == 1 || prop == 2) tie_body(A, (int)sR.n_cand, prop == 1, sc);
+    // (every wave's position atomics complete at agent scope before the block takes its ticket)
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    *ticket = 0;
+    const LoopCtl &C = sC;
+    const Result &R = sR;
+    LoopCtl *ctl = const_cast<LoopCtl *>(A.ctl);
+    Result *res = A.res;
+    if (!decide_check_replaced(ctl, C, R, nullptr, log)) return;
+    ctl->w = -1;
+    if (prop == 4) {
+        ctl->status = LOOP_DONE;
+        return;
+    }
+    if (prop == 5) {
+        ctl->status = LOOP_HOST;
+        ctl->n_host = C.n_host + 1;
+        return;
+    }
+    int32_t a = sc[0].x, b = sc[0].y;
+    if (prop != 3) {
+        const unsigned n = R.n_cand;
+        unsigned long long pos[MAX_CAND];
+        for (unsigned j = 0; j < n; ++j) {
+            pos[j] = __hip_atomic_load(&res->last[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            res->last[j] = 0;   // (for the next tie)
+        }
+        ctl->n_tie = C.n_tie + 1;
+        int lone = 0;
+        const int r3 = decide_r3(prop, n, pos, sc, a, b, lone);
+        if (r3 == 1) {
+            ctl->status = LOOP_HOST;
+            ctl->n_host = C.n_host + 1;
+            return;
+        }
+        if (lone) ctl->n_lone = C.n_lone + 1;
+        if (prop == 1) ctl->n_tail = C.n_tail + 1;
+        if (r3 == 2) {
+            ctl->status = LOOP_ERROR;
+            ctl->err = 2;
+            return;
+        }
+    }
+    decide_commit(ctl, res, C, (long long)(R.best >> 17), a, b, len16, log);
 }
 
 // Sharded loop: this shard's last tie positions as corpus-wide ones (rank << 40 | position; 0:

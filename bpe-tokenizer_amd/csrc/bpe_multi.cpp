@@ -25,6 +25,8 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -129,6 +131,12 @@ int all_reduce(bpe_multi *m, std::vector<unsigned long long *> &buf, size_t coun
         MHIP(hipSetDevice(m->dev[r]));
         MHIP(hipMemcpyAsync(m->h_buf, buf[r], count * 8, hipMemcpyDeviceToHost, m->st[r]));
         MHIP(hipStreamSynchronize(m->st[r]));
+        static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
+        if (dbg && !max)
+            for (size_t i = 0; i < count; ++i)
+                if (m->h_buf[i] >> 32)
+                    fprintf(stderr, "[bpe debug] all-reduce: shard %d word %zu (other %lld row %lld) = %llu = 0x%llx\n",
+                            r, i, (long long)((i - 8) / 6), (long long)((i - 8) % 6), m->h_buf[i], m->h_buf[i]);
         if (r == 0) {
             std::memcpy(m->h_sum, m->h_buf, count * 8);
         } else if (max) {
@@ -222,6 +230,11 @@ int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
             hipMalloc((void **)&m->d_table[r], BPE_TABLE_BINS * 8) != hipSuccess ||
             hipMalloc((void **)&m->d_xchg[r], BPE_XCHG_WORDS * 8) != hipSuccess ||
             hipMalloc((void **)&m->d_tie[r], BPE_TIE_WORDS * 8) != hipSuccess)
+            return bail(bpe_fail(BPE_ERR_OOM, "bpe native: multi-device buffers"));
+        // the rank loop owes the caller nothing about these buffers' contents (bpe.h): a poison
+        // pattern makes any reliance on zeroed memory fail the same way on every run
+        if (hipMemset(m->d_xchg[r], 0xA5, BPE_XCHG_WORDS * 8) != hipSuccess ||
+            hipMemset(m->d_tie[r], 0xA5, BPE_TIE_WORDS * 8) != hipSuccess)
             return bail(bpe_fail(BPE_ERR_OOM, "bpe native: multi-device buffers"));
     }
     if (hipHostMalloc((void **)&m->h_buf, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess ||
@@ -563,6 +576,8 @@ int multi_apply_merges(bpe_multi *m, const int32_t *abc, int64_t n, int64_t *rep
     return BPE_OK;
 }
 
+int debug_compare_global(bpe_multi *m, int64_t merges_so_far);
+
 // The maintained state over the shards: the global table (all-reduced) and every shard's exact
 // cold-pair list, gathered through the host, loaded into every shard (bpe_set_global_counts).
 int enter_maintained(bpe_multi *m) {
@@ -600,6 +615,66 @@ int enter_maintained(bpe_multi *m) {
     }
     m->maintained = true;
     m->heavy_streak = 0;
+    static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
+    if (dbg) MTRY(debug_compare_global(m, -1));
+    return BPE_OK;
+}
+
+extern "C" int bpe_debug_tables(bpe_ctx *c, uint64_t *hot, uint32_t *keys, uint64_t *counts,
+                                int64_t cap, int64_t *n);
+
+// (debug: BPE_DEBUG_GLOBAL=1) every shard's copy of the global tables must be the same: the hot
+// bins, and the cold pairs with a count (holes and dead claims aside)
+int debug_compare_global(bpe_multi *m, int64_t merges_so_far) {
+    std::vector<uint64_t> hot0(BPE_HOT_BINS), hot(BPE_HOT_BINS);
+    std::map<uint32_t, uint64_t> cold0;
+    for (int r = 0; r < m->n; ++r) {
+        int64_t nu = 0;
+        MTRY(bpe_debug_tables(m->sh[r], hot.data(), nullptr, nullptr, 0, &nu));
+        std::vector<uint32_t> k(nu);
+        std::vector<uint64_t> v(nu);
+        MTRY(bpe_debug_tables(m->sh[r], hot.data(), k.data(), v.data(), nu, &nu));
+        std::map<uint32_t, uint64_t> cold;
+        for (int64_t i = 0; i < nu; ++i)
+            if (v[i] && k[i] != 0xFFFFFFFFu) cold[k[i]] += v[i];
+        if (r == 0) {
+            hot0 = hot;
+            cold0 = cold;
+            continue;
+        }
+        for (int b = 0; b < BPE_HOT_BINS; ++b)
+            if (hot[b] != hot0[b]) {
+                fprintf(stderr, "[bpe debug] after %lld merges: shard %d hot bin (%d, %d) = %llu, shard 0: %llu\n",
+                        (long long)merges_so_far, r, b & 255, b >> 8, (unsigned long long)hot[b],
+                        (unsigned long long)hot0[b]);
+                return bpe_fail(BPE_ERR_STATE, "bpe debug: global hot tables differ");
+            }
+        if (cold != cold0) {
+            for (auto &kv : cold0)
+                if (cold[kv.first] != kv.second) {
+                    fprintf(stderr, "[bpe debug] after %lld merges: shard %d cold (%u, %u) = %llu, shard 0: %llu\n",
+                            (long long)merges_so_far, r, kv.first >> 16, kv.first & 0xFFFF,
+                            (unsigned long long)cold[kv.first], (unsigned long long)kv.second);
+                    break;
+                }
+            return bpe_fail(BPE_ERR_STATE, "bpe debug: global cold tables differ");
+        }
+    }
+    // no count may exceed the corpus (a count of 2^32 and more here is garbage)
+    for (int b = 0; b < BPE_HOT_BINS; ++b)
+        if (hot0[b] >> 32) {
+            fprintf(stderr, "[bpe debug] after %lld merges: hot bin (%d, %d) = %llu\n", (long long)merges_so_far,
+                    b & 255, b >> 8, (unsigned long long)hot0[b]);
+            return bpe_fail(BPE_ERR_STATE, "bpe debug: garbage hot count");
+        }
+    for (auto &kv : cold0)
+        if (kv.second >> 32) {
+            fprintf(stderr, "[bpe debug] after %lld merges: cold (%u, %u) = %llu\n", (long long)merges_so_far,
+                    kv.first >> 16, kv.first & 0xFFFF, (unsigned long long)kv.second);
+            return bpe_fail(BPE_ERR_STATE, "bpe debug: garbage cold count");
+        }
+    fprintf(stderr, "[bpe debug] after %lld merges: %d shards agree (%zu cold pairs)\n",
+            (long long)merges_so_far, m->n, cold0.size());
     return BPE_OK;
 }
 
@@ -665,10 +740,14 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                 if (tot != log[0][4 * i + 2]) return bpe_fail(BPE_ERR_STATE, "bpe native: replacement count != W");
                 put((int32_t)log[0][4 * i], (int32_t)log[0][4 * i + 1], log[0][4 * i + 2]);
             }
+            static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
+            if (dbg && batch_maintained && status == 0) MTRY(debug_compare_global(m, n));
             if (status != 0) m->maintained = false;   // (the shards left the global state)
             if (status == 1) break;                                        // no pair qualifies
             if (status == 0) {
                 batch = std::min<int64_t>(BPE_LOOP_BATCH, 2 * batch);
+                static const int dbg_batch = getenv("BPE_DEBUG_BATCH") ? atoi(getenv("BPE_DEBUG_BATCH")) : 0;
+                if (dbg_batch > 0 && m->maintained) batch = std::min<int64_t>(batch, dbg_batch);
                 continue;
             }
             batch = std::max<int64_t>(1, std::min<int64_t>(BPE_LOOP_BATCH, 2 * nd));

@@ -207,7 +207,8 @@ class ShardedTrainer:
             return cls(eng, rank, world, dist, nt, bytes_per_rank)
         # global first-appearance order (core.ts:186-199) across the shards, in corpus order
         import torch
-        first = first_appearance(data, alphabet)
+        # (the zipf generator's bytes are not the uniform stream's alphabet: look for all 256)
+        first = first_appearance(data, 256 if corpus == 'zipf' else alphabet)
         big = np.iinfo(np.int64).max
         key = np.where(first >= 0, (np.int64(rank) << RANK_SHIFT) + first, big)
         t = torch.tensor(key, dtype=torch.int64, device=torch.device('cuda', device))
@@ -307,8 +308,9 @@ class ShardedTrainer:
         eng = self.engine
         if self._rl is None:
             dev = self.shard.device
-            self._rl = (torch.zeros(pkg.XCHG_WORDS, dtype=torch.int64, device=dev),
-                        torch.zeros(pkg.TIE_WORDS, dtype=torch.int64, device=dev),
+            # (poisoned: the rank loop must not rely on the buffers' contents, include/bpe.h)
+            self._rl = (torch.full((pkg.XCHG_WORDS,), -0x5A5A5A5A5A5A5A5B, dtype=torch.int64, device=dev),
+                        torch.full((pkg.TIE_WORDS,), -0x5A5A5A5A5A5A5A5B, dtype=torch.int64, device=dev),
                         torch.cuda.ExternalStream(eng.stream(), device=dev))
         xchg, tie, stream = self._rl
         gloo, all_reduce = self._collectives()

@@ -272,6 +272,7 @@ typedef struct {
     int64_t pix_builds;       /* incremental mode: position-index builds (one sort of the corpus) */
     int64_t pix_merges;       /* incremental mode: merges made on the index (O(W) each) */
     int64_t pix_host;         /* incremental mode: iterations the index handed to the stream */
+    double pix_build_ms;      /* incremental mode: wall time of those builds (host clock, synced) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -167,7 +167,7 @@ def test_rccl_exchange_over_two_devices():
     assert two.merge_until(0, 2, 300) == one.merge_until(0, 2, 300)
 
 
-@pytest.mark.parametrize('shards,mib,n,max_length', [(3, 6, 900, 0), (4, 4, 600, 5)])
+@pytest.mark.parametrize('shards,mib,n,max_length', [(3, 6, 900, 0), (4, 4, 600, 5), (2, 8, 700, 0)])
 def test_maintained_state_over_shards_on_zipf_words(shards, mib, n, max_length):
     """A skewed corpus over several shards: the cold pairs outgrow the sketch, the shards move to
     the maintained state (global tables on every shard, delta rows exchanged per merge) and stay

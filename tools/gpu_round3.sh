@@ -20,8 +20,10 @@ if has smoke; then
   cat "$OUT/smoke.log"
 fi
 if has driver; then
-  /usr/bin/time -v timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver.jsonl" 2> "$OUT/driver.err"
-  cat "$OUT/driver.jsonl"; grep "Elapsed" "$OUT/driver.err"
+  t0=$(date +%s.%N)
+  timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver.jsonl" 2> "$OUT/driver.err"
+  t1=$(date +%s.%N)
+  cat "$OUT/driver.jsonl"; echo "driver wall: $(python3 -c "print('%.1f s' % ($t1 - $t0))")" | tee "$OUT/driver.wall"
 fi
 if has bench; then
   timeout -k 10 600 python3 bench.py --incremental > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
