@@ -282,6 +282,8 @@ int sync_len16(bpe_ctx *c, int64_t max_length) {
 // grid of the scans over the cold table's dense view (>= HOT_BINS / 256 for k_collect)
 constexpr int COLD_GRID = 1024;
 static_assert(COLD_GRID * 256 >= HOT_BINS, "k_collect covers the hot bins");
+static_assert(COLD_GRID <= TK_GROUP * TK_MAX_GROUPS && (MAX_REGIONS + 3) / 4 <= TK_GROUP * TK_MAX_GROUPS,
+              "grid_last's counters cover k_select_maint's and k_tie_fused's grids");
 
 // Empties the cold table: free slots, zero dense counts (the invariant past n_used), n_used = 0.
 int cold_clear(bpe_ctx *c) {
@@ -2021,9 +2023,9 @@ int bpe_create(bpe_ctx **out, int device) {
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if ((rc = dev_alloc(&c->d_ctl, 1))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_ticket, 1))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_ticket, TICKET_WORDS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_brec, COLD_GRID))) return bail(rc);
-    if (hipMemset(c->d_ticket, 0, sizeof(unsigned int)) != hipSuccess)
+    if (hipMemset(c->d_ticket, 0, TICKET_WORDS * sizeof(unsigned int)) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
     if ((rc = dev_alloc(&c->d_repl, REPLAY_BATCH))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_repl, REPLAY_BATCH * sizeof(unsigned long long),

@@ -1830,6 +1830,27 @@ __global__ void k_argmax_cold(ColdTable ct, const int32_t *__restrict__ len16, i
     }
 }
 
+// Last-block detection over a whole grid.  Thread 0 of each block calls it after its block's
+// writes and a __threadfence; it returns true in the one block that finishes last.  Same-address
+// atomics are serialised by the memory side (a device-wide ticket of 1024 blocks took ~60 us), so
+// blocks count in groups of TK_GROUP, one counter per group on its own 128-byte line, and only
+// each group's last block takes the top ticket.  Counters are zero between launches (each last
+// block resets the counter it completed).
+constexpr int TK_STRIDE = 32, TK_GROUP = 32, TK_MAX_GROUPS = 64;
+constexpr int TICKET_WORDS = TK_STRIDE * (1 + TK_MAX_GROUPS);
+__device__ bool grid_last(unsigned int *ticket) {
+    const unsigned G = gridDim.x, g = blockIdx.x / TK_GROUP;
+    const unsigned ng = (G + TK_GROUP - 1) / TK_GROUP;
+    const unsigned size = min((unsigned)TK_GROUP, G - g * TK_GROUP);
+    unsigned int *gc = ticket + TK_STRIDE * (1 + g);
+    if (atomicAdd(gc, 1u) != size - 1) return false;
+    *gc = 0;
+    __threadfence();
+    if (atomicAdd(ticket, 1u) != ng - 1) return false;
+    *ticket = 0;
+    return true;
+}
+
 // The maintained state's selection in one launch (the single-corpus device loop; was k_argmax_hot
 // + k_argmax_cold + k_collect): the best key over the hot bins and the cold table's dense entries,
 // and every pair holding it.  Each thread keeps its best key, its first entry holding it and how
@@ -1842,7 +1863,7 @@ constexpr int SEL_MAX = MAX_CAND + 1;   // (more than MAX_CAND candidates: the h
 struct BlockBest {
     unsigned long long key;
     uint32_t n;
-    uint32_t pad_;
+    uint32_t dead;   // the block's dead claims
     int2 cand[SEL_MAX];
 };
 
@@ -1928,27 +1949,46 @@ __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *
         BlockBest &r = rec[blockIdx.x];
         r.key = bb;
         r.n = s_n;
+        r.dead = s_dead;
         for (unsigned k = 0; k < min(s_n, (unsigned)SEL_MAX); ++k) r.cand[k] = s_c[k];
-        if (bb) atomicMax(&res->best, bb);
-        if (s_dead) atomicAdd(&res->cold_dead, (unsigned long long)s_dead);
         __threadfence();
-        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        s_last = grid_last(ticket);
     }
     __syncthreads();
-    if (!s_last || threadIdx.x != 0) return;
+    if (!s_last) return;
     __threadfence();
-    *ticket = 0;
-    const unsigned long long g = __hip_atomic_load(&res->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned total = 0;
+    // the last block: the global best, the dead claims and the candidates from every block's
+    // record, read by all its threads (one thread alone waited on ~1000 dependent loads)
+    unsigned long long g = 0, dsum = 0;
+    for (unsigned q = threadIdx.x; q < gridDim.x; q += blockDim.x) {
+        g = max(g, rec[q].key);
+        dsum += rec[q].dead;
+    }
+    g = wave_max_u64(g);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dsum += __shfl_xor(dsum, d);
+    __shared__ unsigned long long s_dsum[4];
+    if ((threadIdx.x & 63) == 0) {
+        s_best[threadIdx.x >> 6] = g;
+        s_dsum[threadIdx.x >> 6] = dsum;
+    }
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    g = max(max(s_best[0], s_best[1]), max(s_best[2], s_best[3]));
     if (g)
-        for (unsigned q = 0; q < gridDim.x; ++q) {
+        for (unsigned q = threadIdx.x; q < gridDim.x; q += blockDim.x) {
             const BlockBest &r = rec[q];
             if (r.key != g) continue;
-            for (unsigned k = 0; k < min(r.n, (unsigned)SEL_MAX) && total + k < (unsigned)SEL_MAX; ++k)
-                cand[total + k] = r.cand[k];
-            total += r.n;
+            const unsigned k0 = atomicAdd(&s_n, r.n);
+            for (unsigned k = 0; k < min(r.n, (unsigned)SEL_MAX) && k0 + k < (unsigned)SEL_MAX; ++k)
+                cand[k0 + k] = r.cand[k];
         }
-    res->n_cand = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        res->best = g;
+        res->n_cand = s_n;
+        res->cold_dead = s_dsum[0] + s_dsum[1] + s_dsum[2] + s_dsum[3];
+    }
 }
 
 // One workgroup: best hot key (wave + LDS max), the hot pairs sharing it, and the heavy sketch
@@ -2755,39 +2795,15 @@ __global__ void __launch_bounds__(256) k_tie(TieArgs A) {
 }
 
 // The single-corpus device loop's selection tail in one launch (k_decide phase 0, k_tie, k_decide
-// phase 1): every block takes the same proposal from the same snapshot of the control block, the
-// Result and the candidates (nothing writes them during the launch); with a tie the blocks scan
-// for rule R3; the last block to finish (a ticket) commits the decision, with the positions every
-// block left.  `ticket` is zero between launches.
-__global__ void __launch_bounds__(256) k_tie_fused(TieArgs A, int32_t *len16, long long *log,
-                                                   unsigned int *ticket) {
-    __shared__ LoopCtl sC;
-    __shared__ Result sR;
-    __shared__ int2 sc[MAX_CAND];
-    __shared__ int s_prop;
-    __shared__ bool s_last;
-    if (threadIdx.x == 0) {
-        sC = *A.ctl;
-        sR = *A.res;
-        const unsigned n = min(sR.n_cand, (unsigned)MAX_CAND);
-        for (unsigned j = 0; j < n; ++j) sc[j] = A.cand[j];
-        int vote = 0;
-        s_prop = sC.status == LOOP_RUN ? decide_propose(sC, sR, sc, vote) : 0;
-    }
-    __syncthreads();
-    const int prop = s_prop;
-    if (prop == 0) return;   // (the batch has ended: every block, no ticket)
-    if (prop == 1 || prop == 2) tie_body(A, (int)sR.n_cand, prop == 1, sc);
-    // (every wave's position atomics complete at agent scope before the block takes its ticket)
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last || threadIdx.x != 0) return;
-    __threadfence();
-    *ticket = 0;
-    const LoopCtl &C = sC;
-    const Result &R = sR;
+// phase 1).  Without a tie, block 0 decides alone and the other blocks return at once: a
+// device-wide ticket costs one same-address atomic per block, which the memory side serialises
+// (1024 of them took 62 us, an iteration's whole selection budget).  With a tie (2 to MAX_CAND
+// candidates and an R3 proposal), every block takes the same proposal from the same snapshot of
+// the control block, the Result and the candidates (nothing writes them until every block has
+// taken its ticket), scans for rule R3, and the last block to finish (the ticket) commits the
+// decision with the positions every block left.  `ticket` is zero between launches.
+__device__ void fused_commit(const TieArgs &A, const LoopCtl &C, const Result &R, const int2 *sc,
+                             int prop, int32_t *len16, long long *log) {
     LoopCtl *ctl = const_cast<LoopCtl *>(A.ctl);
     Result *res = A.res;
     if (!decide_check_replaced(ctl, C, R, nullptr, log)) return;
@@ -2826,6 +2842,48 @@ __global__ void __launch_bounds__(256) k_tie_fused(TieArgs A, int32_t *len16, lo
         }
     }
     decide_commit(ctl, res, C, (long long)(R.best >> 17), a, b, len16, log);
+}
+
+__global__ void __launch_bounds__(256) k_tie_fused(TieArgs A, int32_t *len16, long long *log,
+                                                   unsigned int *ticket) {
+    __shared__ LoopCtl sC;
+    __shared__ Result sR;
+    __shared__ int2 sc[MAX_CAND];
+    __shared__ int s_prop;
+    __shared__ bool s_last;
+    if (threadIdx.x == 0) {
+        int prop = 0;
+        // (blocks other than 0 look further only when a tie pass is possible; a late block that
+        // finds block 0's decision already made returns here too: the status or n_cand changed)
+        const unsigned nc = blockIdx.x ? __hip_atomic_load(&A.res->n_cand, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 2u;
+        if (nc >= 2 && nc <= (unsigned)MAX_CAND) {
+            sC = *A.ctl;
+            sR = *A.res;
+            const unsigned n = min(sR.n_cand, (unsigned)MAX_CAND);
+            for (unsigned j = 0; j < n; ++j) sc[j] = A.cand[j];
+            int vote = 0;
+            prop = sC.status == LOOP_RUN ? decide_propose(sC, sR, sc, vote) : 0;
+            if (blockIdx.x && prop != 1 && prop != 2) prop = 0;
+        }
+        s_prop = prop;
+    }
+    __syncthreads();
+    const int prop = s_prop;
+    if (prop == 0) return;   // (the batch has ended, or block 0 decides alone)
+    if (prop != 1 && prop != 2) {
+        if (threadIdx.x == 0) fused_commit(A, sC, sR, sc, prop, len16, log);   // (block 0 only)
+        return;
+    }
+    tie_body(A, (int)sR.n_cand, prop == 1, sc);
+    // (every wave's position atomics complete at agent scope before the block takes its ticket)
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = grid_last(ticket);
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    fused_commit(A, sC, sR, sc, prop, len16, log);
 }
 
 // Sharded loop: this shard's last tie positions as corpus-wide ones (rank << 40 | position; 0:

@@ -48,7 +48,8 @@ def main():
     out = {'corpus_mib': mib, 'merges': len(g1), 'incremental_s': t1,
            'incremental_ms_per_merge': 1e3 * t1 / max(1, len(g1)),
            'incremental_equiv_pair_scans_per_s': s1 / t1,
-           'first_call_5_merges_s': st1['first_call_s'], 'pix_builds': st1['pix_builds'], 'pix_host': st1['pix_host'], 'pix_merges': st1['pix_merges']}
+           'first_call_5_merges_s': st1['first_call_s'], 'pix_builds': st1['pix_builds'], 'pix_build_ms': st1['pix_build_ms'],
+           'pix_host': st1['pix_host'], 'pix_merges': st1['pix_merges']}
     if '--no-stream' not in sys.argv:
         g2, t2, s2, i2, st2 = run(data, 'stream', merges)
         out.update({'stream_s': t2, 'stream_ms_per_merge': 1e3 * t2 / max(1, len(g2)),
