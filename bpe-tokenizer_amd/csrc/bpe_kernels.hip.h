@@ -56,6 +56,14 @@ static_assert(RING >= 5, "ring depth");
 // (the overflow screen runs once per ring round: 16 waves x RING chunks x 256 adds must stay
 // below the 49152 adds of headroom above 0x4000, see lds_sweep)
 static_assert(WAVES_PER_WG * RING * 256 < 49152, "ring depth vs the LDS overflow screen");
+// How far ahead k_step loads: chunk c + LEAD at stage c, into the slot of chunk c + LEAD - RING.
+// At stage c the wave holds chunks c - 1 (count), c (apply) and c + 1 (its first token), so every
+// slot of a chunk <= c - 2 is free: LEAD <= RING - 2.
+#ifndef BPE_LEAD
+#define BPE_LEAD (BPE_RING - 3)
+#endif
+constexpr int LEAD = BPE_LEAD;
+static_assert(LEAD >= 2 && LEAD <= RING - 2, "load lead");
 // Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
 // pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
 // this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
@@ -1417,7 +1425,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         };
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
                          Defer &df) __attribute__((always_inline)) {
-            load(fre, c + RING - 3);
+            load(fre, c + LEAD);
             if (c < nc) {
                 finish_load(cur);
             } else {
@@ -1438,7 +1446,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         };
         if (nc > 0) {
             Chunk S[RING];   // (constant indices only: the ring stays in registers)
-            static_for<0, RING - 3>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
+            static_for<0, LEAD>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
             S[RING - 1].len = 0;
             if (MERGE) {
                 // does the token before the region match the region's first live token?
@@ -1453,7 +1461,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
                     constexpr int i = decltype(I)::value;
                     stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
-                          S[(i + RING - 3) % RING], c + i, D[i]);
+                          S[(i + LEAD) % RING], c + i, D[i]);
                 });
                 screen_round();
             }
