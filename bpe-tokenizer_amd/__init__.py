@@ -66,7 +66,8 @@ class Stats(ctypes.Structure):
         ('tie_lone', ctypes.c_int64), ('loop_host', ctypes.c_int64),
         ('fused_passes', ctypes.c_int64), ('pix_builds', ctypes.c_int64),
         ('pix_merges', ctypes.c_int64), ('pix_host', ctypes.c_int64),
-        ('pix_build_ms', ctypes.c_double),
+        ('pix_build_ms', ctypes.c_double), ('cold_used', ctypes.c_int64),
+        ('sel_blocks', ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -100,7 +100,8 @@ struct bpe_ctx {
     Result *d_res = nullptr, *h_res = nullptr;
     int2 *d_cand = nullptr;
     ColdTable cold{};
-    uint32_t *d_cold_flags = nullptr;   // [0] n_used, [1] overflow
+    // [0] n_used, [1] overflow, [2] n_blist, [3] sel_n0, [4] dead, [5] n_recomputed (ColdTable)
+    uint32_t *d_cold_flags = nullptr;
     uint64_t cold_cap = 0;
     // an applied merge whose replacement count is still on the device (settled at the next sync)
     bool pending = false;
@@ -290,7 +291,9 @@ int cold_clear(bpe_ctx *c) {
     c->cold_list = false;
     HIP_TRY(hipMemsetAsync(c->cold.slots, 0xFF, c->cold_cap * sizeof(unsigned long long), c->stream));
     HIP_TRY(hipMemsetAsync(c->cold.dcounts, 0, c->cold_cap * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, 2 * sizeof(uint32_t), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_cold_flags, 0, 5 * sizeof(uint32_t), c->stream));
+    // (the block maxima: no block flagged; the next selection of a batch is a full scan)
+    HIP_TRY(hipMemsetAsync(c->cold.bdirty, 0, (c->cold_cap / CB + 1) * sizeof(uint32_t), c->stream));
     c->cold_used = 0;
     return BPE_OK;
 }
@@ -310,10 +313,16 @@ int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     dfree(c->cold.slots);
     dfree(c->cold.dkeys);
     dfree(c->cold.dcounts);
+    dfree(c->cold.bmax);
+    dfree(c->cold.bdirty);
+    dfree(c->cold.blist);
     int rc;
     if ((rc = dev_alloc(&c->cold.slots, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.dkeys, cap))) return rc;
     if ((rc = dev_alloc(&c->cold.dcounts, cap))) return rc;
+    if ((rc = dev_alloc(&c->cold.bmax, cap / CB + 1))) return rc;
+    if ((rc = dev_alloc(&c->cold.bdirty, cap / CB + 1))) return rc;
+    if ((rc = dev_alloc(&c->cold.blist, cap / CB + 1))) return rc;
     c->cold_cap = cap;
     c->cold.mask = (uint32_t)(cap - 1);
     int lg = 0;
@@ -321,6 +330,10 @@ int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     c->cold.shift = 32 - lg;
     c->cold.n_used = c->d_cold_flags;
     c->cold.overflow = c->d_cold_flags + 1;
+    c->cold.n_blist = c->d_cold_flags + 2;
+    c->cold.sel_n0 = c->d_cold_flags + 3;
+    c->cold.dead = c->d_cold_flags + 4;
+    c->cold.n_recomputed = c->d_cold_flags + 5;
     c->counts_valid = false;
     c->cold_exact = false;
     return cold_clear(c);
@@ -876,6 +889,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     c->opt_max_length = max_length;
     const bool maint = c->cold_exact && c->counts_valid && c->carry_valid &&
                        !getenv("BPE_DEBUG_NO_FUSED");
+    // (A/B and checking knob: every maintained selection a full scan of the cold table)
+    static const bool sel_full = getenv("BPE_SEL_FULL") != nullptr;
     if (!maint) c->cold_exact = false;
     if (!maint && (!table_ok(c) || !c->carry_valid))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
@@ -927,9 +942,13 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         hipEvent_t e_sel = span_begin(c);
         if (maint) {
             // best key over the hot bins and the cold table, its pairs, the table's flags
-            k_select_maint<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, max_length,
-                                                     c->d_res, c->d_cand, c->d_brec, c->d_ticket,
-                                                     c->d_ctl);
+            // a full scan of the cold table on the first selection of the batch and every
+            // SEL_FULL_EVERY-th (its dead claims), else the block maxima on a grid of one
+            // workgroup per 256 hot bins
+            const bool full = !c->use_incr || sel_full || i % SEL_FULL_EVERY == 0;
+            k_select_maint<<<full ? COLD_GRID : HOT_BINS / 256, 256, 0, s>>>(
+                c->d_hot, c->cold, c->d_len16, max_length, c->d_res, c->d_cand, c->d_brec,
+                c->d_ticket, c->d_ctl, full ? 1 : 0);
         } else {
             k_select_multi<<<TABLE_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, max_length,
                                                             c->d_res, c->d_cand, c->d_heavy,
@@ -941,7 +960,8 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
         if (maint && c->use_incr) {
-            k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl);
+            k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl,
+                                                        c->d_len16, max_length);
             k_step_loop<MODE_INCR><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
                                                        c->d_carry, c->d_ctl, c->d_partials,
                                                        c->d_spill, c->cold, c->d_sums,
@@ -1025,6 +1045,12 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     c->len16_lo = base + nd;   // k_decide wrote the new lengths on the device
     if (maint) {
         c->cold_used = c->h_res->cold_flags & 0xFFFFFFFFu;   // (as of the last selection)
+        if (c->stats_on) {
+            c->stats.cold_used = std::max<int64_t>(c->stats.cold_used, (int64_t)c->cold_used);
+            uint32_t nr = 0;
+            HIP_TRY(hipMemcpy(&nr, c->cold.n_recomputed, sizeof nr, hipMemcpyDeviceToHost));
+            c->stats.sel_blocks = nr;   // (cumulative since the context was made)
+        }
         if (nd) c->sketch_valid = false;                     // (fused passes)
         if (c->stats_on) c->stats.fused_passes += nd;
     }
@@ -1706,6 +1732,15 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
     if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
     HIP_TRY(hipHostMalloc((void **)&P->h_ctl, sizeof(PixCtl), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void **)&P->h_log, 3 * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
+    // the hot passes' scratch: per workgroup and half a slab of 32768 counts (then offsets), the
+    // hot pairs' totals, slots and uncounted (x, x) occurrences
+    Scratch hs;
+    const int G = (int)std::min<uint32_t>(PH_WG_MAX, nblk);
+    uint32_t *slab, *htot, *hslot;
+    unsigned long long *oddxx;
+    if ((rc = hs.get(&slab, (size_t)2 * G * PH_HALF)) || (rc = hs.get(&htot, 65536)) ||
+        (rc = hs.get(&hslot, 65536)) || (rc = hs.get(&oddxx, 256)))
+        return rc;
     // the pair table: room for the current pairs and the ones merges will add
     uint64_t cap = 1u << 20;
     while (cap < (uint64_t)N / 8) cap <<= 1;
@@ -1730,6 +1765,7 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         HIP_TRY(hipMemsetAsync(T.len, 0, cap * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(T.bdirty, 0, T.nblocks * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(T.sbdirty, 0, T.nsuper * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(oddxx, 0, 256 * sizeof(unsigned long long), s));
         PixCtl *h = P->h_ctl;
         memset(h, 0, sizeof *h);
         h->status = PIX_RUN;
@@ -1739,7 +1775,10 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         h->pool_cap = pool_cap;
         h->used_cap = cap / 10 * 7;
         HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
-        k_pix_build_count<<<4096, 256, 0, s>>>(C, T, P->d_ctl, carry);
+        for (int half = 0; half < 2; ++half)
+            k_pix_hot_count<<<G, PH_T, 0, s>>>(C, T, P->d_ctl, carry, half, slab, oddxx);
+        k_pix_hot_scan<<<2 * PH_HALF / 256, 256, 0, s>>>(slab, G, htot);
+        k_pix_hot_claim<<<65536 / 256, 256, 0, s>>>(T, P->d_ctl, htot, oddxx, hslot);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -1754,7 +1793,9 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         if (attempt == 3) return PIX_NOT_ELIGIBLE;
     }
     k_pix_build_alloc<<<4096, 256, 0, s>>>(T, P->d_ctl, (uint32_t)cap);
-    k_pix_build_fill<<<4096, 256, 0, s>>>(C, T, B);
+    for (int half = 0; half < 2; ++half)
+        k_pix_hot_fill<<<G, PH_T, 0, s>>>(C, T, B, half, slab, hslot);
+    HIP_TRY(hipGetLastError());
     // per-merge buffers
     B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
     B.ent_cap = 2 * B.site_cap + 16;
@@ -2017,7 +2058,7 @@ int bpe_create(bpe_ctx **out, int device) {
     if ((rc = dev_alloc(&c->d_outoff, MAX_REGIONS))) return bail(rc);
     if ((rc = dev_alloc(&c->d_res, 1))) return bail(rc);
     if ((rc = dev_alloc(&c->d_cand, CAND_CAP))) return bail(rc);
-    if ((rc = dev_alloc(&c->d_cold_flags, 4))) return bail(rc);
+    if ((rc = dev_alloc(&c->d_cold_flags, 8))) return bail(rc);
     if (hipHostMalloc((void **)&c->h_cand, MAX_CAND * sizeof(int2), hipHostMallocDefault) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
     if (hipHostMalloc((void **)&c->h_res, sizeof(Result), hipHostMallocDefault) != hipSuccess)
@@ -2036,7 +2077,7 @@ int bpe_create(bpe_ctx **out, int device) {
         hipHostMalloc((void **)&c->h_log, LOG_WORDS * LOOP_BATCH * sizeof(long long), hipHostMallocDefault) !=
             hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: hipHostMalloc failed"));
-    if (hipMemset(c->d_cold_flags, 0, 16) != hipSuccess)
+    if (hipMemset(c->d_cold_flags, 0, 32) != hipSuccess)
         return bail(fail(BPE_ERR_HIP, "bpe native: memset failed"));
     if ((rc = ensure_chunks(c, 1))) return bail(rc);
     if ((rc = ensure_vocab(c, 0))) return bail(rc);
@@ -2078,6 +2119,7 @@ int bpe_destroy(bpe_ctx *c) {
     void *ptrs[] = {c->d_ids, c->d_tmp, c->d_len16, c->d_partials, c->d_spill, c->d_hot,
                     c->d_total, c->d_sums, c->d_carry, c->d_outoff, c->d_res, c->d_cand,
                     c->d_heavy, c->d_cold_flags, c->cold.slots, c->cold.dkeys, c->cold.dcounts,
+                    c->cold.bmax, c->cold.bdirty, c->cold.blist,
                     c->d_ctl, c->d_log, c->d_repl, c->d_ticket, c->d_brec};
     for (void *p : ptrs) dfree(p);
     if (c->h_res) (void)hipHostFree(c->h_res);

@@ -146,7 +146,18 @@ struct ColdTable {
     uint32_t *overflow;  // set when a probe sequence wraps the table or the dense arrays fill up
     uint32_t mask;       // slots - 1 (= dense capacity - 1)
     uint32_t shift;
+    // Block maxima of the dense view (the device loop's maintained selection, k_select_maint):
+    // per CB entries the best packed key, exact except in the blocks flagged dirty (listed in
+    // blist, n_blist entries); sel_n0 = n_used at the last selection, dead = the dead claims
+    // found by the last full scan.  n_blist, sel_n0 and dead follow n_used and overflow in the
+    // same flags array.
+    unsigned long long *bmax;
+    uint32_t *bdirty, *blist;
+    uint32_t *n_blist, *sel_n0, *dead;
+    uint32_t *n_recomputed;   // block maxima recomputed by incremental selections (a statistic)
 };
+// entries per block of the cold table's block maxima
+constexpr uint32_t CB = 1024;
 
 struct Result {
     unsigned long long best;             // packed (W << 17) | (0x1FFFF - c_index), 0 = none
@@ -1861,13 +1872,27 @@ __device__ bool grid_last(unsigned int *ticket) {
 
 // The maintained state's selection in one launch (the single-corpus device loop; was k_argmax_hot
 // + k_argmax_cold + k_collect): the best key over the hot bins and the cold table's dense entries,
-// and every pair holding it.  Each thread keeps its best key, its first entry holding it and how
-// many of its entries hold it; each block its best and the entries holding it (a rescan only by
-// the threads with several); a global atomicMax settles the best, and the last block to finish
-// (a ticket) gathers the entries of the blocks whose best is the global one.  Also the cold
-// table's flags and its dead claims (count 0, key set), as k_argmax_cold.  res->best and
-// res->n_cand are zero on entry (k_decide / k_tie_fused clear them).
+// and every pair holding it.  res->best and res->n_cand are zero on entry (k_decide / k_tie_fused
+// clear them).  Two forms, the same for every block of the launch:
+//  - full (full_req: the first selection of a batch, every SEL_FULL_EVERY-th, and always in
+//    MODE_FUSED; launched on the full grid): every dense entry.  Workgroup w takes the CB-entry blocks w, w + G, ...; each
+//    thread keeps its best key, its first entry holding it and how many of its entries hold it;
+//    each workgroup its best and the entries holding it (a rescan only by the threads with
+//    several).  Every block's max is written (ct.bmax), the dirty flags cleared, and the dead
+//    claims (count 0, key set) counted: they decide when the table is rebuilt.
+//  - incremental: a merge (a, b) -> c changes only the pairs with a side in {a, b, c}.  Those with
+//    a or b were zeroed (k_incr_invalidate flagged the blocks whose max they may have been) and
+//    recounted to at most their old count; those with c are new claims, at the end of the dense
+//    view.  So only the flagged blocks and the blocks of claims made since the last selection are
+//    recomputed; the other blocks' maxima are still exact.  The hot bins are scanned in full.
+//    (Launched on HOT_BINS / 256 workgroups: zipf C3 recomputes ~24 of ~7700 blocks per merge,
+//    so the grid's tickets and the last workgroup's record scan were most of the cost.)
+// A ticket picks the last workgroup, which settles the global best from the workgroups' records
+// (and, incremental, from the block maxima: the entries of the blocks holding it are the cold
+// candidates).  The dead-claim count of the last full scan stands for the incremental ones.
 constexpr int SEL_MAX = MAX_CAND + 1;   // (more than MAX_CAND candidates: the host path)
+constexpr int SEL_FULL_EVERY = 16;
+constexpr uint32_t SEL_MAX_BLOCKS = 1u << 16;   // (more blocks: always the full scan)
 struct BlockBest {
     unsigned long long key;
     uint32_t n;
@@ -1875,29 +1900,63 @@ struct BlockBest {
     int2 cand[SEL_MAX];
 };
 
+__device__ __forceinline__ unsigned long long cold_entry_key(const ColdTable &ct, uint32_t i,
+                                                             uint32_t n, const int32_t *len16,
+                                                             int64_t max_length, int2 &ab,
+                                                             unsigned &dead) {
+    if (i >= n) return 0;
+    const unsigned long long v = ct.dcounts[i];
+    const uint32_t kk = ct.dkeys[i];
+    dead += (v == 0) & (kk != EMPTY);
+    ab = make_int2((int32_t)(kk >> 16), (int32_t)(kk & 0xFFFFu));
+    return v && pair_ok(ab.x, ab.y, len16, max_length) ? pack_key(v, ab.x, ab.y) : 0ull;
+}
+
+// max over a 256-thread workgroup (s: 4 words of LDS); every thread gets it
+__device__ __forceinline__ unsigned long long wg_max_u64(unsigned long long v, unsigned long long *s) {
+    v = wave_max_u64(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return max(max(s[0], s[1]), max(s[2], s[3]));
+}
+
 __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *__restrict__ hot,
                                                       ColdTable ct, const int32_t *__restrict__ len16,
                                                       int64_t max_length, Result *res, int2 *cand,
                                                       BlockBest *rec, unsigned int *ticket,
-                                                      const LoopCtl *ctl) {
-    __shared__ unsigned long long s_best[4];
+                                                      const LoopCtl *ctl, int full_req) {
+    __shared__ unsigned long long s_best[4], s_red[4];
     __shared__ unsigned s_dead, s_n;
     __shared__ int2 s_c[SEL_MAX];
     __shared__ bool s_last;
+    __shared__ int s_full;
+    __shared__ uint32_t s_nl, s_b0, s_b1, s_ncb;
+    __shared__ uint32_t s_cb[64];
     if (loop_off(ctl)) return;
     const uint32_t n_cold = cold_used(ct);
+    const uint32_t nblk = (n_cold + CB - 1) / CB;
+    if (threadIdx.x == 0) {
+        // (read once and broadcast: every branch around a barrier below is uniform)
+        const uint32_t n0 = *ct.sel_n0;
+        s_full = full_req || nblk > SEL_MAX_BLOCKS || n0 > n_cold;
+        s_nl = min(*ct.n_blist, ct.mask / CB + 1);
+        s_b0 = n0 / CB;              // blocks holding claims made since the last selection
+        s_b1 = nblk;
+        s_dead = s_n = 0;
+    }
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     if (tid == 0) res->cold_flags = ((unsigned long long)*ct.overflow << 32) | n_cold;
-    if (threadIdx.x == 0) s_dead = s_n = 0;
-    // this thread's elements: hot bins tid, tid + stride, ... then cold entries likewise
+    __syncthreads();
+    const bool full = s_full;
     unsigned long long best = 0;
     int2 first = make_int2(-1, -1);
     uint32_t cnt = 0;
     unsigned dead = 0;
-    auto see = [&](unsigned long long k, int32_t a, int32_t b) {
+    auto see = [&](unsigned long long k, int2 ab) {
         if (k > best) {
             best = k;
-            first = make_int2(a, b);
+            first = ab;
             cnt = 1;
         } else if (k && k == best) {
             ++cnt;
@@ -1905,25 +1964,40 @@ __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *
     };
     for (uint32_t bin = tid; bin < (uint32_t)HOT_BINS; bin += stride) {
         const int32_t a = bin_a(bin), b = bin_b(bin);
-        if (pair_ok(a, b, len16, max_length)) see(pack_key(hot[bin], a, b), a, b);
+        if (pair_ok(a, b, len16, max_length)) see(pack_key(hot[bin], a, b), make_int2(a, b));
     }
-    for (uint32_t i0 = tid; i0 < n_cold; i0 += COLD_ILP * stride) {
-        unsigned long long v[COLD_ILP];
-        uint32_t kk[COLD_ILP];
+    // one CB-entry block: every thread its 4 entries (coalesced); the block's max to ct.bmax
+    auto block = [&](uint32_t blk, bool keep) {
+        unsigned long long m = 0;
 #pragma unroll
-        for (int q = 0; q < COLD_ILP; ++q) {
-            const uint32_t i = i0 + q * stride;
-            v[q] = i < n_cold ? ct.dcounts[i] : 0ull;
-            kk[q] = i < n_cold ? ct.dkeys[i] : EMPTY;
+        for (int q = 0; q < (int)(CB / 256); ++q) {
+            int2 ab;
+            const unsigned long long k =
+                cold_entry_key(ct, blk * CB + threadIdx.x + 256 * q, n_cold, len16, max_length, ab, dead);
+            if (keep) see(k, ab);
+            m = max(m, k);
         }
-#pragma unroll
-        for (int q = 0; q < COLD_ILP; ++q) {
-            dead += (v[q] == 0) & (kk[q] != EMPTY);
-            const int32_t a = (int32_t)(kk[q] >> 16), b = (int32_t)(kk[q] & 0xFFFFu);
-            if (v[q] && pair_ok(a, b, len16, max_length)) see(pack_key(v[q], a, b), a, b);
+        m = wg_max_u64(m, s_red);
+        if (threadIdx.x == 0) {
+            ct.bmax[blk] = m;
+            ct.bdirty[blk] = 0;
         }
+    };
+    if (full) {
+        for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) block(blk, true);
+    } else {
+        // the flagged blocks, then the blocks of the new claims
+        const uint32_t nl = s_nl, nn = s_b1 - min(s_b0, s_b1);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ct.n_recomputed, nl + nn);
+        for (uint32_t j = blockIdx.x; j < nl + nn; j += gridDim.x) {
+            // (blist holds blocks of entries below n_used: always < nblk, so every thread of
+            // the workgroup calls block() with the same blk)
+            block(j < nl ? ct.blist[j] : s_b0 + (j - nl), false);
+        }
+        dead = 0;
     }
     unsigned long long bb = wave_max_u64(best);
+    __syncthreads();
     if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = bb;
     if (dead) atomicAdd(&s_dead, dead);
     __syncthreads();
@@ -1941,15 +2015,17 @@ __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *
                     if (k < SEL_MAX) s_c[k] = make_int2(a, b);
                 }
             }
-            for (uint32_t i = tid; i < n_cold; i += stride) {
-                const unsigned long long v = ct.dcounts[i];
-                const uint32_t kk = ct.dkeys[i];
-                const int32_t a = (int32_t)(kk >> 16), b = (int32_t)(kk & 0xFFFFu);
-                if (v && pair_ok(a, b, len16, max_length) && pack_key(v, a, b) == bb) {
-                    const unsigned k = atomicAdd(&s_n, 1u);
-                    if (k < SEL_MAX) s_c[k] = make_int2(a, b);
-                }
-            }
+            if (full)
+                for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+                    for (int q = 0; q < (int)(CB / 256); ++q) {
+                        int2 ab;
+                        unsigned dd = 0;
+                        if (cold_entry_key(ct, blk * CB + threadIdx.x + 256 * q, n_cold, len16,
+                                           max_length, ab, dd) == bb) {
+                            const unsigned k = atomicAdd(&s_n, 1u);
+                            if (k < SEL_MAX) s_c[k] = ab;
+                        }
+                    }
         }
     }
     __syncthreads();
@@ -1972,17 +2048,36 @@ __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *
         g = max(g, rec[q].key);
         dsum += rec[q].dead;
     }
-    g = wave_max_u64(g);
+    // incremental: the best block max; per thread its best, its first block holding it and how
+    // many (16 loads in flight per thread: one at a time left this scan latency-bound)
+    unsigned long long gc = 0;
+    uint32_t gfirst = 0, gcnt = 0;
+    if (!full)
+        for (uint32_t b0 = threadIdx.x; b0 < nblk; b0 += 16 * 256) {
+            unsigned long long v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = b0 + 256 * q < nblk ? ct.bmax[b0 + 256 * q] : 0ull;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                if (v[q] > gc) {
+                    gc = v[q];
+                    gfirst = b0 + 256 * q;
+                    gcnt = 1;
+                } else if (v[q] && v[q] == gc) {
+                    ++gcnt;
+                }
+            }
+        }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) dsum += __shfl_xor(dsum, d);
     __shared__ unsigned long long s_dsum[4];
-    if ((threadIdx.x & 63) == 0) {
-        s_best[threadIdx.x >> 6] = g;
-        s_dsum[threadIdx.x >> 6] = dsum;
+    if ((threadIdx.x & 63) == 0) s_dsum[threadIdx.x >> 6] = dsum;
+    g = wg_max_u64(max(g, gc), s_best);
+    if (threadIdx.x == 0) {
+        s_n = 0;
+        s_ncb = 0;
     }
-    if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    g = max(max(s_best[0], s_best[1]), max(s_best[2], s_best[3]));
     if (g)
         for (unsigned q = threadIdx.x; q < gridDim.x; q += blockDim.x) {
             const BlockBest &r = rec[q];
@@ -1991,11 +2086,45 @@ __global__ void __launch_bounds__(256) k_select_maint(const unsigned long long *
             for (unsigned k = 0; k < min(r.n, (unsigned)SEL_MAX) && k0 + k < (unsigned)SEL_MAX; ++k)
                 cand[k0 + k] = r.cand[k];
         }
+    if (!full && g) {
+        // the cold blocks holding the best key, then their entries holding it
+        if (gc == g && gcnt == 1) {
+            const unsigned k = atomicAdd(&s_ncb, 1u);
+            if (k < 64) s_cb[k] = gfirst;
+        } else if (gc == g) {
+            // (rare: several of this thread's blocks hold it) its blocks again
+            for (uint32_t blk = threadIdx.x; blk < nblk; blk += blockDim.x)
+                if (ct.bmax[blk] == g) {
+                    const unsigned k = atomicAdd(&s_ncb, 1u);
+                    if (k < 64) s_cb[k] = blk;
+                }
+        }
+        __syncthreads();
+        const uint32_t ncb = s_ncb;
+        if (ncb > 64) {
+            if (threadIdx.x == 0) s_n = SEL_MAX;   // (too many: the host path)
+        } else {
+            for (uint32_t j = 0; j < ncb; ++j)
+#pragma unroll
+                for (int q = 0; q < (int)(CB / 256); ++q) {
+                    int2 ab;
+                    unsigned dd = 0;
+                    if (cold_entry_key(ct, s_cb[j] * CB + threadIdx.x + 256 * q, n_cold, len16,
+                                       max_length, ab, dd) == g) {
+                        const unsigned k = atomicAdd(&s_n, 1u);
+                        if (k < SEL_MAX) cand[k] = ab;
+                    }
+                }
+        }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         res->best = g;
         res->n_cand = s_n;
-        res->cold_dead = s_dsum[0] + s_dsum[1] + s_dsum[2] + s_dsum[3];
+        if (full) *ct.dead = (uint32_t)(s_dsum[0] + s_dsum[1] + s_dsum[2] + s_dsum[3]);
+        res->cold_dead = *ct.dead;
+        *ct.n_blist = 0;
+        *ct.sel_n0 = n_cold;
     }
 }
 
@@ -2413,7 +2542,7 @@ __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b, const Loop
         for (int q = 0; q < COLD_ILP; ++q) {
             const int32_t x = (int32_t)(kk[q] >> 16), y = (int32_t)(kk[q] & 0xFFFFu);
             if ((kk[q] != EMPTY) & ((x == a) | (x == b) | (y == a) | (y == b)))
-                ct.dcounts[i0 + q * stride] = 0;
+                ct.dcounts[i0 + q * stride] = 0;   // (MODE_FUSED: its selections are full scans)
         }
     }
 }
@@ -2422,7 +2551,9 @@ __global__ void k_cold_invalidate(ColdTable ct, int32_t a, int32_t b, const Loop
 // MODE_INCR before the pass of the merge (a, b) -> c: every pair with a side a or b loses its
 // count, in the maintained hot table (rows and columns a, b) and in the cold table.
 __global__ void k_incr_invalidate(ColdTable ct, unsigned long long *__restrict__ hot, int32_t a,
-                                  int32_t b, const LoopCtl *ctl = nullptr) {
+                                  int32_t b, const LoopCtl *ctl = nullptr,
+                                  const int32_t *__restrict__ len16 = nullptr,
+                                  int64_t max_length = 0) {
     if (loop_off(ctl)) return;
     if (ctl) {
         a = ctl->a;
@@ -2445,8 +2576,21 @@ __global__ void k_incr_invalidate(ColdTable ct, unsigned long long *__restrict__
 #pragma unroll
         for (int q = 0; q < COLD_ILP; ++q) {
             const int32_t x = (int32_t)(kk[q] >> 16), y = (int32_t)(kk[q] & 0xFFFFu);
-            if ((kk[q] != EMPTY) & ((x == a) | (x == b) | (y == a) | (y == b)))
-                ct.dcounts[i0 + q * stride] = 0;
+            if ((kk[q] != EMPTY) & ((x == a) | (x == b) | (y == a) | (y == b))) {
+                const uint32_t i = i0 + q * stride;
+                const unsigned long long old = ct.dcounts[i];
+                ct.dcounts[i] = 0;
+                // a fall matters to the block maxima only where the entry may have been its
+                // block's max (W at least the max's): that block is recomputed before the next
+                // selection (the recount after this merge can only give it back less)
+                const uint32_t blk = i / CB;
+                const unsigned long long ko =
+                    old && pair_ok(x, y, len16, max_length) ? pack_key(old, x, y) : 0ull;
+                if (ko && ko >= ct.bmax[blk] && atomicExch(&ct.bdirty[blk], 1u) == 0u) {
+                    const uint32_t k = atomicAdd(ct.n_blist, 1u);
+                    if (k <= ct.mask / CB) ct.blist[k] = blk;
+                }
+            }
         }
     }
 }

@@ -186,13 +186,20 @@ __device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32
 // (no sort: the pair table itself is the histogram)
 //   k_pix_build_links  links i -> i +- 1, and per block of PB positions its last run start
 //   k_pix_scan_max     the run start each block's first position continues (exclusive max-scan)
-//   k_pix_build_count  per valid pair position: its table slot (claimed on first sight), list
-//                      length + 1, count + 1 when counted (a pair (x, x) at an odd offset of its
-//                      run is not, core.ts:285-290)
+//   k_pix_hot_count    per valid pair position: list length + 1 and, for (x, x) at an odd offset
+//                      of its run, one uncounted occurrence (core.ts:285-290).  Hot pairs (both
+//                      ids < 256) go to a dense LDS counter per workgroup, one half of the 65536
+//                      hot pairs per pass (second id >> 7), dumped as the workgroup's slab; other
+//                      pairs claim their table slot and count there (global atomics)
+//   k_pix_hot_scan     per hot pair: its total, and each workgroup's exclusive offset (in place)
+//   k_pix_hot_claim    a table slot per hot pair that occurs, with its length and count
 //   k_pix_build_alloc  a pool segment per pair (one pool atomic per wave)
-//   k_pix_build_fill   every position into its pair's segment
-constexpr int PB = 4096;          // positions per build block (256 threads x 16)
-constexpr int PB_PER = PB / 256;
+//   k_pix_hot_fill     every position into its pair's segment: hot pairs through per-workgroup
+//                      LDS cursors (segment + the workgroup's offset), the others through the
+//                      pair's global fill counter
+// Round 2 sorted the keys with rocPRIM, and round 3's first version claimed and counted every
+// position with global atomics (65536 hot addresses, 2 atomics per position: 150 ms at C3).
+constexpr int PB = 4096;          // positions per build block
 
 __device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t *red) {
 #pragma unroll
@@ -279,67 +286,144 @@ __global__ void __launch_bounds__(1024) k_pix_scan_sum(uint32_t *__restrict__ v,
     if (t == 1023 && total) *total = part[1023];
 }
 
-// The block's PB positions (+ the next one) staged in LDS; per thread 16 consecutive ones with
-// their run starts: a block max-scan of the threads' last run starts, seeded with the block's
-// carry (the run start its first position continues).
-struct BuildSpan {
-    uint32_t i0;     // first position of the thread
-    int32_t rs;      // run start of the position before i0 (carry into the thread)
-};
+// The hot passes: PH_WG workgroups (one per CU) of PH_T threads, each over the blocks blk =
+// workgroup, workgroup + PH_WG, ...; per block, each thread takes PH_PER consecutive positions.
+constexpr int PH_T = 1024;
+constexpr int PH_PER = PB / PH_T;
+constexpr int PH_HALF = 32768;     // hot pairs per pass: (x, y) with y >> 7 == half
+constexpr int PH_WG_MAX = 256;
 
-__device__ __forceinline__ BuildSpan build_span(const PixCorpus &C, int32_t *tk, int32_t *sc,
-                                                uint32_t blk, int32_t carry) {
+__device__ __forceinline__ uint32_t ph_local(int32_t x, int32_t y) {
+    return ((uint32_t)x << 7) | ((uint32_t)y & 127u);
+}
+
+// the hot pair of pass `half`, local index i -> (x << 8) | y
+__device__ __forceinline__ uint32_t ph_index(uint32_t half, uint32_t i) {
+    return ((i >> 7) << 8) | (half << 7) | (i & 127u);
+}
+
+// Stages block blk's PB tokens and the one after them in tk.  RS: also the run start that this
+// thread's first position continues (an inclusive max-scan of the threads' last run starts: by
+// shuffles in the wave, across the waves through sc, seeded with the block's carry).
+template <bool RS>
+__device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int32_t *sc,
+                                           uint32_t blk, int32_t carry) {
     const uint32_t b0 = blk * PB;
-    for (uint32_t k = threadIdx.x; k <= (uint32_t)PB; k += 256) {
+    for (uint32_t k = threadIdx.x; k <= (uint32_t)PB; k += PH_T) {
         const uint32_t i = b0 + k;
         tk[k] = i < C.n ? C.tok[i] : SEP;
     }
     __syncthreads();
-    const uint32_t l0 = threadIdx.x * PB_PER;
+    if (!RS) return -1;
+    const uint32_t l0 = threadIdx.x * PH_PER;
     int32_t last = -1;
-    for (int k = 0; k < PB_PER; ++k) {
+#pragma unroll
+    for (int k = 0; k < PH_PER; ++k) {
         const uint32_t l = l0 + k, i = b0 + l;
         if (i < C.n && (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != tk[l])) last = (int32_t)i;
     }
-    sc[threadIdx.x] = last;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-        const int32_t o = (int)threadIdx.x >= d ? sc[threadIdx.x - d] : -1;
-        __syncthreads();
-        sc[threadIdx.x] = max(sc[threadIdx.x], o);
-        __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t v = last;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_up(v, d);
+        if (lane >= d) v = max(v, o);
     }
-    BuildSpan sp;
-    sp.i0 = b0 + l0;
-    sp.rs = max(carry, threadIdx.x ? sc[threadIdx.x - 1] : -1);
-    return sp;
+    if (lane == 63) sc[wv] = v;
+    __syncthreads();
+    int32_t rs = carry;
+    for (int w = 0; w < wv; ++w) rs = max(rs, sc[w]);
+    const int32_t ex = __shfl_up(v, 1);
+    return lane ? max(rs, ex) : rs;
 }
 
-__global__ void __launch_bounds__(256) k_pix_build_count(PixCorpus C, PixTable t, PixCtl *ctl,
-                                                         const int32_t *__restrict__ carry) {
+__global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t, PixCtl *ctl,
+                                                        const int32_t *__restrict__ carry, int half,
+                                                        uint32_t *__restrict__ slab,
+                                                        unsigned long long *__restrict__ oddxx) {
+    __shared__ uint32_t cnt[PH_HALF];
     __shared__ int32_t tk[PB + 1];
-    __shared__ int32_t sc[256];
+    __shared__ int32_t sc[PH_T / 64];
+    __shared__ uint32_t odd[128];
+    for (int i = threadIdx.x; i < PH_HALF; i += PH_T) cnt[i] = 0;
+    if (threadIdx.x < 128) odd[threadIdx.x] = 0;
     const uint32_t nblk = (C.n + PB - 1) / PB;
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const BuildSpan sp = build_span(C, tk, sc, blk, carry[blk]);
-        int32_t rs = sp.rs;
-        const uint32_t l0 = threadIdx.x * PB_PER;
-        for (int k = 0; k < PB_PER; ++k) {
-            const uint32_t l = l0 + k, i = sp.i0 + k;
+        __syncthreads();   // (tk and sc of the previous block are read; the counters are zero)
+        int32_t rs = ph_span<true>(C, tk, sc, blk, carry[blk]);
+        const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
+#pragma unroll
+        for (int k = 0; k < PH_PER; ++k) {
+            const uint32_t l = l0 + k, i = i0 + k;
             if (i >= C.n) break;
             const int32_t x = tk[l], y = i + 1 < C.n ? tk[l + 1] : SEP;
             if (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != x) rs = (int32_t)i;
             if ((x | y) < 0) continue;
-            const uint32_t s = pix_slot(t, ctl, pix_key(x, y), true, true);
-            if (s == PIX_NONE) {
-                atomicOr(&ctl->err, 9);   // (the table is too full: the host builds a bigger one)
-                continue;
+            const bool uncounted = x == y && ((i - (uint32_t)rs) & 1u);
+            if ((x | y) < 256) {
+                if ((y >> 7) != half) continue;
+                atomicAdd(&cnt[ph_local(x, y)], 1u);
+                if (uncounted) atomicAdd(&odd[x & 127], 1u);
+            } else if (half == 0) {
+                const uint32_t s = pix_slot(t, ctl, pix_key(x, y), true, true);
+                if (s == PIX_NONE) {
+                    atomicOr(&ctl->err, 9);   // (the table is too full: the host builds a bigger one)
+                    continue;
+                }
+                atomicAdd(&t.len[s], 1u);
+                if (!uncounted) atomicAdd(&t.cnt[s], 1ull);
             }
-            atomicAdd(&t.len[s], 1u);
-            if (x != y || !((i - (uint32_t)rs) & 1u)) atomicAdd(&t.cnt[s], 1ull);
         }
-        __syncthreads();
     }
+    __syncthreads();
+    uint32_t *out = slab + ((size_t)half * gridDim.x + blockIdx.x) * PH_HALF;
+    for (int i = threadIdx.x; i < PH_HALF; i += PH_T) out[i] = cnt[i];
+    if (threadIdx.x < 128 && odd[threadIdx.x])
+        atomicAdd(&oddxx[half * 128 + threadIdx.x], (unsigned long long)odd[threadIdx.x]);
+}
+
+// One thread per hot pair: the workgroups' counts (G slabs of the pair's half) become their
+// exclusive offsets, and the total goes to htot[(x << 8) | y].  Loads issued 16 at a time.
+__global__ void __launch_bounds__(256) k_pix_hot_scan(uint32_t *__restrict__ slab, int G,
+                                                      uint32_t *__restrict__ htot) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= 2u * PH_HALF) return;
+    const uint32_t half = j / PH_HALF, i = j % PH_HALF;
+    uint32_t *p = slab + (size_t)half * G * PH_HALF + i;
+    uint32_t run = 0;
+    for (int w0 = 0; w0 < G; w0 += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = w0 + q < G ? p[(size_t)(w0 + q) * PH_HALF] : 0u;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (w0 + q < G) p[(size_t)(w0 + q) * PH_HALF] = run;
+            run += v[q];
+        }
+    }
+    htot[ph_index(half, i)] = run;
+}
+
+// A table slot for every hot pair that occurs, with its list length and count.
+__global__ void __launch_bounds__(256) k_pix_hot_claim(PixTable t, PixCtl *ctl,
+                                                       const uint32_t *__restrict__ htot,
+                                                       const unsigned long long *__restrict__ oddxx,
+                                                       uint32_t *__restrict__ hslot) {
+    const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= 65536u) return;
+    const uint32_t n = htot[idx];
+    uint32_t s = PIX_NONE;
+    if (n) {
+        const int32_t x = (int32_t)(idx >> 8), y = (int32_t)(idx & 255u);
+        s = pix_slot(t, ctl, pix_key(x, y), true, true);
+        if (s == PIX_NONE) {
+            atomicOr(&ctl->err, 9);
+        } else {
+            t.len[s] = n;
+            t.cnt[s] = (unsigned long long)n - (x == y ? oddxx[x] : 0ull);
+        }
+    }
+    hslot[idx] = s;
 }
 
 __global__ void __launch_bounds__(256) k_pix_build_alloc(PixTable t, PixCtl *ctl, uint32_t cap) {
@@ -364,18 +448,42 @@ __global__ void __launch_bounds__(256) k_pix_build_alloc(PixTable t, PixCtl *ctl
     }
 }
 
-__global__ void __launch_bounds__(256) k_pix_build_fill(PixCorpus C, PixTable t, PixBufs B) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i + 1 < C.n;
-         i += gridDim.x * blockDim.x) {
-        const int32_t x = C.tok[i], y = C.tok[i + 1];
-        if ((x | y) < 0) continue;
-        const uint32_t key = pix_key(x, y);
-        uint32_t s = pix_hash(key) & t.mask;
-        // (present: claimed by the count, within its probe bound)
-        for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
-        if (t.keys[s] != key) continue;
-        const uint32_t k = atomicAdd(&t.fill[s], 1u);
-        B.pool[t.off[s] + k] = i;
+// Every position into its pair's segment.  Hot pairs of this pass: a per-workgroup LDS cursor
+// per pair, starting at the pair's segment + this workgroup's offset (k_pix_hot_scan), so no two
+// workgroups share a global counter.  Other pairs (pass 0): the pair's global fill counter.
+__global__ void __launch_bounds__(PH_T) k_pix_hot_fill(PixCorpus C, PixTable t, PixBufs B, int half,
+                                                       const uint32_t *__restrict__ slab,
+                                                       const uint32_t *__restrict__ hslot) {
+    __shared__ uint32_t cur[PH_HALF];
+    __shared__ int32_t tk[PB + 1];
+    const uint32_t *base = slab + ((size_t)half * gridDim.x + blockIdx.x) * PH_HALF;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)PH_HALF; i += PH_T) {
+        const uint32_t s = hslot[ph_index((uint32_t)half, i)];
+        cur[i] = s != PIX_NONE ? t.off[s] + base[i] : 0u;
+    }
+    const uint32_t nblk = (C.n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        __syncthreads();
+        ph_span<false>(C, tk, nullptr, blk, 0);
+        const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
+#pragma unroll
+        for (int k = 0; k < PH_PER; ++k) {
+            const uint32_t l = l0 + k, i = i0 + k;
+            if (i + 1 >= C.n) break;
+            const int32_t x = tk[l], y = tk[l + 1];
+            if ((x | y) < 0) continue;
+            if ((x | y) < 256) {
+                if ((y >> 7) != half) continue;
+                B.pool[atomicAdd(&cur[ph_local(x, y)], 1u)] = i;
+            } else if (half == 0) {
+                const uint32_t key = pix_key(x, y);
+                uint32_t s = pix_hash(key) & t.mask;
+                // (present: claimed by the count, within its probe bound)
+                for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
+                if (t.keys[s] != key) continue;
+                B.pool[t.off[s] + atomicAdd(&t.fill[s], 1u)] = i;
+            }
+        }
     }
 }
 

@@ -273,6 +273,9 @@ typedef struct {
     int64_t pix_merges;       /* incremental mode: merges made on the index (O(W) each) */
     int64_t pix_host;         /* incremental mode: iterations the index handed to the stream */
     double pix_build_ms;      /* incremental mode: wall time of those builds (host clock, synced) */
+    int64_t cold_used;        /* maintained state: claimed entries of the cold-pair table (largest seen) */
+    int64_t sel_blocks;       /* maintained state: block maxima recomputed by incremental selections
+                                 (cumulative since the context was made) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);
