@@ -1925,7 +1925,6 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             k_pix_begin<<<1, 1, 0, s>>>(P->d_ctl, want, (int32_t)base, mw);
             for (int64_t i = 0; i < want; ++i) {
                 k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
-                k_pix_tie<<<MAX_CAND * PIX_TIE_SPLIT, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
                 k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
                 k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
                 k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, c->d_len16, P->d_log);

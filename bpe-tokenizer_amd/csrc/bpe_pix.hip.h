@@ -17,8 +17,7 @@
 //
 // One merge (a, b) -> c, every kernel reading the decision from PixCtl (no host round trip):
 //   k_pix_select   the superblock maxima the previous merge lowered, then the best key, the
-//                  candidates, W, min_weight / vocabulary checks
-//   k_pix_tie      R3 over the candidates' lists (only with a tie)
+//                  candidates, R3 over their lists when tied, W, min_weight / vocabulary checks
 //   k_pix_sites    the merge sites from the (a, b) list and the count changes around them (for
 //                  a == b the runs, walked from their heads: sites at even offsets, replaceAll's
 //                  left-to-right rule); the new adjacencies, all of which contain c
@@ -556,13 +555,42 @@ __global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long
 }
 
 // ---- one merge --------------------------------------------------------------------------------
+// R3 (core.ts:294-305) costs one iteration of the kernel sequence, not a launch per merge: when the
+// best key is tied, k_pix_select publishes the candidates and sets tie = 1; k_pix_sites then scans
+// their lists on the whole grid instead of merging (the last block decides: tie = 2), k_pix_alloc
+// and k_pix_apply do nothing; the next k_pix_select commits the decided pair.  (A separate tie
+// launch cost 5.5 us per merge for the 372 ties among the 8000 C3 merges; one block scanning the
+// lists took ~240 us per tie.)
+enum PixTie { PIX_TIE_NONE = 0, PIX_TIE_SCAN = 1, PIX_TIE_DECIDED = 2 };
+
+// The merge of pair slot s (key `key`, list length len): vocabulary and table-room checks, then
+// the decision every later kernel reads.  (Thread 0 of k_pix_select.)
+__device__ void pix_commit(PixCtl *ctl, uint32_t s, uint32_t key, uint32_t len) {
+    if (ctl->next_id >= ctl->max_id) {
+        ctl->status = PIX_HOST;                                       // vocabulary limit
+        ctl->err = 5;
+        return;
+    }
+    // room for this merge's claims (<= 2 per site) within the table's fill limit
+    if (ctl->used + 2 * (unsigned long long)len + 64 > ctl->used_cap) {
+        ctl->status = PIX_HOST;
+        ctl->err = 6;
+        return;
+    }
+    ctl->c = ctl->next_id;
+    ctl->pair_slot = s;
+    ctl->a = (int32_t)(key >> 16);
+    ctl->b = (int32_t)(key & 0xFFFF);
+    ctl->tie = PIX_TIE_NONE;
+}
+
 // Best key, candidates (every pair sharing it), the decision.  One block of 1024.
 __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixCtl *ctl) {
     __shared__ unsigned long long red[16];
     __shared__ uint32_t lst[64];
     __shared__ uint32_t n_lst, n_blk, n_cs;
-    __shared__ uint32_t blks[64], cs[MAX_CAND];
-    __shared__ uint32_t s_go, s_nd;
+    __shared__ uint32_t blks[64], cs[MAX_CAND], cs_key[MAX_CAND], cs_len[MAX_CAND];
+    __shared__ uint32_t s_go, s_nd, s_tie;
     __shared__ long long s_mw;
     const int tid = threadIdx.x;
     // (every control value a branch below depends on is read by one thread and broadcast through
@@ -571,9 +599,20 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         s_go = ctl->status != PIX_RUN ? 0u : ctl->n_done >= ctl->n_want ? 1u : 2u;
         s_nd = min(ctl->n_dsuper, t.nsuper);
         s_mw = ctl->min_weight;
+        s_tie = (uint32_t)ctl->tie;
     }
     __syncthreads();
     if (s_go == 0) return;
+    if (s_go == 2 && s_tie == PIX_TIE_DECIDED) {
+        // the tie the last iteration's scan decided (nothing changed since): commit its pair
+        if (tid == 0) {
+            const uint32_t sl = ctl->pair_slot;
+            ctl->n_sites = ctl->n_ent = ctl->n_dblocks = ctl->n_dsuper = 0;
+            ctl->n_check = 0;
+            pix_commit(ctl, sl, t.keys[sl], t.len[sl]);
+        }
+        return;
+    }
     {
         // the superblocks the previous merge may have lowered (one wave each)
         const int lane = tid & 63, wv = tid >> 6;
@@ -602,10 +641,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         // counters of the previous merge (nothing else reads them now)
         ctl->n_sites = ctl->n_ent = ctl->n_dblocks = ctl->n_dsuper = 0;
         ctl->n_cand = 0;
-        ctl->tie = 0;
-        ctl->tie_done = 0;
         ctl->n_check = 0;
-        for (int q = 0; q < MAX_CAND; ++q) ctl->last[q] = 0;
         n_lst = n_blk = n_cs = 0;
     }
     if (s_go == 1) {
@@ -642,16 +678,20 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         }
     }
     __syncthreads();
-    // the candidates gather in LDS; thread 0 publishes them (a global counter that other waves of
-    // this block add to while thread 0 has just stored it, then reads back, is not ordered by the
-    // barrier: a candidate could be lost, and a tie with it)
+    // the candidates gather in LDS with their keys and list lengths (a global counter that other
+    // waves of this block add to while thread 0 has just stored it, then reads back, is not
+    // ordered by the barrier: a candidate could be lost, and a tie with it)
     const uint32_t nbk = min(n_blk, 64u);
     for (uint32_t q = 0; q < nbk; ++q) {
         if (tid < PIX_B) {
             const uint32_t s = blks[q] * PIX_B + tid;
             if (pix_sel(t, s) == best) {
                 const uint32_t k = atomicAdd(&n_cs, 1u);
-                if (k < MAX_CAND) cs[k] = s;
+                if (k < MAX_CAND) {
+                    cs[k] = s;
+                    cs_key[k] = t.keys[s];
+                    cs_len[k] = t.len[s];
+                }
             }
         }
     }
@@ -659,74 +699,55 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
     if (tid == 0) {
         const uint32_t nc = n_cs;
         ctl->n_cand = nc;
-        for (uint32_t j = 0; j < min(nc, (uint32_t)MAX_CAND); ++j) ctl->cand_slot[j] = cs[j];
         if (n_lst > 64 || n_blk > 64 || nc > (uint32_t)MAX_CAND || nc == 0) {
             ctl->status = PIX_HOST;
             ctl->err = nc == 0 ? 10 : 4;
             return;
         }
-        if (ctl->next_id >= ctl->max_id) {
-            ctl->status = PIX_HOST;                                   // vocabulary limit
-            ctl->err = 5;
-            return;
-        }
-        // room for this merge's claims (<= 2 per site) within the table's fill limit
-        const uint32_t s0 = ctl->cand_slot[0];
-        unsigned long long room = 0;
-        for (uint32_t j = 0; j < nc; ++j) room = max(room, (unsigned long long)t.len[ctl->cand_slot[j]]);
-        if (ctl->used + 2 * room + 64 > ctl->used_cap) {
-            ctl->status = PIX_HOST;
-            ctl->err = 6;
-            return;
-        }
         ctl->best = best;
         ctl->W = (unsigned long long)W;
-        ctl->c = ctl->next_id;
-        ctl->tie = nc > 1;
-        ctl->pair_slot = s0;
-        ctl->a = (int32_t)(t.keys[s0] >> 16);
-        ctl->b = (int32_t)(t.keys[s0] & 0xFFFF);
+        if (nc == 1) {
+            pix_commit(ctl, cs[0], cs_key[0], cs_len[0]);
+        } else {
+            // tied: k_pix_sites scans the candidates' lists this iteration
+            for (uint32_t j = 0; j < nc; ++j) {
+                ctl->cand_slot[j] = cs[j];
+                ctl->last[j] = 0;
+            }
+            ctl->tie_done = 0;
+            ctl->tie = PIX_TIE_SCAN;
+        }
     }
 }
 
-// R3 (core.ts:296-305): among the tied pairs, the one whose last counted occurrence comes first.
-// PIX_TIE_SPLIT blocks per candidate find the last valid slot of its list (atomicMax); the last
-// block to finish turns it into the last counted one (for (x, x): the last valid slot at an even
-// offset of its run) and decides.
-constexpr int PIX_TIE_SPLIT = 16;
-__global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
+// The tie scan (k_pix_sites with tie == PIX_TIE_SCAN, the whole grid): the last valid slot of
+// each candidate's list (atomicMax into ctl->last), then the last block to finish turns it into
+// the last counted occurrence (for (x, x): the last valid slot at an even offset of its run) and
+// the earliest of those wins (tie = PIX_TIE_DECIDED, pair_slot = the winner).
+__device__ void pix_tie_scan(const PixCorpus &C, const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                             uint32_t nc) {
     __shared__ unsigned long long red[4];
     __shared__ bool last_block;
-    __shared__ uint32_t s_run, s_nc;
-    // (the control block is read by one thread and broadcast, so every branch around a barrier
-    // below is uniform by construction, whatever the compiler can prove)
-    if (threadIdx.x == 0) {
-        s_run = ctl->status == PIX_RUN && ctl->tie;
-        s_nc = ctl->n_cand;
-    }
-    __syncthreads();
-    if (!s_run) return;
-    const uint32_t j = blockIdx.x / PIX_TIE_SPLIT, part = blockIdx.x % PIX_TIE_SPLIT;
-    const uint32_t nc = s_nc;
-    unsigned long long m = 0;
-    if (j < nc) {
+    for (uint32_t j = 0; j < nc; ++j) {
         const uint32_t s = ctl->cand_slot[j];
-        const int32_t u = (int32_t)(t.keys[s] >> 16), v = (int32_t)(t.keys[s] & 0xFFFF);
+        const uint32_t key = t.keys[s];
+        const int32_t u = (int32_t)(key >> 16), v = (int32_t)(key & 0xFFFF);
         const uint32_t off = t.off[s], len = t.len[s];
-        for (uint32_t i = part * 256 + threadIdx.x; i < len; i += PIX_TIE_SPLIT * 256) {
+        unsigned long long m = 0;
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
             const uint32_t p = B.pool[off + i];
             if (C.tok[p] == u && pix_tok_is(C, C.nxt[p], v)) m = max(m, (unsigned long long)p + 1);
         }
-    }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0 && j < nc) {
-        m = max(max(red[0], red[1]), max(red[2], red[3]));
-        if (m) atomicMax(&ctl->last[j], m);
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, d));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            m = max(max(red[0], red[1]), max(red[2], red[3]));
+            if (m) atomicMax(&ctl->last[j], m);
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
         last_block = atomicAdd(&ctl->tie_done, 1u) == gridDim.x - 1;
@@ -765,10 +786,8 @@ __global__ void __launch_bounds__(256) k_pix_tie(PixCorpus C, PixTable t, PixBuf
         ctl->err = 8;
         return;
     }
-    const uint32_t s = ctl->cand_slot[bj];
-    ctl->pair_slot = s;
-    ctl->a = (int32_t)(t.keys[s] >> 16);
-    ctl->b = (int32_t)(t.keys[s] & 0xFFFF);
+    ctl->pair_slot = ctl->cand_slot[bj];
+    ctl->tie = PIX_TIE_DECIDED;
 }
 
 // a != b: the count changes around each site p (q = next, l = prev of p, r = next of q).
@@ -868,13 +887,18 @@ __device__ __forceinline__ void pix_push_site(const PixBufs &B, PixCtl *ctl, uin
 // odd), so (l, a) -> (l, c) on the left, (a, r) -> (c, r) on the right when L is even, (c, a)
 // when L is odd, and floor(m/2) pairs (c, c) for the m c's.
 __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl) {
-    __shared__ uint32_t s_run, s_len;
+    __shared__ uint32_t s_run, s_len, s_tie;
     if (threadIdx.x == 0) {   // (read once and broadcast: the loop around the barriers is uniform)
         s_run = ctl->status == PIX_RUN;
-        s_len = s_run ? t.len[ctl->pair_slot] : 0u;
+        s_tie = s_run && ctl->tie == PIX_TIE_SCAN ? min(ctl->n_cand, (uint32_t)MAX_CAND) : 0u;
+        s_len = s_run && !s_tie ? t.len[ctl->pair_slot] : 0u;
     }
     __syncthreads();
     if (!s_run) return;
+    if (s_tie) {
+        pix_tie_scan(C, t, B, ctl, s_tie);
+        return;
+    }
     const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
     const uint32_t s = ctl->pair_slot;
     const uint32_t off = t.off[s], len = s_len;
@@ -977,8 +1001,9 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
     __shared__ unsigned long long wsum[4], wown[4], base_s;
     __shared__ uint32_t s_ne;
     if (threadIdx.x == 0)   // (read once and broadcast: the loop around the barriers is uniform)
-        s_ne = ctl->status != PIX_RUN ? 0u
-                                      : min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
+        s_ne = ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE
+                   ? 0u
+                   : min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t ne = s_ne;
@@ -1032,7 +1057,7 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
 // W must equal the sites found.
 __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl,
                                                    int32_t *len16, long long *log) {
-    if (ctl->status != PIX_RUN) return;
+    if (ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE) return;   // (a tie scan: no merge)
     const unsigned long long W = ctl->W;
     if (ctl->n_sites != W || (ctl->a == ctl->b && ctl->n_check != W)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -52,7 +52,9 @@ def main():
     out = {'launches': len(rows), 'span_ms': span / 1e6, 'kernels': {}}
     for n in sorted(dur, key=lambda k: -sum(dur[k])):
         d, g = dur[n], gap[n]
+        ds = sorted(d)
         out['kernels'][n] = {'calls': len(d), 'avg_us': sum(d) / len(d) / 1e3, 'total_ms': sum(d) / 1e6,
+                             'median_us': ds[len(ds) // 2] / 1e3, 'p90_us': ds[9 * len(ds) // 10] / 1e3,
                              'avg_gap_before_us': (sum(g) / len(g) / 1e3) if g else None,
                              'total_gap_ms': sum(g) / 1e6}
     out['busy_ms'] = sum(v['total_ms'] for v in out['kernels'].values())
