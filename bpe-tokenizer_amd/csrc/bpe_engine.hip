@@ -14,6 +14,15 @@
 #include "bpe_multi.h"
 #include "bpe_tools.h"
 
+namespace bpe_step {
+// (csrc/bpe_step.hip: the C3 hot path's pass, compiled with its own flags; the structures are
+// the ones of bpe_kernels.hip.h, passed untyped)
+hipError_t launch_step_loop_table(unsigned grid, hipStream_t s, int32_t *ids, int64_t n_chunks,
+                                  int64_t cpr, int R, const void *carry, const void *ctl,
+                                  uint32_t *partials, unsigned long long *spill, const void *ct,
+                                  void *sums, unsigned long long *replaced);
+}
+
 #include <algorithm>
 #include <chrono>
 #include <cstddef>
@@ -973,9 +982,10 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
                                                         c->d_spill, c->cold, c->d_sums,
                                                         &c->d_res->replaced);
         } else {
-            k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
-                                            c->d_ctl, c->d_partials, c->d_spill, c->cold,
-                                            c->d_sums, &c->d_res->replaced);
+            HIP_TRY(bpe_step::launch_step_loop_table(c->G, s, c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                     c->d_carry, c->d_ctl, c->d_partials,
+                                                     c->d_spill, &c->cold, c->d_sums,
+                                                     &c->d_res->replaced));
         }
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_step, 0))) return rc;
@@ -1235,9 +1245,9 @@ int rank_loop_count(bpe_ctx *c) {
                                                    c->d_ctl, c->d_partials, c->d_spill, c->cold,
                                                    c->d_sums, &c->d_res->replaced, c->d_hot, x);
     } else {
-        k_step_loop<<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, c->d_ctl,
-                                        c->d_partials, c->d_spill, c->cold, c->d_sums,
-                                        &c->d_res->replaced);
+        HIP_TRY(bpe_step::launch_step_loop_table(c->G, s, c->d_ids, c->n_chunks, c->cpr, c->R,
+                                                 c->d_carry, c->d_ctl, c->d_partials, c->d_spill,
+                                                 &c->cold, c->d_sums, &c->d_res->replaced));
     }
     HIP_TRY(hipGetLastError());
     int rc;
