@@ -4,7 +4,7 @@
 // uniform branches of the ring stay scalar branches instead of lane-mask regions: k_step_loop
 // 0.789 -> 0.775 ms at C3 (tools/ab_exp.sh, profiles/r03_ab_skip_uniform.json).  The same flag
 // made the maintained-state pass (MODE_INCR) 2 % slower on zipf C3, so only this instantiation
-// takes it.
+// takes it, with its own scheduling flags and ring depth (Makefile STEP_FLAGS).
 //
 // The kernel header is included with internal linkage (an anonymous namespace), so its other
 // kernels are not defined twice in libbpe.so; the launcher therefore takes the engine's
