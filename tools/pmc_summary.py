@@ -25,7 +25,7 @@ def per_launch(path, counter):
     for f in glob.glob(os.path.join(path, '**', '*counter_collection.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
             if r['Counter_Name'] == counter:
-                vals[r['Kernel_Name'].split('(')[0].replace('void bpe::', '')].append(float(r['Counter_Value']))
+                vals[r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void bpe::', '')].append(float(r['Counter_Value']))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
 
@@ -44,7 +44,7 @@ def main():
     stats = {}
     for f in glob.glob(os.path.join(src, 'trace', '**', '*kernel_stats.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
-            stats[r['Name'].split('(')[0].replace('void bpe::', '')] = {
+            stats[r['Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void bpe::', '')] = {
                 'calls': int(r['Calls']), 'avg_ns': float(r['AverageNs']), 'pct': float(r['Percentage'])}
     out['kernel_stats'] = stats
     bench = os.path.join(src, 'bench.jsonl')

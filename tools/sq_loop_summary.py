@@ -12,7 +12,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for sub in ('sq', 'sq2'):
     for f in glob.glob(os.path.join(d, sub, '**', '*counter_collection.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
-            kern = r['Kernel_Name'].split('(')[0].replace('void bpe::', '').replace('bpe::', '')
+            kern = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void bpe::', '').replace('bpe::', '')
             agg[(kern, r['Counter_Name'])][r['Dispatch_Id']] += float(r['Counter_Value'])
 rows = {}
 for (kern, c), v in sorted(agg.items()):

@@ -16,7 +16,7 @@ for f in sorted(glob.glob(os.path.join(d, '*', '**', '*counter_collection.csv'),
     for r in csv.DictReader(open(f)):
         if 'k_step' not in r['Kernel_Name']:
             continue
-        kern = r['Kernel_Name'].split('(')[0].replace('void bpe::', '')
+        kern = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void bpe::', '')
         agg[(kern, r['Counter_Name'])][r['Dispatch_Id']] += float(r['Counter_Value'])
     for (kern, c), v in sorted(agg.items()):
         vals = list(v.values())

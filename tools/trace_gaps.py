@@ -16,7 +16,7 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split('(')[0]
+    n = name.replace('(anonymous namespace)::', '').split('(')[0]
     n = n.replace('void ', '').replace('bpe::', '')
     return n[:80]
 
