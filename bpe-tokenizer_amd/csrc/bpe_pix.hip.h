@@ -631,11 +631,12 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
                 t.sbdirty[sb] = 0;
             }
         }
-        // (their new maxima are read below by other waves: made visible at agent scope, L1
-        // invalidated after the barrier)
-        __threadfence();
+        // (their new maxima are read below by other waves of this block, on this CU: a
+        // workgroup-scope fence, i.e. the stores complete before the barrier.  No other wave
+        // loaded those lines in this launch, so no L1 line can be stale.  Agent-scope fences
+        // here cost ~2 us each)
+        __threadfence_block();
         __syncthreads();
-        __threadfence();
     }
     if (tid == 0) {
         // counters of the previous merge (nothing else reads them now)
