@@ -560,7 +560,9 @@ int compact(bpe_ctx *c) {
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
     hipStream_t s = c->stream;
     k_scan_live<<<1, 1024, 0, s>>>(c->d_sums, c->R, c->d_outoff, c->d_total);
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
+    // (no fill of the target first: k_compact writes the live prefix and seal_packed the last
+    // chunk's tail and the spare chunk, the only slots past the prefix that anything reads.  A
+    // fill of the whole buffer cost ~0.7 ms per compaction, 58 of them on zipf C3)
     k_compact<<<(c->R + 3) / 4, 256, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_outoff,
                                              c->d_tmp);
     HIP_TRY(hipGetLastError());
@@ -1746,10 +1748,11 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
     // hot pairs' totals, slots and uncounted (x, x) occurrences
     Scratch hs;
     const int G = (int)std::min<uint32_t>(PH_WG_MAX, nblk);
-    uint32_t *slab, *htot, *hslot;
+    uint32_t *slab, *htot, *hslot, *hseg, *bucket, *xoff;
     unsigned long long *oddxx;
     if ((rc = hs.get(&slab, (size_t)2 * G * PH_HALF)) || (rc = hs.get(&htot, 65536)) ||
-        (rc = hs.get(&hslot, 65536)) || (rc = hs.get(&oddxx, 256)))
+        (rc = hs.get(&hslot, 65536)) || (rc = hs.get(&oddxx, 256)) || (rc = hs.get(&hseg, 65536)) ||
+        (rc = hs.get(&bucket, 257)) || (rc = hs.get(&xoff, (size_t)G * 256)))
         return rc;
     // the pair table: room for the current pairs and the ones merges will add
     uint64_t cap = 1u << 20;
@@ -1787,6 +1790,7 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
         for (int half = 0; half < 2; ++half)
             k_pix_hot_count<<<G, PH_T, 0, s>>>(C, T, P->d_ctl, carry, half, slab, oddxx);
+        k_pix_hot_xoff<<<256, 256, 0, s>>>(slab, G, xoff);
         k_pix_hot_scan<<<2 * PH_HALF / 256, 256, 0, s>>>(slab, G, htot);
         k_pix_hot_claim<<<65536 / 256, 256, 0, s>>>(T, P->d_ctl, htot, oddxx, hslot);
         HIP_TRY(hipGetLastError());
@@ -1802,9 +1806,28 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         cap <<= 2;
         if (attempt == 3) return PIX_NOT_ELIGIBLE;
     }
-    k_pix_build_alloc<<<4096, 256, 0, s>>>(T, P->d_ctl, (uint32_t)cap);
-    for (int half = 0; half < 2; ++half)
-        k_pix_hot_fill<<<G, PH_T, 0, s>>>(C, T, B, half, slab, hslot);
+    // the hot pairs' segments in (x, y) order (buckets by first token), then the cold pairs'
+    k_pix_hot_seg<<<1, 1024, 0, s>>>(T, P->d_ctl, htot, hslot, hseg, bucket);
+    k_pix_build_alloc<<<4096, 256, 0, s>>>(T, P->d_ctl, (uint32_t)cap, 1);
+    HIP_TRY(hipGetLastError());
+    // The two-level fill when no first token holds more than 1/32 of the hot positions (a
+    // workgroup per bucket does the second level); else the per-pair cursors (k_pix_hot_fill)
+    uint32_t hb[257];
+    HIP_TRY(hipMemcpyAsync(hb, bucket, sizeof hb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t bmax = 0;
+    for (int x = 0; x < 256; ++x) bmax = std::max(bmax, hb[x + 1] - hb[x]);
+    uint2 *stage = nullptr;
+    const bool two_level = hb[256] > 0 && (uint64_t)bmax * 32 <= (uint64_t)hb[256] + (1u << 20) &&
+                           !getenv("BPE_PIX_FILL_PAIRS") && hs.get(&stage, hb[256]) == BPE_OK;
+    if (!two_level) (void)hipGetLastError();   // (a failed staging allocation is not an error)
+    if (two_level) {
+        k_pix_fill_x<<<G, PH_T, 0, s>>>(C, T, B, xoff, bucket, stage);
+        k_pix_fill_y<<<256, 1024, 0, s>>>(B, hseg, bucket, stage);
+    } else {
+        for (int half = 0; half < 2; ++half)
+            k_pix_hot_fill<<<G, PH_T, 0, s>>>(C, T, B, half, slab, hslot);
+    }
     HIP_TRY(hipGetLastError());
     // per-merge buffers
     B.site_cap = (uint32_t)std::min<uint64_t>(N / 2 + 16, 1u << 26);
@@ -1839,7 +1862,7 @@ int pix_finish(bpe_ctx *c) {
         const uint32_t nblk = (N + PB - 1) / PB;
         int rc;
         if ((rc = t.get(&cnt, nblk)) || (rc = t.get(&d_total, 1))) return rc;
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_tmp, SEP, c->cap_slots, s));
+        // (no fill first: the scatter writes the live prefix, seal_packed the rest that is read)
         k_pix_live_count<<<4096, 256, 0, s>>>(c->d_ids, N, cnt);
         k_pix_scan_sum<<<1, 1024, 0, s>>>(cnt, nblk, d_total);
         k_pix_live_scatter<<<4096, 256, 0, s>>>(c->d_ids, N, cnt, c->d_tmp);

@@ -425,11 +425,17 @@ __global__ void __launch_bounds__(256) k_pix_hot_claim(PixTable t, PixCtl *ctl,
     hslot[idx] = s;
 }
 
-__global__ void __launch_bounds__(256) k_pix_build_alloc(PixTable t, PixCtl *ctl, uint32_t cap) {
+__device__ __forceinline__ bool pix_hot_key(uint32_t k) {
+    return k != PIX_NONE && (k >> 16) < 256u && (k & 0xFFFFu) < 256u;
+}
+
+// (skip_hot: the hot pairs' segments were placed by k_pix_hot_seg, in (x, y) order)
+__global__ void __launch_bounds__(256) k_pix_build_alloc(PixTable t, PixCtl *ctl, uint32_t cap,
+                                                         int skip_hot = 0) {
     const int lane = threadIdx.x & 63;
     for (uint32_t s0 = (blockIdx.x * blockDim.x) & ~63u; s0 < cap; s0 += gridDim.x * blockDim.x) {
         const uint32_t s = s0 + lane + (threadIdx.x & ~63u);
-        const uint32_t len = s < cap ? t.len[s] : 0u;
+        const uint32_t len = s < cap && !(skip_hot && pix_hot_key(t.keys[s])) ? t.len[s] : 0u;
         uint32_t incl = len;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -483,6 +489,146 @@ __global__ void __launch_bounds__(PH_T) k_pix_hot_fill(PixCorpus C, PixTable t, 
                 B.pool[t.off[s] + atomicAdd(&t.fill[s], 1u)] = i;
             }
         }
+    }
+}
+
+// The two-level fill (the corpus's hot pairs are not skewed towards a few first tokens): the hot
+// pairs' segments lie in (x, y) order, so the segments of first token x form one bucket.
+//   k_pix_hot_seg    per hot pair its segment (an exclusive scan of the totals in (x, y) order),
+//                    per x its bucket; the cold pairs' segments follow (pool_top)
+//   k_pix_hot_xoff   per (workgroup, x) where that workgroup's positions of bucket x start (its
+//                    count from the slabs, an exclusive scan over the workgroups)
+//   k_pix_fill_x     every hot position (y, i) into its bucket, through 256 LDS cursors per
+//                    workgroup; cold positions through their pair's global fill counter
+//   k_pix_fill_y     one workgroup per bucket: every (y, i) into segment (x, y), 256 LDS cursors
+// Each workgroup writes 256 streams at a time (k_pix_hot_fill: 32768), few enough for L2 to
+// combine the 4- and 8-byte stores into lines.
+__global__ void __launch_bounds__(1024) k_pix_hot_seg(PixTable t, PixCtl *ctl,
+                                                      const uint32_t *__restrict__ htot,
+                                                      const uint32_t *__restrict__ hslot,
+                                                      uint32_t *__restrict__ hseg,
+                                                      uint32_t *__restrict__ bucket) {
+    __shared__ uint32_t part[1024];
+    const uint32_t tid = threadIdx.x, i0 = tid * 64;   // 64 hot pairs per thread, (x, y) order
+    uint32_t acc = 0;
+    for (int k = 0; k < 64; ++k) acc += htot[i0 + k];
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t o = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += o;
+        __syncthreads();
+    }
+    uint32_t run = tid ? part[tid - 1] : 0u;
+    for (int k = 0; k < 64; ++k) {
+        const uint32_t idx = i0 + k, n = htot[idx];
+        hseg[idx] = run;
+        if ((idx & 255u) == 0) bucket[idx >> 8] = run;
+        const uint32_t sl = hslot[idx];
+        if (n && sl != PIX_NONE) {
+            t.off[sl] = run;
+            t.fill[sl] = 0;
+        }
+        run += n;
+    }
+    if (tid == 1023) {
+        bucket[256] = run;
+        ctl->pool_top = run;   // (the cold pairs' segments after the hot ones)
+    }
+}
+
+// block x, thread w: workgroup w's positions with first token x start at bucket[x] +
+// xoff[w * 256 + x].  (Runs on the slabs' counts, before k_pix_hot_scan turns them into offsets.)
+__global__ void __launch_bounds__(256) k_pix_hot_xoff(const uint32_t *__restrict__ slab, int G,
+                                                      uint32_t *__restrict__ xoff) {
+    __shared__ uint32_t part[256];
+    const uint32_t x = blockIdx.x, w = threadIdx.x;
+    uint32_t c = 0;
+    if ((int)w < G)
+        for (uint32_t half = 0; half < 2; ++half) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(slab + ((size_t)half * G + w) * PH_HALF +
+                                                             (x << 7));
+#pragma unroll 8
+            for (int k = 0; k < 32; ++k) {
+                const uint4 v = p[k];
+                c += v.x + v.y + v.z + v.w;
+            }
+        }
+    part[w] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t o = w >= d ? part[w - d] : 0u;
+        __syncthreads();
+        part[w] += o;
+        __syncthreads();
+    }
+    if ((int)w < G) xoff[w * 256 + x] = w ? part[w - 1] : 0u;
+}
+
+__global__ void __launch_bounds__(PH_T) k_pix_fill_x(PixCorpus C, PixTable t, PixBufs B,
+                                                     const uint32_t *__restrict__ xoff,
+                                                     const uint32_t *__restrict__ bucket,
+                                                     uint2 *__restrict__ stage) {
+    __shared__ uint32_t cur[256];
+    __shared__ int32_t tk[PB + 1];
+    if (threadIdx.x < 256) cur[threadIdx.x] = bucket[threadIdx.x] + xoff[blockIdx.x * 256 + threadIdx.x];
+    const uint32_t nblk = (C.n + PB - 1) / PB;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        __syncthreads();
+        ph_span<false>(C, tk, nullptr, blk, 0);
+        const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
+        // (the hot positions' cursor adds first, all of them, then their stores: one LDS
+        // round trip per PH_PER positions instead of one per position)
+        uint32_t at[PH_PER];
+#pragma unroll
+        for (int k = 0; k < PH_PER; ++k) {
+            const int32_t x = tk[l0 + k], y = tk[l0 + k + 1];
+            const bool hot = i0 + k + 1 < C.n && (x | y) >= 0 && (x | y) < 256;
+            at[k] = hot ? atomicAdd(&cur[x], 1u) : PIX_NONE;
+        }
+#pragma unroll
+        for (int k = 0; k < PH_PER; ++k)
+            if (at[k] != PIX_NONE) stage[at[k]] = make_uint2((uint32_t)tk[l0 + k + 1], i0 + k);
+#pragma unroll
+        for (int k = 0; k < PH_PER; ++k) {
+            const uint32_t l = l0 + k, i = i0 + k;
+            if (i + 1 >= C.n) break;
+            const int32_t x = tk[l], y = tk[l + 1];
+            if ((x | y) < 0) continue;
+            if ((x | y) < 256) {
+                continue;   // (above)
+            } else {
+                const uint32_t key = pix_key(x, y);
+                uint32_t s = pix_hash(key) & t.mask;
+                // (present: claimed by the count, within its probe bound)
+                for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
+                if (t.keys[s] != key) continue;
+                B.pool[t.off[s] + atomicAdd(&t.fill[s], 1u)] = i;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_pix_fill_y(PixBufs B, const uint32_t *__restrict__ hseg,
+                                                     const uint32_t *__restrict__ bucket,
+                                                     const uint2 *__restrict__ stage) {
+    __shared__ uint32_t cur[256];
+    const uint32_t x = blockIdx.x;
+    if (threadIdx.x < 256) cur[threadIdx.x] = hseg[x * 256 + threadIdx.x];
+    __syncthreads();
+    const uint32_t b0 = bucket[x], b1 = bucket[x + 1];
+    // (4 entries per thread and round: their loads, cursor adds and stores each issued together)
+    for (uint32_t j0 = b0 + threadIdx.x; j0 < b1; j0 += 4 * 1024) {
+        uint2 e[4];
+        uint32_t at[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = j0 + 1024 * k < b1 ? stage[j0 + 1024 * k] : make_uint2(256u, 0u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) at[k] = e[k].x < 256u ? atomicAdd(&cur[e[k].x], 1u) : PIX_NONE;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (at[k] != PIX_NONE) B.pool[at[k]] = e[k].y;
     }
 }
 
