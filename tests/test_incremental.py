@@ -109,3 +109,30 @@ def test_zipf_words_match_the_stream():
     got = b.merge_until(0, 2, 1500)
     assert got == want
     assert np.array_equal(a.read_corpus()[0], b.read_corpus()[0])
+
+
+@pytest.mark.parametrize('fill', ['two_level', 'pairs'])
+@pytest.mark.parametrize('seed', range(3))
+def test_index_build_fill_forms(fill, seed, monkeypatch):
+    """The index build's two fill forms (csrc/bpe_pix.hip.h: the two-level scatter by first then
+    second token, and the per-pair cursors it falls back to when one first token dominates,
+    forced here with BPE_PIX_FILL_PAIRS): the oracle's merges either way, with skewed first tokens
+    in one of the corpora."""
+    if fill == 'pairs':
+        monkeypatch.setenv('BPE_PIX_FILL_PAIRS', '1')
+    rng = random.Random(1300 + seed)
+    alphabet = [256, 40, 256][seed]
+    samples = random_corpus(rng, 300000, alphabet, [0.0, 0.2, 0.6][seed], rng.choice([9, 100]))
+    if seed == 2:   # (one first token in most hot positions)
+        samples = [np.where(np.arange(len(s)) % 2 == 0, 7, s).astype(np.int32) for s in samples]
+    len16 = [1] * alphabet
+    ids, off = _flat(samples)
+    st = OracleState(ids, off, len16, alphabet)
+    e = make_engine(samples, len16)
+    e.set_mode('incremental')
+    e.stats_enable(True)
+    want = st.merge_until(0, 2, 60)
+    got = e.merge_until(0, 2, 60)
+    assert got == want, (got[:3], want[:3])
+    assert e.samples() == st.samples()
+    assert e.stats()['pix_merges'] > 0
