@@ -1788,8 +1788,8 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
         h->pool_cap = pool_cap;
         h->used_cap = cap / 10 * 7;
         HIP_TRY(hipMemcpyAsync(P->d_ctl, h, sizeof *h, hipMemcpyHostToDevice, s));
-        for (int half = 0; half < 2; ++half)
-            k_pix_hot_count<<<G, PH_T, 0, s>>>(C, T, P->d_ctl, carry, half, slab, oddxx);
+        HIP_TRY(hipMemsetAsync(slab, 0, (size_t)2 * G * PH_HALF * sizeof(uint32_t), s));
+        k_pix_hot_count<<<G, PH_T, 0, s>>>(C, T, P->d_ctl, carry, slab, oddxx);
         k_pix_hot_xoff<<<256, 256, 0, s>>>(slab, G, xoff);
         k_pix_hot_scan<<<2 * PH_HALF / 256, 256, 0, s>>>(slab, G, htot);
         k_pix_hot_claim<<<65536 / 256, 256, 0, s>>>(T, P->d_ctl, htot, oddxx, hslot);

@@ -304,6 +304,34 @@ __device__ __forceinline__ uint32_t ph_index(uint32_t half, uint32_t i) {
 // Stages block blk's PB tokens and the one after them in tk.  RS: also the run start that this
 // thread's first position continues (an inclusive max-scan of the threads' last run starts: by
 // shuffles in the wave, across the waves through sc, seeded with the block's carry).
+// (the loads of a block's tokens into registers, a block ahead of their store into tk, so the
+// next block's loads overlap this block's work)
+struct PhNext {
+    int32_t v[PB / PH_T + 1];
+};
+
+__device__ __forceinline__ void ph_fetch(const PixCorpus &C, uint32_t blk, PhNext &r) {
+    const uint32_t b0 = blk * PB;
+#pragma unroll
+    for (int q = 0; q <= PB / PH_T; ++q) {
+        const uint32_t k = threadIdx.x + q * PH_T, i = b0 + k;
+        r.v[q] = k <= (uint32_t)PB && i < C.n ? __builtin_nontemporal_load(C.tok + i) : SEP;
+    }
+}
+
+__device__ __forceinline__ void ph_put(int32_t *tk, const PhNext &r) {
+#pragma unroll
+    for (int q = 0; q <= PB / PH_T; ++q) {
+        const uint32_t k = threadIdx.x + q * PH_T;
+        if (k <= (uint32_t)PB) tk[k] = r.v[q];
+    }
+    __syncthreads();
+}
+
+template <bool RS>
+__device__ __forceinline__ int32_t ph_runs(const PixCorpus &C, int32_t *tk, int32_t *sc,
+                                           uint32_t blk, int32_t carry);
+
 template <bool RS>
 __device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int32_t *sc,
                                            uint32_t blk, int32_t carry) {
@@ -313,7 +341,15 @@ __device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int3
         tk[k] = i < C.n ? C.tok[i] : SEP;
     }
     __syncthreads();
+    return ph_runs<RS>(C, tk, sc, blk, carry);
+}
+
+// The run start that this thread's first position continues (tk staged)
+template <bool RS>
+__device__ __forceinline__ int32_t ph_runs(const PixCorpus &C, int32_t *tk, int32_t *sc,
+                                           uint32_t blk, int32_t carry) {
     if (!RS) return -1;
+    const uint32_t b0 = blk * PB;
     const uint32_t l0 = threadIdx.x * PH_PER;
     int32_t last = -1;
 #pragma unroll
@@ -336,21 +372,38 @@ __device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int3
     return lane ? max(rs, ex) : rs;
 }
 
+// One pass over the corpus for both halves: 16-bit LDS counters, two per dword (pair
+// p = (x << 8) | y: dword p >> 1, half p & 1).  Every add returns the dword it found; a block
+// whose adds saw some half at >= 0x4000 ends with a sweep that moves every such half into the
+// workgroup's slab entry (global, zeroed by the host), so no half passes 0x4000 + PB.
 __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t, PixCtl *ctl,
-                                                        const int32_t *__restrict__ carry, int half,
+                                                        const int32_t *__restrict__ carry,
                                                         uint32_t *__restrict__ slab,
                                                         unsigned long long *__restrict__ oddxx) {
-    __shared__ uint32_t cnt[PH_HALF];
+    __shared__ uint32_t cnt[32768];
     __shared__ int32_t tk[PB + 1];
     __shared__ int32_t sc[PH_T / 64];
-    __shared__ uint32_t odd[128];
-    for (int i = threadIdx.x; i < PH_HALF; i += PH_T) cnt[i] = 0;
-    if (threadIdx.x < 128) odd[threadIdx.x] = 0;
+    __shared__ uint32_t odd[256];
+    __shared__ uint32_t s_sweep;
+    const uint32_t G = gridDim.x;
+    // (slab index of pair p: the layout of the two half passes, [half][workgroup][x << 7 | y & 127])
+    auto slab_at = [&](uint32_t p) {
+        return ((size_t)((p >> 7) & 1u) * G + blockIdx.x) * PH_HALF + ((p >> 8) << 7) + (p & 127u);
+    };
+    for (int i = threadIdx.x; i < 32768; i += PH_T) cnt[i] = 0;
+    if (threadIdx.x < 256) odd[threadIdx.x] = 0;
+    bool swept = false;
     const uint32_t nblk = (C.n + PB - 1) / PB;
-    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        __syncthreads();   // (tk and sc of the previous block are read; the counters are zero)
-        int32_t rs = ph_span<true>(C, tk, sc, blk, carry[blk]);
+    PhNext nx;
+    if (blockIdx.x < nblk) ph_fetch(C, blockIdx.x, nx);
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += G) {
+        __syncthreads();   // (tk and sc of the previous block are read; so is s_sweep)
+        if (threadIdx.x == 0) s_sweep = 0;
+        ph_put(tk, nx);
+        if (blk + G < nblk) ph_fetch(C, blk + G, nx);
+        int32_t rs = ph_runs<true>(C, tk, sc, blk, carry[blk]);
         const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
+        uint32_t seen = 0;
 #pragma unroll
         for (int k = 0; k < PH_PER; ++k) {
             const uint32_t l = l0 + k, i = i0 + k;
@@ -360,10 +413,10 @@ __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t,
             if ((x | y) < 0) continue;
             const bool uncounted = x == y && ((i - (uint32_t)rs) & 1u);
             if ((x | y) < 256) {
-                if ((y >> 7) != half) continue;
-                atomicAdd(&cnt[ph_local(x, y)], 1u);
-                if (uncounted) atomicAdd(&odd[x & 127], 1u);
-            } else if (half == 0) {
+                const uint32_t p = ((uint32_t)x << 8) | (uint32_t)y;
+                seen |= atomicAdd(&cnt[p >> 1], 1u << ((p & 1u) << 4));
+                if (uncounted) atomicAdd(&odd[x], 1u);
+            } else {
                 const uint32_t s = pix_slot(t, ctl, pix_key(x, y), true, true);
                 if (s == PIX_NONE) {
                     atomicOr(&ctl->err, 9);   // (the table is too full: the host builds a bigger one)
@@ -373,12 +426,35 @@ __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t,
                 if (!uncounted) atomicAdd(&t.cnt[s], 1ull);
             }
         }
+        if (seen & 0xC000C000u) s_sweep = 1;
+        __syncthreads();
+        if (s_sweep) {   // (uniform: read by every thread between the two barriers)
+            swept = true;
+            for (uint32_t w = threadIdx.x; w < 32768u; w += PH_T) {
+                uint32_t v = cnt[w];
+                if (!(v & 0xC000C000u)) continue;
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t c = (v >> (h << 4)) & 0xFFFFu;
+                    if (c < 0x4000u) continue;
+                    atomicAdd(&slab[slab_at(2 * w + h)], c);
+                    v &= ~(0xFFFFu << (h << 4));
+                }
+                cnt[w] = v;
+            }
+        }
     }
     __syncthreads();
-    uint32_t *out = slab + ((size_t)half * gridDim.x + blockIdx.x) * PH_HALF;
-    for (int i = threadIdx.x; i < PH_HALF; i += PH_T) out[i] = cnt[i];
-    if (threadIdx.x < 128 && odd[threadIdx.x])
-        atomicAdd(&oddxx[half * 128 + threadIdx.x], (unsigned long long)odd[threadIdx.x]);
+    for (uint32_t j = threadIdx.x; j < 65536u; j += PH_T) {
+        // (slab order: half, then x, then y & 127)
+        const uint32_t half = j >> 15, loc = j & 32767u;
+        const uint32_t p = ((loc >> 7) << 8) | (half << 7) | (loc & 127u);
+        const uint32_t c = (cnt[p >> 1] >> ((p & 1u) << 4)) & 0xFFFFu;
+        uint32_t *o = slab + ((size_t)half * G + blockIdx.x) * PH_HALF + loc;
+        if (swept) atomicAdd(o, c);
+        else *o = c;
+    }
+    if (threadIdx.x < 256 && odd[threadIdx.x])
+        atomicAdd(&oddxx[threadIdx.x], (unsigned long long)odd[threadIdx.x]);
 }
 
 // One thread per hot pair: the workgroups' counts (G slabs of the pair's half) become their
@@ -566,70 +642,151 @@ __global__ void __launch_bounds__(256) k_pix_hot_xoff(const uint32_t *__restrict
     if ((int)w < G) xoff[w * 256 + x] = w ? part[w - 1] : 0u;
 }
 
+// (staged: a bucket's entries collect in LDS, FX_SB per bucket, and leave as runs of at least
+// FX_FLUSH consecutive entries of this workgroup's range; what does not fit goes straight out)
+constexpr int FX_SB = 32;
+constexpr int FX_FLUSH = 16;
+
+__device__ __forceinline__ void fx_flush(uint2 *__restrict__ stage, uint32_t *cur, uint32_t *lc,
+                                         const uint2 *buf, uint32_t min_n) {
+    // two buckets per wave and round, FX_SB lanes each
+    const int lane = threadIdx.x & 63, half = lane >> 5, sl = lane & 31;
+    for (uint32_t b = (threadIdx.x >> 6) * 2 + half; b < 256; b += (PH_T / 64) * 2) {
+        const uint32_t n = min(lc[b], (uint32_t)FX_SB);
+        if (n >= min_n && n > 0) {
+            const uint32_t at = cur[b];
+            if ((uint32_t)sl < n) stage[at + sl] = buf[b * FX_SB + sl];
+            // (every lane of the half has read cur[b] and lc[b] before lane 0 updates them:
+            // the reads and the writes are one wave's instructions, in program order)
+            if (sl == 0) { cur[b] = at + n; lc[b] = 0; }
+        } else if (sl == 0) {
+            lc[b] = n;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(PH_T) k_pix_fill_x(PixCorpus C, PixTable t, PixBufs B,
                                                      const uint32_t *__restrict__ xoff,
                                                      const uint32_t *__restrict__ bucket,
                                                      uint2 *__restrict__ stage) {
-    __shared__ uint32_t cur[256];
+    __shared__ uint32_t cur[256], lc[256];
+    __shared__ uint2 buf[256 * FX_SB];
     __shared__ int32_t tk[PB + 1];
-    if (threadIdx.x < 256) cur[threadIdx.x] = bucket[threadIdx.x] + xoff[blockIdx.x * 256 + threadIdx.x];
+    if (threadIdx.x < 256) {
+        cur[threadIdx.x] = bucket[threadIdx.x] + xoff[blockIdx.x * 256 + threadIdx.x];
+        lc[threadIdx.x] = 0;
+    }
     const uint32_t nblk = (C.n + PB - 1) / PB;
+    PhNext nx;
+    if (blockIdx.x < nblk) ph_fetch(C, blockIdx.x, nx);
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         __syncthreads();
-        ph_span<false>(C, tk, nullptr, blk, 0);
+        ph_put(tk, nx);
+        if (blk + gridDim.x < nblk) ph_fetch(C, blk + gridDim.x, nx);
         const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
-        // (the hot positions' cursor adds first, all of them, then their stores: one LDS
-        // round trip per PH_PER positions instead of one per position)
+        // (the hot positions' slot claims first, all of them, then their stores)
         uint32_t at[PH_PER];
 #pragma unroll
         for (int k = 0; k < PH_PER; ++k) {
             const int32_t x = tk[l0 + k], y = tk[l0 + k + 1];
             const bool hot = i0 + k + 1 < C.n && (x | y) >= 0 && (x | y) < 256;
-            at[k] = hot ? atomicAdd(&cur[x], 1u) : PIX_NONE;
+            at[k] = hot ? atomicAdd(&lc[x], 1u) : PIX_NONE;
         }
 #pragma unroll
-        for (int k = 0; k < PH_PER; ++k)
-            if (at[k] != PIX_NONE) stage[at[k]] = make_uint2((uint32_t)tk[l0 + k + 1], i0 + k);
+        for (int k = 0; k < PH_PER; ++k) {
+            if (at[k] == PIX_NONE) continue;
+            const int32_t x = tk[l0 + k];
+            const uint2 e = make_uint2((uint32_t)tk[l0 + k + 1], i0 + k);
+            if (at[k] < (uint32_t)FX_SB) buf[x * FX_SB + at[k]] = e;
+            else stage[atomicAdd(&cur[x], 1u)] = e;
+        }
 #pragma unroll
         for (int k = 0; k < PH_PER; ++k) {
             const uint32_t l = l0 + k, i = i0 + k;
             if (i + 1 >= C.n) break;
             const int32_t x = tk[l], y = tk[l + 1];
-            if ((x | y) < 0) continue;
-            if ((x | y) < 256) {
-                continue;   // (above)
-            } else {
-                const uint32_t key = pix_key(x, y);
-                uint32_t s = pix_hash(key) & t.mask;
-                // (present: claimed by the count, within its probe bound)
-                for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
-                if (t.keys[s] != key) continue;
-                B.pool[t.off[s] + atomicAdd(&t.fill[s], 1u)] = i;
-            }
+            if ((x | y) < 256) continue;   // (a separator, or hot: above)
+            const uint32_t key = pix_key(x, y);
+            uint32_t s = pix_hash(key) & t.mask;
+            // (present: claimed by the count, within its probe bound)
+            for (int p = 0; p < PIX_PROBE && t.keys[s] != key; ++p) s = (s + 1) & t.mask;
+            if (t.keys[s] != key) continue;
+            B.pool[t.off[s] + atomicAdd(&t.fill[s], 1u)] = i;
         }
+        __syncthreads();
+        fx_flush(stage, cur, lc, buf, FX_FLUSH);
     }
+    __syncthreads();
+    fx_flush(stage, cur, lc, buf, 1);
 }
+
+// (staged as in k_pix_fill_x: a segment's positions collect in LDS, FY_SB per segment, and
+// leave as runs of at least FY_FLUSH; the stage is read a round ahead)
+constexpr int FY_SB = 64;
+constexpr int FY_FLUSH = 32;
+constexpr int FY_PER = 8;   // entries per thread and round
 
 __global__ void __launch_bounds__(1024) k_pix_fill_y(PixBufs B, const uint32_t *__restrict__ hseg,
                                                      const uint32_t *__restrict__ bucket,
                                                      const uint2 *__restrict__ stage) {
-    __shared__ uint32_t cur[256];
+    __shared__ uint32_t cur[256], lc[256];
+    __shared__ uint32_t buf[256 * FY_SB];
     const uint32_t x = blockIdx.x;
-    if (threadIdx.x < 256) cur[threadIdx.x] = hseg[x * 256 + threadIdx.x];
-    __syncthreads();
-    const uint32_t b0 = bucket[x], b1 = bucket[x + 1];
-    // (4 entries per thread and round: their loads, cursor adds and stores each issued together)
-    for (uint32_t j0 = b0 + threadIdx.x; j0 < b1; j0 += 4 * 1024) {
-        uint2 e[4];
-        uint32_t at[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) e[k] = j0 + 1024 * k < b1 ? stage[j0 + 1024 * k] : make_uint2(256u, 0u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) at[k] = e[k].x < 256u ? atomicAdd(&cur[e[k].x], 1u) : PIX_NONE;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (at[k] != PIX_NONE) B.pool[at[k]] = e[k].y;
+    if (threadIdx.x < 256) {
+        cur[threadIdx.x] = hseg[x * 256 + threadIdx.x];
+        lc[threadIdx.x] = 0;
     }
+    const uint32_t b0 = bucket[x], b1 = bucket[x + 1];
+    uint2 nx[FY_PER];
+    auto fetch = [&](uint32_t r0) {
+#pragma unroll
+        for (int k = 0; k < FY_PER; ++k) {
+            const uint32_t j = r0 + threadIdx.x + 1024 * k;
+            if (j < b1) {
+                const unsigned long long v = __builtin_nontemporal_load(
+                    reinterpret_cast<const unsigned long long *>(stage + j));
+                nx[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+            } else {
+                nx[k] = make_uint2(256u, 0u);
+            }
+        }
+    };
+    // one segment per wave and round, a lane per buffered position
+    auto flush = [&](uint32_t min_n) {
+        const int lane = threadIdx.x & 63;
+        for (uint32_t y = threadIdx.x >> 6; y < 256; y += 16) {
+            const uint32_t n = min(lc[y], (uint32_t)FY_SB);
+            if (n >= min_n && n > 0) {
+                const uint32_t at = cur[y];
+                if ((uint32_t)lane < n) B.pool[at + lane] = buf[y * FY_SB + lane];
+                // (the wave's reads of cur[y] and lc[y] precede lane 0's writes, in program order)
+                if (lane == 0) { cur[y] = at + n; lc[y] = 0; }
+            } else if (lane == 0) {
+                lc[y] = n;
+            }
+        }
+    };
+    fetch(b0);
+    for (uint32_t r0 = b0; r0 < b1; r0 += FY_PER * 1024) {
+        __syncthreads();   // (the last flush is done)
+        uint2 e[FY_PER];
+        uint32_t at[FY_PER];
+#pragma unroll
+        for (int k = 0; k < FY_PER; ++k) e[k] = nx[k];
+        fetch(r0 + FY_PER * 1024);
+#pragma unroll
+        for (int k = 0; k < FY_PER; ++k) at[k] = e[k].x < 256u ? atomicAdd(&lc[e[k].x], 1u) : PIX_NONE;
+#pragma unroll
+        for (int k = 0; k < FY_PER; ++k) {
+            if (at[k] == PIX_NONE) continue;
+            if (at[k] < (uint32_t)FY_SB) buf[e[k].x * FY_SB + at[k]] = e[k].y;
+            else B.pool[atomicAdd(&cur[e[k].x], 1u)] = e[k].y;
+        }
+        __syncthreads();
+        flush(FY_FLUSH);
+    }
+    __syncthreads();
+    flush(1);
 }
 
 // Block maxima: of every block (build), or recomputed for the blocks whose max entry fell

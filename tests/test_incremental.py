@@ -111,6 +111,33 @@ def test_zipf_words_match_the_stream():
     assert np.array_equal(a.read_corpus()[0], b.read_corpus()[0])
 
 
+def test_index_build_count_sweeps():
+    """Per-workgroup counts far past the index build's 16-bit LDS counters (k_pix_hot_count: the
+    block-end sweeps into the slab): 24 MiB of 'ab' repeats, runs of 'z' of every parity and
+    random bytes, against the streaming mode."""
+    rng = np.random.default_rng(77)
+    parts = []
+    for kind, n in zip(rng.choice(3, 60000, p=[0.55, 0.3, 0.15]), rng.integers(40, 1200, 60000)):
+        if kind == 0:
+            parts.append(np.resize(np.frombuffer(b'ab', np.uint8), n))
+        elif kind == 1:
+            parts.append(np.full(n, ord('z'), np.uint8))
+        else:
+            parts.append(rng.integers(0, 256, n, dtype=np.uint8))
+    data = np.concatenate(parts)[:24 << 20]
+    a = pkg.Engine(0)
+    a.add_latin1(data, sample_bytes=1 << 20)
+    b = pkg.Engine(0)
+    b.add_latin1(data, sample_bytes=1 << 20)
+    b.set_mode('incremental')
+    b.stats_enable(True)
+    want = a.merge_until(0, 2, 40)
+    got = b.merge_until(0, 2, 40)
+    assert got == want
+    assert b.stats()['pix_merges'] > 0
+    assert np.array_equal(a.read_corpus()[0], b.read_corpus()[0])
+
+
 @pytest.mark.parametrize('fill', ['two_level', 'pairs'])
 @pytest.mark.parametrize('seed', range(3))
 def test_index_build_fill_forms(fill, seed, monkeypatch):
