@@ -1960,7 +1960,7 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
                 k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
                 k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
                 k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
-                k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, c->d_len16, P->d_log);
+                k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, P->d_log);
             }
             HIP_TRY(hipGetLastError());
             PixCtl *h = P->h_ctl;
@@ -1999,7 +1999,7 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
                     out_abw[3 * n + 2] = W;
                 }
             }
-            c->len16_lo = base + nd;   // k_pix_apply wrote the new lengths on the device
+            c->len16_lo = base + nd;   // pix_commit wrote the new lengths on the device
             if (status == PIX_DONE) break;
             if (status == PIX_RUN || status == PIX_PAUSE) continue;
             if (c->stats_on) c->stats.pix_host += 1;

@@ -49,7 +49,7 @@ struct PixCorpus {
 };
 
 struct PixTable {
-    const int32_t *len16;    // UTF-16 lengths (max_length filter)
+    int32_t *len16;          // UTF-16 lengths (max_length filter)
     long long ml;            // max_length of this index's selections
     uint32_t *keys;
     unsigned long long *cnt;
@@ -187,12 +187,13 @@ __device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32
 //   k_pix_scan_max     the run start each block's first position continues (exclusive max-scan)
 //   k_pix_hot_count    per valid pair position: list length + 1 and, for (x, x) at an odd offset
 //                      of its run, one uncounted occurrence (core.ts:285-290).  Hot pairs (both
-//                      ids < 256) go to a dense LDS counter per workgroup, one half of the 65536
-//                      hot pairs per pass (second id >> 7), dumped as the workgroup's slab; other
-//                      pairs claim their table slot and count there (global atomics)
+//                      ids < 256) go to 65536 16-bit LDS counters per workgroup (one pass),
+//                      dumped as the workgroup's slab; other pairs claim their table slot and
+//                      count there (global atomics)
 //   k_pix_hot_scan     per hot pair: its total, and each workgroup's exclusive offset (in place)
 //   k_pix_hot_claim    a table slot per hot pair that occurs, with its length and count
 //   k_pix_build_alloc  a pool segment per pair (one pool atomic per wave)
+//   (k_pix_hot_seg, k_pix_hot_xoff, k_pix_fill_x, k_pix_fill_y: the two-level fill, below)
 //   k_pix_hot_fill     every position into its pair's segment: hot pairs through per-workgroup
 //                      LDS cursors (segment + the workgroup's offset), the others through the
 //                      pair's global fill counter
@@ -868,7 +869,7 @@ enum PixTie { PIX_TIE_NONE = 0, PIX_TIE_SCAN = 1, PIX_TIE_DECIDED = 2 };
 
 // The merge of pair slot s (key `key`, list length len): vocabulary and table-room checks, then
 // the decision every later kernel reads.  (Thread 0 of k_pix_select.)
-__device__ void pix_commit(PixCtl *ctl, uint32_t s, uint32_t key, uint32_t len) {
+__device__ void pix_commit(const PixTable &t, PixCtl *ctl, uint32_t s, uint32_t key, uint32_t len) {
     if (ctl->next_id >= ctl->max_id) {
         ctl->status = PIX_HOST;                                       // vocabulary limit
         ctl->err = 5;
@@ -880,11 +881,15 @@ __device__ void pix_commit(PixCtl *ctl, uint32_t s, uint32_t key, uint32_t len) 
         ctl->err = 6;
         return;
     }
-    ctl->c = ctl->next_id;
+    const int32_t c = ctl->next_id, a = (int32_t)(key >> 16), b = (int32_t)(key & 0xFFFF);
+    ctl->c = c;
     ctl->pair_slot = s;
-    ctl->a = (int32_t)(key >> 16);
-    ctl->b = (int32_t)(key & 0xFFFF);
+    ctl->a = a;
+    ctl->b = b;
     ctl->tie = PIX_TIE_NONE;
+    // c's length before this merge's new pairs are ranked (their block maxima in k_pix_alloc and
+    // k_pix_apply read it under max_length)
+    t.len16[c] = t.len16[a] + t.len16[b];                             // core.ts:318
 }
 
 // Best key, candidates (every pair sharing it), the decision.  One block of 1024.
@@ -912,7 +917,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
             const uint32_t sl = ctl->pair_slot;
             ctl->n_sites = ctl->n_ent = ctl->n_dblocks = ctl->n_dsuper = 0;
             ctl->n_check = 0;
-            pix_commit(ctl, sl, t.keys[sl], t.len[sl]);
+            pix_commit(t, ctl, sl, t.keys[sl], t.len[sl]);
         }
         return;
     }
@@ -1011,7 +1016,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         ctl->best = best;
         ctl->W = (unsigned long long)W;
         if (nc == 1) {
-            pix_commit(ctl, cs[0], cs_key[0], cs_len[0]);
+            pix_commit(t, ctl, cs[0], cs_key[0], cs_len[0]);
         } else {
             // tied: k_pix_sites scans the candidates' lists this iteration
             for (uint32_t j = 0; j < nc; ++j) {
@@ -1360,7 +1365,7 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
 // pairs' slots into their segments; the maxima of the touched blocks.  The merge is then logged;
 // W must equal the sites found.
 __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl,
-                                                   int32_t *len16, long long *log) {
+                                                   long long *log) {
     if (ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE) return;   // (a tie scan: no merge)
     const unsigned long long W = ctl->W;
     if (ctl->n_sites != W || (ctl->a == ctl->b && ctl->n_check != W)) {
@@ -1395,7 +1400,6 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         log[3 * k] = ctl->a;
         log[3 * k + 1] = ctl->b;
         log[3 * k + 2] = (long long)W;
-        len16[c] = len16[ctl->a] + len16[ctl->b];                      // core.ts:318
         ctl->n_done = k + 1;
         ctl->next_id = c + 1;
     }

@@ -111,6 +111,34 @@ def test_zipf_words_match_the_stream():
     assert np.array_equal(a.read_corpus()[0], b.read_corpus()[0])
 
 
+@pytest.mark.parametrize('ml', [3, 5])
+def test_max_length_new_pairs_stay_on_the_index(ml):
+    """Under max_length the new token's length is known before its pairs are ranked (pix_commit
+    writes it; k_pix_alloc lifts the block maxima from it): a new pair too long to merge must not
+    raise its block's max, which would leave k_pix_select without a candidate (a hand-off to the
+    stream and a rebuilt index).  'ab' repeats make (c, c) the most frequent new pair."""
+    rng = np.random.default_rng(5 + ml)
+    samples = []
+    for _ in range(60):
+        n = int(rng.integers(500, 3000))
+        s = np.resize(np.array([0, 1], np.int32), n)
+        noise = rng.random(n) < 0.15
+        s[noise] = rng.integers(2, 20, int(noise.sum()))
+        samples.append(s)
+    len16 = [1] * 20
+    ids, off = _flat(samples)
+    st = OracleState(ids, off, len16, 20)
+    e = make_engine(samples, len16)
+    e.set_mode('incremental')
+    e.stats_enable(True)
+    want = st.merge_until(ml, 2, 40)
+    got = e.merge_until(ml, 2, 40)
+    assert got == want, (got[:4], want[:4])
+    assert e.samples() == st.samples()
+    s = e.stats()
+    assert s['pix_merges'] == len(got) and s['pix_host'] == 0, s
+
+
 def test_index_build_count_sweeps():
     """Per-workgroup counts far past the index build's 16-bit LDS counters (k_pix_hot_count: the
     block-end sweeps into the slab): 24 MiB of 'ab' repeats, runs of 'z' of every parity and
