@@ -21,9 +21,9 @@
 //   k_pix_sites    the merge sites from the (a, b) list and the count changes around them (for
 //                  a == b the runs, walked from their heads: sites at even offsets, replaceAll's
 //                  left-to-right rule); the new adjacencies, all of which contain c
-//   k_pix_alloc    segments for the new pairs
+//   k_pix_alloc    segments for the new pairs, the maxima of the blocks whose max entry fell
 //   k_pix_apply    tokens and links (the only kernel that changes the corpus), the new pairs'
-//                  slots into their segments, the maxima of the blocks whose max entry fell
+//                  slots into their segments
 // Anything the index cannot do in bounded work (a run or chain longer than PIX_WALK, a full
 // buffer, more than MAX_CAND tied pairs) sets PIX_HOST before k_pix_apply: the corpus is still
 // that of the last completed merge, and the host takes the iteration on the streaming path.
@@ -804,10 +804,13 @@ __global__ void __launch_bounds__(256) k_pix_bmax_all(PixTable t) {
     }
 }
 
-__device__ __forceinline__ void pix_bmax_dirty(const PixTable &t, const PixBufs &B, PixCtl *ctl) {
+// (rank: this workgroup's place in the grid; k_pix_alloc counts from the end, where the
+// workgroups without entries are)
+__device__ __forceinline__ void pix_bmax_dirty(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                               uint32_t rank) {
     const int lane = threadIdx.x & 63;
     const uint32_t nb = min(ctl->n_dblocks, t.nblocks);
-    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nb; i += gridDim.x * 4) {
+    for (uint32_t i = rank * 4 + (threadIdx.x >> 6); i < nb; i += gridDim.x * 4) {
         const uint32_t blk = B.dblocks[i];
         unsigned long long m = 0;
         for (int k = lane; k < PIX_B; k += 64) m = max(m, pix_sel(t, blk * PIX_B + k));
@@ -1107,16 +1110,15 @@ __device__ void pix_tie_scan(const PixCorpus &C, const PixTable &t, const PixBuf
 //   a chain of m consecutive sites becomes m c's: floor(m/2) pairs (c, c).
 // (two lanes per site: the even one takes the left adjacency and the chain, the odd one the right
 // adjacency; each writes its entry, [2 idx] / [2 idx + 1], or an empty one)
+// (l = prv[p], tl its token, ll = prv[l]: loaded by the caller ahead of the site index)
 __device__ void pix_site_left(const PixCorpus &C, const PixTable &t, const PixBufs &B,
                               PixCtl *ctl, uint32_t p, uint32_t q, uint32_t idx, int32_t a,
-                              int32_t b, int32_t c) {
-    const uint32_t l = C.prv[p];
-    const int32_t tl = l != PIX_NONE ? C.tok[l] : SEP;
+                              int32_t b, int32_t c, uint32_t l, int32_t tl, uint32_t ll) {
     bool done = false;
-    if (tl == b && pix_tok_is(C, C.prv[l], a)) {
+    if (tl == b && pix_tok_is(C, ll, a)) {
         // chained to the site before: (b, a) is lost, (c, c) from that site's slot
         pix_add(t, B, ctl, b, a, -1);
-        pix_entry(t, B, ctl, c, c, C.prv[l], 0, 2 * idx);
+        pix_entry(t, B, ctl, c, c, ll, 0, 2 * idx);
         done = true;
     } else {
         if (tl >= 0) {
@@ -1155,13 +1157,12 @@ __device__ void pix_site_left(const PixCorpus &C, const PixTable &t, const PixBu
     if (!done && 2 * idx < B.ent_cap) B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
 }
 
+// (r = nxt[q], tr its token, rr = nxt[r]: loaded by the caller ahead of the site index)
 __device__ void pix_site_right(const PixCorpus &C, const PixTable &t, const PixBufs &B,
                                PixCtl *ctl, uint32_t p, uint32_t q, uint32_t idx, int32_t a,
-                               int32_t b, int32_t c) {
-    const uint32_t r = C.nxt[q];
-    const int32_t tr = r != PIX_NONE ? C.tok[r] : SEP;
+                               int32_t b, int32_t c, uint32_t r, int32_t tr, uint32_t rr) {
     // (a site starting at r takes this adjacency as its left one)
-    const bool rchain = tr == a && pix_tok_is(C, C.nxt[r], b);
+    const bool rchain = tr == a && pix_tok_is(C, rr, b);
     if (!rchain && tr >= 0) {
         if (tr == b) {
             uint32_t L = 1, x = r;
@@ -1226,12 +1227,23 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
         for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x; g0 < total;
              g0 += (uint64_t)gridDim.x * blockDim.x) {
             const uint64_t g = g0 + threadIdx.x;
-            uint32_t p = 0, q = PIX_NONE;
+            uint32_t p = 0, q = PIX_NONE, x = PIX_NONE, xx = PIX_NONE;
+            int32_t tx = SEP;
             bool valid = false;
             if (g < total) {
+                // (every load the lane's adjacency needs, issued before the site index: the
+                // neighbour x (prv[p] / nxt[q]), its token and its own neighbour xx)
                 p = B.pool[off + (uint32_t)(g >> 1)];
+                const int32_t tp = C.tok[p];
                 q = C.nxt[p];
-                valid = C.tok[p] == a && pix_tok_is(C, q, b);
+                if (role == 0) x = C.prv[p];
+                const int32_t tq = q != PIX_NONE ? C.tok[q] : SEP;
+                if (role == 1 && q != PIX_NONE) x = C.nxt[q];
+                if (x != PIX_NONE) {
+                    tx = C.tok[x];
+                    xx = role == 0 ? C.prv[x] : C.nxt[x];
+                }
+                valid = tp == a && tq == b;
             }
             // one atomic per block for the site indices
             const unsigned long long m0 = __ballot(valid && role == 0);
@@ -1253,9 +1265,9 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
             }
             if (role == 0) {
                 B.sites[idx] = p;
-                pix_site_left(C, t, B, ctl, p, q, idx, a, b, c);
+                pix_site_left(C, t, B, ctl, p, q, idx, a, b, c, x, tx, xx);
             } else {
-                pix_site_right(C, t, B, ctl, p, q, idx, a, b, c);
+                pix_site_right(C, t, B, ctl, p, q, idx, a, b, c, x, tx, xx);
             }
         }
         return;
@@ -1359,10 +1371,15 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
             atomicMax(&t.sbmax[blk / PIX_SB], sel);
         }
     }
+    // The blocks whose max fell (the counts are final after k_pix_sites, and c's length was set
+    // by pix_commit).  A new pair lifted above keeps its block's max either way: the recompute
+    // reads its final count, so its store is >= the lift.  (No merge, no dirty block: k_pix_select
+    // zeroes n_dblocks.)
+    pix_bmax_dirty(t, B, ctl, gridDim.x - 1 - blockIdx.x);
 }
 
 // The corpus rewrite: c at every site, its right slot merged away, the links around it; the new
-// pairs' slots into their segments; the maxima of the touched blocks.  The merge is then logged;
+// pairs' slots into their segments.  The merge is then logged;
 // W must equal the sites found.
 __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixBufs B, PixCtl *ctl,
                                                    long long *log) {
@@ -1394,7 +1411,6 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
         B.pool[t.off[e.x] + k] = e.y & ~PIX_OWNER;
     }
-    pix_bmax_dirty(t, B, ctl);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const long long k = ctl->n_done;
         log[3 * k] = ctl->a;
