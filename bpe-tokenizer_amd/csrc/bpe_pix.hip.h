@@ -121,12 +121,27 @@ __device__ __forceinline__ void pix_fail(PixCtl *ctl, int why) {
     if (atomicCAS(&ctl->status, PIX_RUN, PIX_HOST) == PIX_RUN) ctl->err = why;
 }
 
+// A pair's first probe: its home slot and the key found there, loaded ahead (a site issues the
+// first probes of both pairs it touches together).  Keys are only claimed during a merge, never
+// removed, so a key loaded ahead stays; an empty slot loaded ahead is re-checked by the claim.
+struct PixProbe {
+    uint32_t s, k;
+};
+
+__device__ __forceinline__ PixProbe pix_probe(const PixTable &t, uint32_t key) {
+    const uint32_t s = pix_hash(key) & t.mask;
+    return {s, t.keys[s]};
+}
+
 // find-or-claim the slot of a pair; PIX_NONE when the probe sequence is exhausted
 __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uint32_t key,
-                                             bool claim, bool count_claim = false) {
-    uint32_t s = pix_hash(key) & t.mask;
-    for (int i = 0; i < PIX_PROBE; ++i, s = (s + 1) & t.mask) {
-        const uint32_t k = t.keys[s];
+                                             bool claim, bool count_claim, PixProbe pr) {
+    uint32_t s = pr.s, k = pr.k;
+    for (int i = 0; i < PIX_PROBE; ++i) {
+        if (i) {
+            s = (s + 1) & t.mask;
+            k = t.keys[s];
+        }
         if (k == key) return s;
         if (k == PIX_NONE) {
             if (!claim) return PIX_NONE;
@@ -141,25 +156,39 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
     return PIX_NONE;
 }
 
+__device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uint32_t key,
+                                             bool claim, bool count_claim = false) {
+    return pix_slot(t, ctl, key, claim, count_claim, pix_probe(t, key));
+}
+
 // Count change of an existing or new pair, keeping the block maxima exact.  Only new pairs (they
 // all contain c) rise: k_pix_alloc lifts their block's and superblock's max once per pair.  A fall
 // only matters to the entry that was its block's max, whose block is then recomputed after the
-// merge (k_pix_apply).
+// merge's count changes (k_pix_alloc).  (The block max is read beside the add: no block max
+// changes while k_pix_sites runs.)
 __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
-                                            int32_t u, int32_t v, long long d) {
-    const uint32_t key = pix_key(u, v);
-    const uint32_t s = pix_slot(t, ctl, key, true);
+                                            uint32_t key, long long d, PixProbe pr) {
+    const uint32_t s = pix_slot(t, ctl, key, true, false, pr);
     if (s == PIX_NONE) {
         pix_fail(ctl, 1);
         return s;
     }
     if (d == 0) return s;
-    const unsigned long long old = atomicAdd(&t.cnt[s], (unsigned long long)d);
     if (d < 0) {
+        const unsigned long long bm = t.bmax[s / PIX_B];
+        const unsigned long long old = atomicAdd(&t.cnt[s], (unsigned long long)d);
         const unsigned long long sel = pix_sel_of(t, key, old);
-        if (sel && sel >= t.bmax[s / PIX_B]) pix_mark(t, B, ctl, s);
+        if (sel && sel >= bm) pix_mark(t, B, ctl, s);
+    } else {
+        atomicAdd(&t.cnt[s], (unsigned long long)d);
     }
     return s;
+}
+
+__device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                            int32_t u, int32_t v, long long d) {
+    const uint32_t key = pix_key(u, v);
+    return pix_add(t, B, ctl, key, d, pix_probe(t, key));
 }
 
 // A new adjacency (u, v) at slot pos (u or v is c): its count, one more slot in its segment, the
@@ -167,14 +196,21 @@ __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B,
 // opened the pair's segment carries PIX_OWNER: k_pix_alloc places the segment from it.
 constexpr uint32_t PIX_OWNER = 0x80000000u;
 __device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
-                                          int32_t u, int32_t v, uint32_t pos, long long d,
-                                          uint32_t e = ~0u) {
-    const uint32_t s = pix_add(t, B, ctl, u, v, d);
+                                          uint32_t key, uint32_t pos, long long d, uint32_t e,
+                                          PixProbe pr) {
+    const uint32_t s = pix_add(t, B, ctl, key, d, pr);
     if (s == PIX_NONE) return;
     const uint32_t owner = atomicAdd(&t.len[s], 1u) == 0u ? PIX_OWNER : 0u;
     if (e == ~0u) e = atomicAdd(&ctl->n_ent, 1u);
     if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos | owner);
     else pix_fail(ctl, 3);
+}
+
+__device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                          int32_t u, int32_t v, uint32_t pos, long long d,
+                                          uint32_t e = ~0u) {
+    const uint32_t key = pix_key(u, v);
+    pix_entry(t, B, ctl, key, pos, d, e, pix_probe(t, key));
 }
 
 __device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32_t x) {
@@ -1114,47 +1150,56 @@ __device__ void pix_tie_scan(const PixCorpus &C, const PixTable &t, const PixBuf
 __device__ void pix_site_left(const PixCorpus &C, const PixTable &t, const PixBufs &B,
                               PixCtl *ctl, uint32_t p, uint32_t q, uint32_t idx, int32_t a,
                               int32_t b, int32_t c, uint32_t l, int32_t tl, uint32_t ll) {
-    bool done = false;
-    if (tl == b && pix_tok_is(C, ll, a)) {
-        // chained to the site before: (b, a) is lost, (c, c) from that site's slot
-        pix_add(t, B, ctl, b, a, -1);
-        pix_entry(t, B, ctl, c, c, ll, 0, 2 * idx);
-        done = true;
-    } else {
-        if (tl >= 0) {
-            if (tl == a) {
-                uint32_t L = 1, x = l;
-                while (pix_tok_is(C, x, a)) {
-                    ++L;
-                    x = C.prv[x];
-                    if (L > (uint32_t)PIX_WALK) {
-                        pix_fail(ctl, 13);
-                        return;
-                    }
-                }
-                if ((L & 1u) == 0) pix_add(t, B, ctl, a, a, -1);
-            } else {
-                pix_add(t, B, ctl, tl, a, -1);
-            }
-            pix_entry(t, B, ctl, tl, c, l, 1, 2 * idx);
-            done = true;
-        }
-        // the head of a chain: its length m, floor(m/2) pairs (c, c)
-        uint32_t m = 1, xq = q;
-        for (;;) {
-            const uint32_t xr = C.nxt[xq];
-            if (!pix_tok_is(C, xr, a)) break;
-            const uint32_t xrq = C.nxt[xr];
-            if (!pix_tok_is(C, xrq, b)) break;
-            xq = xrq;
-            if (++m > (uint32_t)PIX_WALK) {
-                pix_fail(ctl, 14);
-                return;
-            }
-        }
-        if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
+    // the two pairs this adjacency touches (k1 loses one, k2 is new), their first probes issued
+    // together
+    const bool chained = tl == b && pix_tok_is(C, ll, a);
+    const uint32_t k1 = chained ? pix_key(b, a) : pix_key(tl, a);
+    const uint32_t k2 = chained ? pix_key(c, c) : pix_key(tl, c);
+    PixProbe p1{0, PIX_NONE}, p2{0, PIX_NONE};
+    if (chained || tl >= 0) {
+        p1 = pix_probe(t, k1);
+        p2 = pix_probe(t, k2);
     }
-    if (!done && 2 * idx < B.ent_cap) B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
+    if (chained) {
+        // chained to the site before: (b, a) is lost, (c, c) from that site's slot
+        pix_add(t, B, ctl, k1, -1, p1);
+        pix_entry(t, B, ctl, k2, ll, 0, 2 * idx, p2);
+        return;
+    }
+    // the head of a chain: its length m, floor(m/2) pairs (c, c)
+    uint32_t m = 1, xq = q;
+    for (;;) {
+        const uint32_t xr = C.nxt[xq];
+        if (!pix_tok_is(C, xr, a)) break;
+        const uint32_t xrq = C.nxt[xr];
+        if (!pix_tok_is(C, xrq, b)) break;
+        xq = xrq;
+        if (++m > (uint32_t)PIX_WALK) {
+            pix_fail(ctl, 14);
+            return;
+        }
+    }
+    if (tl >= 0) {
+        if (tl == a) {
+            // (k1 = (a, a): one fewer when the run of a's ending at l had even length)
+            uint32_t L = 1, x = l;
+            while (pix_tok_is(C, x, a)) {
+                ++L;
+                x = C.prv[x];
+                if (L > (uint32_t)PIX_WALK) {
+                    pix_fail(ctl, 13);
+                    return;
+                }
+            }
+            if ((L & 1u) == 0) pix_add(t, B, ctl, k1, -1, p1);
+        } else {
+            pix_add(t, B, ctl, k1, -1, p1);
+        }
+        pix_entry(t, B, ctl, k2, l, 1, 2 * idx, p2);
+    } else if (2 * idx < B.ent_cap) {
+        B.ent[2 * idx] = make_uint2(PIX_NONE, 0);
+    }
+    if (m >= 2) pix_add(t, B, ctl, c, c, (long long)(m / 2));
 }
 
 // (r = nxt[q], tr its token, rr = nxt[r]: loaded by the caller ahead of the site index)
@@ -1164,6 +1209,8 @@ __device__ void pix_site_right(const PixCorpus &C, const PixTable &t, const PixB
     // (a site starting at r takes this adjacency as its left one)
     const bool rchain = tr == a && pix_tok_is(C, rr, b);
     if (!rchain && tr >= 0) {
+        const uint32_t k1 = pix_key(b, tr), k2 = pix_key(c, tr);   // (tr == b: k1 = (b, b))
+        const PixProbe p1 = pix_probe(t, k1), p2 = pix_probe(t, k2);
         if (tr == b) {
             uint32_t L = 1, x = r;
             while (pix_tok_is(C, x, b)) {
@@ -1174,11 +1221,11 @@ __device__ void pix_site_right(const PixCorpus &C, const PixTable &t, const PixB
                     return;
                 }
             }
-            if ((L & 1u) == 0) pix_add(t, B, ctl, b, b, -1);
+            if ((L & 1u) == 0) pix_add(t, B, ctl, k1, -1, p1);
         } else {
-            pix_add(t, B, ctl, b, tr, -1);
+            pix_add(t, B, ctl, k1, -1, p1);
         }
-        pix_entry(t, B, ctl, c, tr, p, 1, 2 * idx + 1);
+        pix_entry(t, B, ctl, k2, p, 1, 2 * idx + 1, p2);
     } else if (2 * idx + 1 < B.ent_cap) {
         B.ent[2 * idx + 1] = make_uint2(PIX_NONE, 0);
     }
