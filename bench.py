@@ -40,6 +40,41 @@ def cpu_model():
     return 'unknown'
 
 
+def cpu_share():
+    """The host cores this process may use, and why: the cgroup CPU quota (cgroup v2 cpu.max or
+    v1 cfs_quota_us / cfs_period_us), the CPU affinity mask, and OMP_NUM_THREADS (the GPU pool sets
+    it to the box's CPU share for one GPU and asks jobs to keep within it).  The multi-thread leg
+    runs on the smallest of the three."""
+    info = {'affinity': len(os.sched_getaffinity(0)), 'nproc': os.cpu_count()}
+    quota = None
+    try:
+        q, p = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        info['cgroup_cpu_max'] = '%s %s' % (q, p)
+        if q != 'max':
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+            p = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            info['cgroup_cfs_quota'] = '%d %d' % (q, p)
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            info['cgroup_cpu_max'] = 'unreadable'
+    info['quota_cores'] = quota
+    omp = int(os.environ.get('OMP_NUM_THREADS') or 0) or None
+    info['omp_num_threads'] = omp
+    limits = {'affinity': info['affinity']}
+    if quota:
+        limits['cgroup quota'] = max(1, int(quota))
+    if omp:
+        limits['OMP_NUM_THREADS (the pool\'s CPU share per GPU)'] = omp
+    why = min(limits, key=limits.get)
+    info['threads'] = limits[why]
+    info['threads_bound_by'] = why
+    return info
+
+
 def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
     """The multi-threaded CPU restatement (oracle/bpe_cpu_mt.cc: the same full recount per merge
     as the reference and the GPU engine, pinned to the reference's fixtures) on a bounded sample
@@ -59,7 +94,8 @@ def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
     ids = lut[data]
     del data
     off = np.arange(0, n + 1, 1 << 20, dtype=np.int64)
-    threads = int(os.environ.get('OMP_NUM_THREADS') or 0) or len(os.sched_getaffinity(0))
+    share = cpu_share()
+    threads = share['threads']
 
     def timed(T, budget):
         st = CpuMT(ids, off, [1] * nt, nt, threads=T, extra=1 << 14)
@@ -80,8 +116,7 @@ def cpu_baseline(sample_mib, budget_s, corpus='uniform'):
     v_1, it_1, dt_1, _ = timed(1, budget_s * 0.4)
     return {'value': v_mt, 'unit': 'pair-scans/s', 'cores': used, 'kind': 'port',
             'value_1_thread': v_1,
-            'host': {'cpu_model': cpu_model(), 'nproc': os.cpu_count(),
-                     'affinity': len(os.sched_getaffinity(0))},
+            'host': dict(share, cpu_model=cpu_model()),
             'sample': '%d MiB of the same corpus stream (1 MiB samples), mergeUntil from the first '
                       'merge: %d merges in %.1f s on %d threads, %d merges in %.1f s on 1 thread; '
                       'oracle/bpe_cpu_mt.cc (full recount per merge, as the reference)'

@@ -2702,6 +2702,14 @@ int bpe_recount(bpe_ctx *c) {
     return run_pass(c, false, 0, 0, 0, nullptr);
 }
 
+// (internal, bpe_multi.cpp) the corpus of one shard changed outside the rank loop: every shard
+// leaves the replicated global tables, so the next batch starts from the table state on all alike
+int bpe_leave_global(bpe_ctx *c) {
+    if (!c || c->multi) return fail(BPE_ERR_ARG, "bpe native: bad shard context");
+    leave_global(c);
+    return BPE_OK;
+}
+
 // (debug: BPE_DEBUG_GLOBAL, bpe_multi.cpp) this context's maintained tables: the hot bins
 // (HOT_BINS u64 into hot) and the cold table's dense entries (up to cap; *n = n_used)
 int bpe_debug_tables(bpe_ctx *c, uint64_t *hot, uint32_t *keys, uint64_t *counts, int64_t cap,

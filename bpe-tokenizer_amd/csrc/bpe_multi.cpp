@@ -113,7 +113,9 @@ int nccl_check(bpe_multi *m, ncclResult_t r, const char *what) {
 
 // In-place all-reduce of count u64 per shard (SUM or MAX), ordered on the shards' streams.
 int all_reduce(bpe_multi *m, std::vector<unsigned long long *> &buf, size_t count, bool max) {
-    if (m->n == 1) return BPE_OK;
+    // (one shard: nothing to add, but an RCCL context still makes the call, so that the RCCL leg
+    // of the rank loop runs on a one-GPU box as it does on eight)
+    if (m->n == 1 && m->reduce != BPE_REDUCE_RCCL) return BPE_OK;
     if (m->reduce == BPE_REDUCE_RCCL) {
         MTRY(nccl_check(m, m->rccl.group_start(), "ncclGroupStart"));
         for (int r = 0; r < m->n; ++r) {
@@ -240,7 +242,7 @@ int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
     if (hipHostMalloc((void **)&m->h_buf, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&m->h_sum, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_OOM, "bpe native: pinned host buffers"));
-    if (reduce == BPE_REDUCE_RCCL && n > 1) {
+    if (reduce == BPE_REDUCE_RCCL) {   // (one device too: a 1-rank communicator)
         int rc = load_rccl(m->rccl);
         if (rc) return bail(rc);
         m->comms.assign(n, nullptr);
@@ -285,6 +287,18 @@ int multi_set_token_len16(bpe_multi *m, int32_t id, int32_t len16) {
 
 int check_vocab(bpe_multi *m, int32_t *n_tokens);
 
+extern "C" int bpe_leave_global(bpe_ctx *c);
+
+// A sample added to the last shard reseals only that shard, which drops its replicated global
+// tables (the maintained state).  Every shard must leave that state alike, or the next batch's
+// exchange sizes differ between shards: the next batch then starts from the table state.
+int drop_global(bpe_multi *m) {
+    m->maintained = false;
+    m->heavy_streak = 0;
+    for (auto s : m->sh) MTRY(bpe_leave_global(s));
+    return BPE_OK;
+}
+
 int multi_num_tokens(bpe_multi *m, int32_t *n) { return bpe_num_tokens(m->sh[0], n); }
 
 int multi_add_sample(bpe_multi *m, const int32_t *ids, int64_t n) {
@@ -298,7 +312,10 @@ int multi_add_sample(bpe_multi *m, const int32_t *ids, int64_t n) {
     int32_t nt = 0;
     MTRY(bpe_num_tokens(m->sh[0], &nt));
     for (int32_t id = nt; id <= mx; ++id) MTRY(multi_set_token_len16(m, id, 1));
-    if (m->distributed) return bpe_add_sample(m->sh.back(), ids, n);   // (corpus order kept)
+    if (m->distributed) {
+        MTRY(bpe_add_sample(m->sh.back(), ids, n));   // (corpus order kept)
+        return drop_global(m);
+    }
     m->staged.emplace_back(ids, ids + n);
     return BPE_OK;
 }
@@ -346,7 +363,7 @@ int multi_add_latin1(bpe_multi *m, const uint8_t *bytes, int64_t n, int64_t samp
     }
     // every shard knows every token (new ids are numbered by the vocabulary size)
     for (int32_t id = nt0; id < *n_tokens_io; ++id) MTRY(multi_set_token_len16(m, id, 1));
-    return BPE_OK;
+    return drop_global(m);
 }
 
 int multi_clear_corpus(bpe_multi *m) {

@@ -12,7 +12,9 @@ counts its pairs locally (libbpe's streaming pass).  Per iteration the ranks exc
   3. only when several pairs tie on (W, a+b): an all-reduce(MAX) of their last counted positions
      (rule R3; rank r's positions order after rank r-1's).
 Every rank then selects the same merge (libbpe's argmax over the global tables) and applies it to
-its own shard.  world == 1 is the plain single-GPU loop.
+its own shard.  world == 1 is the plain single-GPU loop, unless the trainer is made with
+rank_loop=True: then one rank runs the same exchange protocol and rank loop as N ranks (its
+collectives over a 1-rank process group), which is how the RCCL leg is exercised on a one-GPU box.
 
 ShardedTrainer.run() keeps that exchange on the device (libbpe's rank loop, include/bpe.h
 bpe_rank_loop_*): per iteration the table all-reduce(SUM), the selection kernels, the tie
@@ -172,8 +174,10 @@ def exchange_and_select(shard, dist, rank, world, max_length=0, min_weight=0, in
 
 
 class ShardedTrainer:
-    def __init__(self, shard, rank, world, dist, n_tokens, live_global):
+    def __init__(self, shard, rank, world, dist, n_tokens, live_global, rank_loop=False):
         self.shard = shard
+        # the exchange protocol and the rank loop (always for world > 1; for world 1 on request)
+        self.exchange = world > 1 or rank_loop
         self.engine = getattr(shard, 'engine', shard)
         self.rank = rank
         self.world = world
@@ -189,7 +193,7 @@ class ShardedTrainer:
 
     @classmethod
     def synthetic(cls, device, rank, world, bytes_per_rank, sample_bytes, seed, alphabet, base,
-                  dist=None, corpus='uniform'):
+                  dist=None, corpus='uniform', rank_loop=False):
         """Rank r holds bytes [r*B, (r+1)*B) of one synthetic corpus: the
         xorshift32 byte stream ('uniform') or Zipf(1.1) words ('zipf', bpe_synth_zipf; whole
         samples per rank)."""
@@ -202,7 +206,7 @@ class ShardedTrainer:
             data = pkg.synth_latin1(bytes_per_rank, seed=seed, A=alphabet, base=base,
                                     skip=rank * bytes_per_rank)
         eng = pkg.Engine(device)
-        if world == 1:
+        if world == 1 and not rank_loop:
             cmap, nt, _ = eng.add_latin1(data, sample_bytes=sample_bytes)
             return cls(eng, rank, world, dist, nt, bytes_per_rank)
         # global first-appearance order (core.ts:186-199) across the shards, in corpus order
@@ -221,13 +225,14 @@ class ShardedTrainer:
         for i in range(len(order)):
             eng.set_token_len16(i, 1)
         eng.add_latin1(data, sample_bytes=sample_bytes, char_to_id=cmap, n_tokens=len(order))
-        return cls(GpuShard(eng, device), rank, world, dist, len(order), bytes_per_rank * world)
+        return cls(GpuShard(eng, device), rank, world, dist, len(order), bytes_per_rank * world,
+                   rank_loop=rank_loop)
 
     def live_tokens_global(self):
         return self.live
 
     def find_next_merge(self, max_length=0, min_weight=0):
-        if self.world == 1:
+        if not self.exchange:
             return self.engine.find_next_merge(max_length, min_weight)
         return exchange_and_select(self.shard, self.dist, self.rank, self.world, max_length,
                                    min_weight)
@@ -236,7 +241,7 @@ class ShardedTrainer:
         """n merge iterations (fewer when no pair qualifies); returns the merges [(a, b, W)].
         On one GPU this is the engine's mergeUntil (decisions stay on the device, one host sync
         per batch of iterations); across ranks every iteration exchanges counts (step())."""
-        if self.world == 1:
+        if not self.exchange:
             ms = self.engine.merge_until(max_length, min_weight, n)
             for m in ms:
                 self.n_tokens += 1
@@ -257,6 +262,19 @@ class ShardedTrainer:
             else:              # RCCL, ordered after the stream's kernels by events
                 dist.all_reduce(t, op=op)
         return gloo, all_reduce
+
+    def _check_same_exchange(self, nw, gloo):
+        """Every rank must all-reduce the same number of words this batch (a rank whose tables
+        left the global state would exchange a different buffer): checked as bpe_multi.cpp does,
+        by an all-reduce(MAX) of (nw, -nw) once per batch."""
+        import torch
+        dev = torch.device('cpu') if gloo else self.shard.device
+        t = torch.tensor([nw, -nw], dtype=torch.int64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        hi, lo = int(t[0].item()), -int(t[1].item())
+        if hi != nw or lo != nw:
+            raise RuntimeError('bpe sharded: ranks disagree on the exchange (%d words here, %d..%d '
+                               'over the ranks)' % (nw, lo, hi))
 
     def enter_maintained(self):
         """The maintained state over the ranks (skewed corpora, large vocabularies): the global
@@ -324,6 +342,7 @@ class ShardedTrainer:
             with torch.cuda.stream(stream):
                 nw = eng.rank_loop_begin(max_length, min_weight, xchg.data_ptr(), tie.data_ptr(),
                                          self.rank, self.world)
+                self._check_same_exchange(nw, gloo)
                 view = xchg[:nw]
                 for _ in range(k):
                     all_reduce(view, dist.ReduceOp.SUM)
@@ -363,7 +382,7 @@ class ShardedTrainer:
     def step(self, max_length=0, min_weight=0, info=None):
         """One findNextMerge + applyMerge on every rank; returns (a, b, W) or None."""
         self._maintained = False
-        if self.world == 1:
+        if not self.exchange:
             m = self.engine.find_next_merge(max_length, min_weight)
         else:
             m = exchange_and_select(self.shard, self.dist, self.rank, self.world, max_length,
@@ -371,7 +390,7 @@ class ShardedTrainer:
         if m is None:
             return None
         a, b, w = m
-        if self.world == 1:
+        if not self.exchange:
             self.engine.apply_merge(a, b, self.n_tokens, sync=False)
         else:
             self.shard.apply(a, b, self.n_tokens)   # (no host sync: the count settles lazily)

@@ -241,8 +241,9 @@ int bpe_set_global_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *k
  * BPE_MODE_INCREMENTAL: bpe_merge_until works on a position index: per
  * merge only the W match sites and their neighbours are touched, O(W) instead of O(N).  Same
  * merges, counts and corpus; it changes what pair-scans/s measures, so it is reported apart.
- * Built per call (one radix sort of the corpus); needs < 2^31 live slots.  Env BPE_PIX=1 selects
- * it for new contexts.  Single-device contexts only. */
+ * Built per call by a hand-written counting scatter of the corpus's positions into per-pair lists
+ * (one count pass, one exclusive scan, two fill passes; no sort); needs < 2^31 live slots.  Env
+ * BPE_PIX=1 selects it for new contexts.  Single-device contexts only. */
 #define BPE_MODE_STREAM 0
 #define BPE_MODE_INCREMENTAL 1
 int bpe_set_mode(bpe_ctx *ctx, int mode);

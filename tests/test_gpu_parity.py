@@ -188,6 +188,17 @@ def test_config2_golden():
     for i in range(len(off) - 1):
         h.update(np.append(ids[off[i]:off[i + 1]], -1).astype('<i4').tobytes())
     assert h.hexdigest() == g['final_ids_sha256']
+    # encodeToVector of every sample (core.ts:424-445) on the device encoder: the 10 raw samples
+    # replayed through the merge list by apply-only passes (encode_samples), then compactVectorIndex
+    # from the reference's weight bookkeeping; hashed as the reference's own run was
+    from test_oracle_golden import config2_vectors
+    raw = cmap[data].astype(np.int32)
+    samples = [raw[o:o + g['sample']] for o in range(0, g['total'], g['sample'])]
+    abc = [(a, b, nt + i) for i, (a, b, _) in enumerate(merges)]
+    enc = pkg.encode_samples(samples, abc, [1] * nt)
+    vec, n_vec = config2_vectors(enc, np.bincount(raw, minlength=nt), merges)
+    assert n_vec == g['vectors_len']
+    assert vec == g['vectors_sha256']
 
 
 @pytest.mark.slow

@@ -73,3 +73,13 @@ def test_reference_spec_and_golden_through_js_on_two_shards():
     build_addon()
     out = run_node('spec_gpu.js', '--expose-gc', env={'BPE_DEVICES': '0,0', 'BPE_REDUCE': 'host'})
     assert 'spec_gpu ok' in out
+
+
+@pytest.mark.gpu
+def test_config2_vectors_through_js():
+    """BASELINE config 2 through the drop-in: 10 x 1 MiB samples, mergeUntil({min_weight: 2,
+    max_iterations: 1000}), encodeToVector of every sample on the device encoder; merges, weights,
+    final corpus and vectors hashed as the reference's own run (tests/golden/config2.json)."""
+    build_addon()
+    out = run_node('config2_gpu.js', timeout=900)
+    assert 'config2_gpu ok' in out

@@ -167,6 +167,62 @@ def test_rccl_exchange_over_two_devices():
     assert two.merge_until(0, 2, 300) == one.merge_until(0, 2, 300)
 
 
+@pytest.mark.parametrize('corpus', ['uniform', 'zipf'])
+def test_rccl_one_device_context(corpus):
+    """bpe_create_multi with RCCL on one device (ncclCommInitAll over [0]): the rank loop's
+    all-reduces are real RCCL calls on the shard's stream.  A 64 MiB C3 slice (table state) and a
+    zipf slice (maintained state: delta rows all-reduced every merge) give the single context's
+    merges and corpus."""
+    if corpus == 'zipf':
+        data, n = pkg.synth_zipf(16 << 20, seed=12345), 700
+    else:
+        data, n = pkg.synth_latin1(64 << 20, seed=12345, A=256), 400
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    want = one.merge_until(0, 2, n)
+    ids1, off1 = one.read_corpus()
+    one.close()
+    r = pkg.Engine(devices=[0], reduce='rccl')
+    assert r.shard_count() == 1
+    r.add_latin1(data, sample_bytes=1 << 20)
+    r.stats_enable(True)
+    got = r.merge_until(0, 2, n)
+    st = r.stats()
+    assert got == want
+    ids, off = r.read_corpus()
+    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    if corpus == 'zipf':
+        assert st['fused_passes'] > n // 2, st
+    r.close()
+
+
+@pytest.mark.parametrize('shards', [3, 1])
+def test_samples_added_in_the_maintained_state(shards):
+    """merge (zipf: the shards reach the maintained state), add samples, merge on: a sample added
+    to the last shard makes every shard leave the global tables, so the exchange sizes stay equal;
+    the merges and corpus equal one context's."""
+    data = pkg.synth_zipf(6 << 20, seed=12345)
+    extra = pkg.synth_zipf(2 << 20, seed=777)
+    one = pkg.Engine(0)
+    cm, _, _ = one.add_latin1(data, sample_bytes=1 << 20)
+    w1 = one.merge_until(0, 2, 500)
+    one.add_latin1(extra, sample_bytes=1 << 20, char_to_id=cm)
+    w2 = one.merge_until(0, 2, 300)
+    ids1, off1 = one.read_corpus()
+    one.close()
+    multi = pkg.Engine(devices=[0] * shards, reduce='host')
+    cm3, _, _ = multi.add_latin1(data, sample_bytes=1 << 20)
+    assert np.array_equal(cm, cm3)
+    multi.stats_enable(True)
+    assert multi.merge_until(0, 2, 500) == w1
+    assert multi.stats()['fused_passes'] > 0
+    multi.add_latin1(extra, sample_bytes=1 << 20, char_to_id=cm)
+    assert multi.merge_until(0, 2, 300) == w2
+    ids, off = multi.read_corpus()
+    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    multi.close()
+
+
 @pytest.mark.parametrize('shards,mib,n,max_length', [(3, 6, 900, 0), (4, 4, 600, 5), (2, 8, 700, 0)])
 def test_maintained_state_over_shards_on_zipf_words(shards, mib, n, max_length):
     """A skewed corpus over several shards: the cold pairs outgrow the sketch, the shards move to

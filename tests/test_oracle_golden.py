@@ -128,3 +128,35 @@ def test_oracle_config2():
     for s in st.samples():
         h.update(np.asarray(s + [-1], dtype='<i4').tobytes())
     assert h.hexdigest() == g['final_ids_sha256']
+    # encodeToVector of every sample (core.ts:424-445): the replay of the merges over the sample
+    # (encodeToCode, core.ts:404-406) is what training did to it; sample 0 is replayed on its own
+    # here to show it.  The vector maps ids through compactVectorIndex (core.ts:222-241), built
+    # from the reference's weight bookkeeping (core.ts:201-202, 345-346, 322), not from the corpus.
+    s0 = OracleState(ids[off[0]:off[1]], [0, off[1] - off[0]], len16, len(first), extra=4096)
+    for i, (a, b, _) in enumerate(merges):
+        s0.apply_merge(a, b, len(first) + i)
+    assert s0.samples()[0] == st.samples()[0]
+    vec, n_vec = config2_vectors(st.samples(), np.bincount(ids, minlength=len(first)), merges)
+    assert n_vec == g['vectors_len']
+    assert vec == g['vectors_sha256']
+
+
+def config2_vectors(samples, char_hist, merges):
+    """SHA-256 of encodeToVector over the samples, hashed as oracle/gen_golden.py hashed the
+    reference's run (int32 LE vector + a -1 separator per sample)."""
+    weight = [int(x) for x in char_hist]
+    for a, b, w in merges:
+        weight[a] -= w                                   # core.ts:345-346
+        weight[b] -= w
+        weight.append(w)                                 # c.weight = W (core.ts:322)
+    to_vec = np.full(len(weight), -1, np.int64)
+    live = [i for i, w in enumerate(weight) if w > 0]    # core.ts:233-240
+    to_vec[live] = np.arange(len(live))
+    h = hashlib.sha256()
+    n = 0
+    for s in samples:
+        v = to_vec[np.asarray(s, np.int64)]
+        assert (v >= 0).all(), 'unknown token index'     # core.ts:440
+        h.update(np.append(v, -1).astype('<i4').tobytes())
+        n += len(v) + 1
+    return h.hexdigest(), n

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
-           mib=3, corpus='uniform'):
+           mib=3, corpus='uniform', backend='gloo'):
     import importlib
     import sys
     import torch
@@ -20,13 +20,18 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
     sharded = importlib.import_module('bpe-tokenizer_amd.sharded')
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    if backend == 'nccl':     # (RCCL: one rank per device, so world 1 on the one-GPU box)
+        dist.init_process_group('nccl', rank=rank, world_size=world,
+                                device_id=torch.device('cuda', 0))
+    else:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        torch.cuda.set_device(0)
         tr = sharded.ShardedTrainer.synthetic(device=0, rank=rank, world=world,
                                               bytes_per_rank=mib << 20, sample_bytes=1 << 20,
                                               seed=seed, alphabet=A, base=base, dist=dist,
-                                              corpus=corpus)
+                                              corpus=corpus, rank_loop=True)
+        assert tr.exchange and dist.get_backend() == backend
         tr.engine.stats_enable(True)
         if mode == 'step':
             for _ in range(n):
@@ -110,3 +115,29 @@ def test_rank_loop_maintained_state_on_zipf_words():
 def test_rank_loop_maintained_state_three_ranks_max_length():
     st = check(3, mode='loop', n=400, corpus='zipf', mib=2, seed=99, max_length=6)
     assert all(s['fused_passes'] > 100 for s in st), st
+
+
+# ---- the RCCL leg (torch.distributed 'nccl' = RCCL on ROCm), one rank on the one-GPU box ----------
+# ShardedTrainer(rank_loop=True) runs the N-rank protocol at world 1: the per-iteration
+# all-reduce(SUM) of the exchange buffer and all-reduce(MAX) of the tie words go through RCCL on the
+# engine's stream, exactly as on 8 GPUs (core.ts:265-267 shards at samples).
+
+def test_rccl_rank_loop_one_rank_c3_slice():
+    """64 MiB of the C3 stream (256-char alphabet), 400 merges through the rank loop over a 1-rank
+    RCCL group: the same merges and corpus as the single-context device loop."""
+    st = check(1, mode='loop', n=400, seed=12345, A=256, base=0, mib=64, backend='nccl')
+    assert st[0]['tie_passes'] + st[0]['tie_tail'] > 0 or st[0]['iterations'] >= 400, st
+
+
+def test_rccl_rank_loop_one_rank_zipf_maintained():
+    """Zipf words (skewed): the rank moves to the maintained state (global tables kept with delta
+    rows, exchanged through RCCL every merge) and stays there."""
+    st = check(1, mode='loop', n=600, corpus='zipf', mib=8, seed=12345, backend='nccl')
+    assert st[0]['fused_passes'] > 300, st
+    assert st[0]['loop_host'] <= 12, st
+
+
+def test_rccl_host_protocol_one_rank():
+    """The host protocol (exchange_and_select: table all-reduce, heavy-bucket all-gathers, tie
+    all-reduce) over a 1-rank RCCL group, iteration by iteration."""
+    check(1, mode='step', n=120, seed=4242, A=12, base=97, mib=2, backend='nccl')

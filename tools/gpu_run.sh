@@ -1,0 +1,98 @@
+#!/bin/bash
+# The one GPU-box driver script (run from the repo root on the box, e.g. through gpurun):
+#   tools/gpu_run.sh TAG step [step ...]
+# Every step runs under its own time limit; the script stops at the first failing step.
+# Steps:
+#   tests      pytest -m gpu (PYTEST_PATHS: test paths, PYTEST_K: a -k expression; default all)
+#   smoke      __graft_entry__.smoke()
+#   driver     the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5), timed
+#   bench      full C3 bench line + the incremental mode's line (bench.py --incremental)
+#   zipf       full zipf C3 bench line (bench.py --corpus zipf)
+#   prof       rocprofv3 --kernel-trace --stats of the full C3 bench (kernel stats CSV)
+#   profzipf   the same for zipf C3
+#   profpix    the same for the incremental mode (tools/pix_bench.py, full C3)
+#   pmc        FETCH_SIZE and WRITE_SIZE passes (300 C3 merges), summarised by tools/pmc_summary.py
+#   sq         two SQ counter passes (300 C3 merges), summarised by tools/sq_loop_summary.py
+#   probe      tools/probe/bin/stream_probe3 (loads in flight x VALU work per chunk)
+#   rccl       the RCCL legs at world 1: tools/sharded_overhead.py (per-iteration cost)
+# Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), BPE_LIB (A/B builds)
+set -o pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fail() { echo "step $1 failed"; tail -40 "$2"; exit 1; }
+prof_stats() {  # $1 dir: print the top kernels of the stats CSV
+  find "$1" -name '*kernel_stats.csv' -exec head -14 {} \;
+}
+PMC_BENCH="bench.py --steps 300 --warmup 5 --no-cpu-baseline ${PMC_CORPUS:+--corpus $PMC_CORPUS}"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+  tests)
+    timeout -k 10 1100 python3 -u -m pytest ${PYTEST_PATHS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -v \
+        --maxfail=5 --timeout 400 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
+        || fail tests "$OUT/pytest_gpu.log"
+    tail -3 "$OUT/pytest_gpu.log" ;;
+  smoke)
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || fail smoke "$OUT/smoke.log"
+    cat "$OUT/smoke.log" ;;
+  driver)
+    t0=$(date +%s.%N)
+    timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver.jsonl" 2> "$OUT/driver.err" \
+        || fail driver "$OUT/driver.err"
+    t1=$(date +%s.%N)
+    cat "$OUT/driver.jsonl"; python3 -c "print('driver wall: %.1f s' % ($t1 - $t0))" | tee "$OUT/driver.wall" ;;
+  bench)
+    timeout -k 10 700 python3 bench.py --incremental $BENCH_EXTRA > "$OUT/bench.jsonl" 2> "$OUT/bench.err" \
+        || fail bench "$OUT/bench.err"
+    cat "$OUT/bench.jsonl" ;;
+  zipf)
+    timeout -k 10 600 python3 bench.py --corpus zipf --no-cpu-baseline $BENCH_EXTRA > "$OUT/zipf.jsonl" \
+        2> "$OUT/zipf.err" || fail zipf "$OUT/zipf.err"
+    head -c 1500 "$OUT/zipf.jsonl" ;;
+  prof)
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline $BENCH_EXTRA > "$OUT/trace.jsonl" 2> "$OUT/trace.err" \
+        || fail prof "$OUT/trace.err"
+    head -c 600 "$OUT/trace.jsonl"; echo; prof_stats "$OUT/trace" ;;
+  profzipf)
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/tracez" -o run --output-format csv \
+        -- python3 bench.py --corpus zipf --no-cpu-baseline > "$OUT/tracez.jsonl" 2> "$OUT/tracez.err" \
+        || fail profzipf "$OUT/tracez.err"
+    head -c 600 "$OUT/tracez.jsonl"; echo; prof_stats "$OUT/tracez" ;;
+  profpix)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/pix" -o run --output-format csv \
+        -- python3 tools/pix_bench.py 1024 7995 --no-stream > "$OUT/pix.json" 2> "$OUT/pix.err" \
+        || fail profpix "$OUT/pix.err"
+    cat "$OUT/pix.json"
+    python3 tools/trace_gaps.py "$OUT/pix" "$OUT/gaps_pix.json" --from-kernel k_pix_select > /dev/null \
+        || fail gaps "$OUT/pix.err" ;;
+  pmc)
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
+        -- python3 $PMC_BENCH > "$OUT/fetch.log" 2>&1 || fail fetch "$OUT/fetch.log"
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
+        -- python3 $PMC_BENCH > "$OUT/write.log" 2>&1 || fail write "$OUT/write.log"
+    python3 tools/pmc_summary.py "$OUT" "$OUT/pmc_summary.json" > /dev/null && echo "pmc summary written" ;;
+  sq)
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        -d "$OUT/sq" -o run --output-format csv -- python3 $PMC_BENCH > "$OUT/sq.log" 2>&1 || fail sq "$OUT/sq.log"
+    timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
+        -d "$OUT/sq2" -o run --output-format csv -- python3 $PMC_BENCH > "$OUT/sq2.log" 2>&1 || fail sq2 "$OUT/sq2.log"
+    python3 tools/sq_loop_summary.py "$OUT" > "$OUT/sq_summary.txt" && cat "$OUT/sq_summary.txt" ;;
+  probe)
+    timeout -k 10 300 tools/probe/bin/stream_probe3 > "$OUT/probe3.jsonl" 2>&1 || fail probe "$OUT/probe3.jsonl"
+    cat "$OUT/probe3.jsonl" ;;
+  rccl)
+    for sz in "64 300" "1024 300"; do
+      timeout -k 10 400 python3 -u tools/sharded_overhead.py $sz >> "$OUT/rccl_overhead.jsonl" 2>> "$OUT/rccl.err" \
+          || fail rccl "$OUT/rccl.err"
+    done
+    cat "$OUT/rccl_overhead.jsonl" ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+# keep the merged-back output small (the raw per-dispatch CSVs are tens of MB)
+find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete
+exit 0
