@@ -364,23 +364,29 @@ napi_value MergeUntil(napi_env env, napi_callback_info info) {
     return out;
 }
 
-// The encoder's scratch engine (created on first use, destroyed with the addon's environment).
-bpe_ctx *g_scratch = nullptr;
+// The encoder's scratch engine: one per environment (the addon is context-aware: each
+// worker_threads environment that loads it gets its own instance data, so two workers never share
+// an engine), created on first use and destroyed with its environment (napi_set_instance_data's
+// finalizer).  Each environment's calls come from its one JS thread.
+struct AddonData {
+    bpe_ctx *scratch = nullptr;
+};
 
-void destroy_scratch(void *) {
-    if (g_scratch) bpe_destroy(g_scratch);
-    g_scratch = nullptr;
+void finalize_addon(napi_env, void *data, void *) {
+    AddonData *d = static_cast<AddonData *>(data);
+    if (d->scratch) bpe_destroy(d->scratch);
+    delete d;
 }
 
 bpe_ctx *scratch_engine(napi_env env) {
-    if (!g_scratch) {
-        if (bpe_create(&g_scratch, 0) != BPE_OK) {
-            g_scratch = nullptr;
-            return nullptr;
-        }
-        napi_add_env_cleanup_hook(env, destroy_scratch, nullptr);
+    void *p = nullptr;
+    if (napi_get_instance_data(env, &p) != napi_ok || !p) return nullptr;
+    AddonData *d = static_cast<AddonData *>(p);
+    if (!d->scratch && bpe_create(&d->scratch, 0) != BPE_OK) {
+        d->scratch = nullptr;
+        return nullptr;
     }
-    return g_scratch;
+    return d->scratch;
 }
 
 // encodeMerges(Int32Array ids, Int32Array abc) -> Int32Array: one text through a run of merges
@@ -449,6 +455,12 @@ napi_value Init(napi_env env, napi_value exports) {
         napi_value fn;
         napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn);
         napi_set_named_property(env, exports, f.name, fn);
+    }
+    AddonData *d = new AddonData();
+    if (napi_set_instance_data(env, d, finalize_addon, nullptr) != napi_ok) {
+        delete d;
+        napi_throw_error(env, nullptr, "bpe native: napi_set_instance_data failed");
+        return nullptr;
     }
     return exports;
 }

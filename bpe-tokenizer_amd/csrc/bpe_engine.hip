@@ -179,6 +179,11 @@ struct bpe_ctx {
     int64_t rl_last_w = -1;
     // the cold table holds this shard's exact count of every cold pair (bpe_cold_counts)
     bool cold_list = false;
+    // the global state of a sharded corpus lives in the position index (bpe_set_mode
+    // BPE_MODE_INCREMENTAL, bpe_pix.hip.h): c->pix holds this shard's lists and the GLOBAL counts
+    // between rank loop batches, and the corpus is in the index's slot layout until it is dropped
+    bool rl_pix = false;
+    uint64_t pix_min_cap = 0;    // (the next index build's least table size)
 };
 
 namespace {
@@ -188,16 +193,31 @@ int set_device(bpe_ctx *c) {
     return BPE_OK;
 }
 
+}  // namespace
+int pix_finish(bpe_ctx *c);
+namespace {
+
 // Before anything that reads or updates this shard's own counts: global tables (the sharded
-// maintained state) are dropped, and the next use recounts.
-void leave_global(bpe_ctx *c) {
-    if (!c->rl_global) return;
+// maintained state) are dropped, and the next use recounts.  A sharded position index is dropped
+// too: the corpus goes back to the chunk layout.
+int leave_global(bpe_ctx *c) {
+    if (!c->rl_global) return BPE_OK;
     c->rl_global = false;
     c->rl_delta_pending = false;
     c->counts_valid = c->sketch_valid = c->best_ready = false;
     c->cold_exact = false;
     c->cold_list = false;
+    if (c->rl_pix) {
+        c->rl_pix = false;
+        return pix_finish(c);
+    }
+    return BPE_OK;
 }
+#define LEAVE_GLOBAL(c)                   \
+    do {                                  \
+        const int lg_ = leave_global(c);  \
+        if (lg_) return lg_;              \
+    } while (0)
 
 void geometry(bpe_ctx *c) {
     const int64_t nc = std::max<int64_t>(1, c->n_chunks);
@@ -543,6 +563,8 @@ int settle_with(bpe_ctx *c, unsigned long long Ru) {
 }
 
 int settle(bpe_ctx *c) {
+    // (a sharded position index between rank loop batches: anything else reads the chunk layout)
+    if (c->rl_pix && !c->rl_open) LEAVE_GLOBAL(c);
     if (!c->pending) return BPE_OK;
     unsigned long long R = 0;
     HIP_TRY(hipMemcpyAsync(&R, &c->d_res->replaced, sizeof R, hipMemcpyDeviceToHost, c->stream));
@@ -788,7 +810,7 @@ int do_find(bpe_ctx *c, int64_t max_length, int64_t min_weight, int32_t *a, int3
             int64_t *w) {
     if (min_weight == 0) min_weight = 2;                              // core.ts:256
     int rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     // with a maintained cold table the selection settles a pending merge from the Result it
     // copies back anyway, so the host does not wait for the merge pass before enqueueing it
     const bool deferred = c->pending && c->cold_exact && c->counts_valid;
@@ -845,7 +867,7 @@ int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc);
 
 int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     int rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = register_merge(c, a, b, cc))) return rc;                 // core.ts:315-318
     if (replaced) *replaced = 0;
     if ((rc = settle(c))) return rc;
@@ -894,7 +916,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     int rc;
     *n_done = 0;
     *status = LOOP_DONE;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     c->cold_list = false;
     c->opt_max_length = max_length;
@@ -1099,10 +1121,25 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
 // it must equal W (checked on the device by the next decision, and for the batch's last merge by
 // the host from the log).
 int carry_pass(bpe_ctx *c);
+}  // namespace
+int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *xchg,
+                   unsigned long long *tie, int rank, int world, int64_t *n_words);
+int pix_rank_select(bpe_ctx *c);
+int pix_rank_decide(bpe_ctx *c);
+int pix_rank_count(bpe_ctx *c);
+int pix_rank_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *status);
+int pix_set_global(bpe_ctx *c, const unsigned long long *table, const uint32_t *keys,
+                   const unsigned long long *counts, int64_t n);
+namespace {
 
 int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *xchg,
                     unsigned long long *tie, int rank, int world, int64_t *n_words) {
     int rc;
+    if (c->rl_pix && c->rl_global) {
+        if (!c->rl_delta_pending || xchg == c->rl_table)
+            return pix_rank_begin(c, max_length, min_weight, xchg, tie, rank, world, n_words);
+        LEAVE_GLOBAL(c);   // (another exchange buffer: the last merge's delta rows are not in it)
+    }
     if ((rc = settle(c))) return rc;
     const bool glob = c->rl_global;
     c->opt_max_length = max_length;
@@ -1118,7 +1155,7 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
             if ((rc = carry_pass(c))) return rc;
         if (c->rl_delta_pending && xchg != c->rl_table) {
             // (another exchange buffer: the last merge's delta rows are not in it)
-            leave_global(c);
+            LEAVE_GLOBAL(c);
             return rank_loop_begin(c, max_length, min_weight, xchg, tie, rank, world, n_words);
         }
     } else {
@@ -1192,6 +1229,7 @@ int rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned
 int rank_loop_select(bpe_ctx *c) {
     if (!c->rl_open || c->rl_enqueued >= LOOP_BATCH)
         return fail(BPE_ERR_STATE, "bpe native: rank loop not begun, or its batch is full");
+    if (c->rl_pix) return pix_rank_select(c);
     hipStream_t s = c->stream;
     const int64_t ml = c->rl_max_length;
     hipEvent_t e_sel = span_begin(c);
@@ -1228,6 +1266,7 @@ int rank_loop_select(bpe_ctx *c) {
 // After the all-reduce(MAX) of `tie`: the decision, the same on every rank.
 int rank_loop_decide(bpe_ctx *c) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    if (c->rl_pix) return pix_rank_decide(c);
     k_decide<<<1, 64, 0, c->stream>>>(c->d_ctl, c->d_res, c->d_cand, c->d_len16, c->d_log, 1,
                                       c->rl_tie, c->rl_table);
     HIP_TRY(hipGetLastError());
@@ -1238,6 +1277,7 @@ int rank_loop_decide(bpe_ctx *c) {
 // its replacement count into the exchange buffer.
 int rank_loop_count(bpe_ctx *c) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    if (c->rl_pix) return pix_rank_count(c);
     hipStream_t s = c->stream;
     unsigned long long *x = c->rl_table;
     hipEvent_t e_step = span_begin(c);
@@ -1281,6 +1321,7 @@ int rank_loop_count(bpe_ctx *c) {
 // the host protocol).
 int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *status) {
     if (!c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    if (c->rl_pix) return pix_rank_end(c, out, cap, n_done, status);
     c->rl_open = false;
     hipStream_t s = c->stream;
     LoopCtl *h = c->h_ctl;
@@ -1303,7 +1344,7 @@ int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *s
             fprintf(stderr, "[bpe debug] rank %d ctl: a %d b %d c %d w %lld tie %d vote %d base %lld\n",
                     c->rl_rank, h->a, h->b, h->c, (long long)h->w, h->tie, h->vote, (long long)c->rl_base);
         }
-        leave_global(c);
+        LEAVE_GLOBAL(c);
         c->counts_valid = false;
         char msg[256];
         if (h->err == 1)
@@ -1372,7 +1413,7 @@ int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *s
             c->rl_last_c = (int32_t)(base + nd - 1);
             c->rl_last_w = m[2];
         } else if (!all) {
-            leave_global(c);   // (the host path takes over: this shard's counts are recounted)
+            LEAVE_GLOBAL(c);   // (the host path takes over: this shard's counts are recounted)
         }
     } else if (all && nd > 0) {
         // the last count left this shard's table in the exchange buffer, not summed since
@@ -1393,7 +1434,7 @@ int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *s
 // exports the same list without another pass).
 int cold_counts(bpe_ctx *c, uint32_t *keys, unsigned long long *counts, int64_t cap, int64_t *n) {
     int rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     if (!c->cold_list) {
         hipStream_t s = c->stream;
@@ -1422,9 +1463,10 @@ int cold_counts(bpe_ctx *c, uint32_t *keys, unsigned long long *counts, int64_t 
 int set_global_counts(bpe_ctx *c, const unsigned long long *table, const uint32_t *keys,
                       const unsigned long long *counts, int64_t n) {
     int rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     if (n < 0 || (n && (!keys || !counts))) return fail(BPE_ERR_ARG, "bpe native: bad global counts");
+    if (c->use_pix) return pix_set_global(c, table, keys, counts, n);   // (the incremental mode)
     hipStream_t s = c->stream;
     // room for every distinct pair at half fill, and for the claims of the merges to come (the
     // decisions hand over to the host before 3/4 fill)
@@ -1488,7 +1530,7 @@ int register_merge(bpe_ctx *c, int32_t a, int32_t b, int32_t cc) {
 // extra pass.  replaced (may be null) receives each merge's replacement count.
 int replay(bpe_ctx *c, const int32_t *abc, int64_t n, int64_t *replaced, bool count_after) {
     int rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     const int64_t n_plain = count_after ? n - 1 : n;
     for (int64_t i0 = 0; i0 < n_plain;) {
@@ -1719,8 +1761,10 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
     if (!c->packed)
         if ((rc = compact(c))) return rc;
     const int64_t n = c->live_slots;
-    // positions and pool offsets are 32-bit; the vocabulary key is two 16-bit ids
-    if (n < 2 || n > (int64_t)0x7FFFFFFF || c->h_len16.size() > 0xFFFF) return PIX_NOT_ELIGIBLE;
+    // positions and pool offsets are 32-bit (PIX_NONE = 2^32 - 1 is no position; the margin keeps
+    // a block's end, block * PB + PB, below 2^32); the vocabulary key is two 16-bit ids
+    // (a shard of a sharded corpus may hold fewer than two slots: its index is just empty)
+    if (n > (int64_t)PIX_MAX_SLOTS || c->h_len16.size() > 0xFFFF) return PIX_NOT_ELIGIBLE;
     if ((rc = ensure_vocab(c, (int64_t)c->h_len16.size()))) return rc;
     if ((rc = sync_len16(c, 1))) return rc;
     pix_free(c);
@@ -1736,30 +1780,31 @@ int pix_build_timed(bpe_ctx *c, int64_t max_length) {
     PixBufs &B = P->B;
     if ((rc = pix_alloc(P, &B.pool, pool_cap))) return rc;
     const uint32_t nblk = (N + PB - 1) / PB;
-    int32_t *carry;
+    uint32_t *carry;
     if ((rc = pix_alloc(P, &carry, nblk))) return rc;
     k_pix_build_links<<<4096, 256, 0, s>>>(C, carry);
     k_pix_scan_max<<<1, 1024, 0, s>>>(carry, nblk);
     HIP_TRY(hipGetLastError());
-    if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, 3 * PIX_BATCH))) return rc;
+    if ((rc = pix_alloc(P, &P->d_ctl, 1)) || (rc = pix_alloc(P, &P->d_log, PIX_LOG * PIX_BATCH))) return rc;
     HIP_TRY(hipHostMalloc((void **)&P->h_ctl, sizeof(PixCtl), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&P->h_log, 3 * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&P->h_log, PIX_LOG * PIX_BATCH * sizeof(long long), hipHostMallocDefault));
     // the hot passes' scratch: per workgroup and half a slab of 32768 counts (then offsets), the
     // hot pairs' totals, slots and uncounted (x, x) occurrences
     Scratch hs;
-    const int G = (int)std::min<uint32_t>(PH_WG_MAX, nblk);
+    const int G = (int)std::max<uint32_t>(1, std::min<uint32_t>(PH_WG_MAX, nblk));
     uint32_t *slab, *htot, *hslot, *hseg, *bucket, *xoff;
     unsigned long long *oddxx;
     if ((rc = hs.get(&slab, (size_t)2 * G * PH_HALF)) || (rc = hs.get(&htot, 65536)) ||
         (rc = hs.get(&hslot, 65536)) || (rc = hs.get(&oddxx, 256)) || (rc = hs.get(&hseg, 65536)) ||
         (rc = hs.get(&bucket, 257)) || (rc = hs.get(&xoff, (size_t)G * 256)))
         return rc;
-    // the pair table: room for the current pairs and the ones merges will add
+    // the pair table: room for the current pairs and the ones merges will add (a shard of a
+    // sharded corpus: also every pair of the other shards, pix_min_cap)
     uint64_t cap = 1u << 20;
-    while (cap < (uint64_t)N / 8) cap <<= 1;
+    while (cap < (uint64_t)N / 8 || cap < c->pix_min_cap) cap <<= 1;
     PixTable &T = P->T;
     for (int attempt = 0;; ++attempt) {
-        if (cap > (1ull << 31)) return PIX_NOT_ELIGIBLE;
+        if (cap >= (1ull << 31)) return PIX_NOT_ELIGIBLE;   // (slot numbers keep PIX_OWNER free)
         P->cap = cap;
         T = PixTable{};
         T.mask = (uint32_t)(cap - 1);
@@ -1878,6 +1923,8 @@ int pix_finish(bpe_ctx *c) {
     return seal_packed(c);
 }
 
+int pix_reserve(bpe_ctx *c);
+
 // mergeUntil on the index: batches of PIX_BATCH merges, one host round trip each.  An iteration
 // the index cannot take (PIX_HOST) runs on the streaming path, and the index is rebuilt after it.
 int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t max_iterations,
@@ -1886,7 +1933,8 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     int64_t n = 0;
     const int64_t mw = min_weight == 0 ? 2 : min_weight;                  // core.ts:256
     int builds = 0;
-    leave_global(c);
+    bool just_built = false;
+    LEAVE_GLOBAL(c);
     // Heavy merges first on the stream: a merge costs the index O(W) (plus contention on the
     // new pairs' slots when W is large), the stream one pass whatever W.  While the next merge's
     // W exceeds max(2^16, n_live / 8192) (C3: 131 K against W = 16 K, so never; a skewed corpus's
@@ -1929,6 +1977,7 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             if (c->n_live < 2) break;
             rc = pix_build(c, max_length);
             ++builds;
+            just_built = true;
             if (rc == BPE_ERR_OOM) {
                 // (the index does not fit next to the corpus: the stream needs no extra memory)
                 if (c->pix) {
@@ -1944,6 +1993,9 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             }
             if (rc) return rc;
         }
+        if (builds && !just_built)
+            if ((rc = pix_reserve(c))) return rc;   // (grow the pool / table in place)
+        just_built = false;
         PixState *P = c->pix;
         hipStream_t s = c->stream;
         const int64_t base = (int64_t)c->h_len16.size();
@@ -1965,7 +2017,7 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             HIP_TRY(hipGetLastError());
             PixCtl *h = P->h_ctl;
             HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(P->h_log, P->d_log, 3 * want * sizeof(long long),
+            HIP_TRY(hipMemcpyAsync(P->h_log, P->d_log, PIX_LOG * want * sizeof(long long),
                                    hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
             status = h->status;
@@ -1979,8 +2031,8 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
             c->h_len16.resize(base + nd, 1);
             c->h_count.resize(base + nd, 0);
             for (int64_t i = 0; i < nd; ++i, ++n) {
-                const int32_t a = (int32_t)P->h_log[3 * i], b = (int32_t)P->h_log[3 * i + 1];
-                const int64_t W = P->h_log[3 * i + 2];
+                const int32_t a = (int32_t)P->h_log[PIX_LOG * i], b = (int32_t)P->h_log[PIX_LOG * i + 1];
+                const int64_t W = P->h_log[PIX_LOG * i + 2];
                 const int64_t cc = base + i;
                 c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];            // core.ts:318
                 if (c->stats_on) {
@@ -2030,6 +2082,277 @@ int pix_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
     if ((rc = pix_finish(c))) return rc;
     *n_merges = n;
     return settle(c);
+}
+
+// ================================================================================================
+// A shard of a sharded corpus in the incremental mode: the position index inside the rank loop
+// (bpe_pix.hip.h, "a shard of a sharded corpus").  The index holds this shard's lists and every
+// pair's GLOBAL count; each merge's count changes travel as delta rows.
+// ================================================================================================
+
+// bpe_set_global_counts in the incremental mode: this shard's index, then the global counts (the
+// summed table's hot bins, every shard's cold pairs) in place of its own.
+int pix_set_global(bpe_ctx *c, const unsigned long long *table, const uint32_t *keys,
+                   const unsigned long long *counts, int64_t n) {
+    int rc;
+    // every pair of the corpus at most half the table (n counts a pair once per shard holding it;
+    // pix_reserve grows the table in place as merges add pairs)
+    c->pix_min_cap = 2 * (uint64_t)(HOT_BINS + n);
+    rc = pix_build(c, c->opt_max_length);
+    c->pix_min_cap = 0;
+    if (rc == PIX_NOT_ELIGIBLE || rc == BPE_ERR_OOM) {
+        if (c->pix) {
+            (void)hipStreamSynchronize(c->stream);
+            pix_free(c);
+        }
+        return fail(BPE_ERR_STATE, "bpe native: the position index does not fit this shard "
+                                   "(use the streaming mode)");
+    }
+    if (rc) return rc;
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    HIP_TRY(hipMemsetAsync(P->T.cnt, 0, P->cap * sizeof(unsigned long long), s));
+    k_pix_load_global<<<1024, 256, 0, s>>>(P->T, P->d_ctl, table, keys, counts, n);
+    k_pix_bmax_all<<<4096, 256, 0, s>>>(P->T);
+    k_pix_sbmax<<<1024, 256, 0, s>>>(P->T, P->B, P->d_ctl, 1);
+    HIP_TRY(hipGetLastError());
+    PixCtl *h = P->h_ctl;
+    HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->err || h->used * 2 > P->cap) {
+        pix_free(c);
+        return fail(BPE_ERR_STATE, "bpe native: position index: the global pairs overflow the table");
+    }
+    c->rl_global = true;
+    c->rl_pix = true;
+    c->rl_delta_pending = false;
+    c->counts_valid = c->sketch_valid = c->best_ready = false;
+    c->cold_exact = false;
+    return BPE_OK;
+}
+
+// Room for the next batch, grown in place (no hand-off, no rebuild): the pool when less than an
+// eighth of the corpus is left of it (the new segments of a merge take two entries per site), the
+// pair table (rehashed twice as large) past 45 % fill.  Between batches, with no tie pending (a
+// decided tie names its pair by slot).  A shard of a sharded corpus grows its own index alone.
+int pix_reserve(bpe_ctx *c) {
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    PixCtl *h = P->h_ctl;
+    HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->status != PIX_RUN && h->status != PIX_PAUSE) return BPE_OK;
+    const uint64_t N = P->C.n;
+    const uint64_t slack = std::max<uint64_t>(N / 8, 1u << 20);
+    if (h->pool_top + slack > h->pool_cap && h->pool_cap < 0xFFFFFFF0ull) {
+        const uint64_t ncap = std::min<uint64_t>(0xFFFFFFF0ull, h->pool_cap + std::max<uint64_t>(N / 2, 4 * slack));
+        uint32_t *np = nullptr;
+        int rc = dev_alloc(&np, ncap);
+        if (rc == BPE_OK) {
+            HIP_TRY(hipMemcpyAsync(np, P->B.pool, h->pool_top * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            P->owned.erase(std::find(P->owned.begin(), P->owned.end(), (void *)P->B.pool));
+            dfree(P->B.pool);
+            P->B.pool = np;
+            P->owned.push_back(np);
+            h->pool_cap = ncap;
+            HIP_TRY(hipMemcpyAsync(&P->d_ctl->pool_cap, &h->pool_cap, sizeof h->pool_cap,
+                                   hipMemcpyHostToDevice, s));
+        } else {
+            (void)hipGetLastError();   // (no memory: the pool fills, and the batch hands over)
+        }
+    }
+    if (h->used * 20 > P->cap * 9 && h->tie == PIX_TIE_NONE && P->cap * 2 < (1ull << 31)) {
+        const uint64_t ncap = P->cap * 2;
+        PixTable T = P->T;
+        T.mask = (uint32_t)(ncap - 1);
+        T.nblocks = (uint32_t)(ncap / PIX_B);
+        T.nsuper = (T.nblocks + PIX_SB - 1) / PIX_SB;
+        std::vector<void *> fresh;
+        auto get = [&](auto **q, size_t n) {
+            const int r = dev_alloc(q, n);
+            if (r == BPE_OK) fresh.push_back(*q);
+            return r;
+        };
+        uint32_t *dblocks = nullptr, *dsuper = nullptr;
+        if (get(&T.keys, ncap) || get(&T.cnt, ncap) || get(&T.off, ncap) || get(&T.len, ncap) ||
+            get(&T.fill, ncap) || get(&T.bmax, T.nblocks) || get(&T.sbmax, T.nsuper) ||
+            get(&T.bdirty, T.nblocks) || get(&T.sbdirty, T.nsuper) || get(&dblocks, T.nblocks) ||
+            get(&dsuper, T.nsuper)) {
+            for (void *q : fresh) dfree(q);
+            (void)hipGetLastError();
+            return BPE_OK;   // (no memory: the table fills, and the batch hands over)
+        }
+        HIP_TRY(hipMemsetAsync(T.keys, 0xFF, ncap * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(T.bdirty, 0, T.nblocks * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(T.sbdirty, 0, T.nsuper * sizeof(uint32_t), s));
+        k_pix_rehash<<<4096, 256, 0, s>>>(P->T, T, P->d_ctl, (uint32_t)P->cap);
+        // (the old table's dirty lists name its blocks: every block max is recomputed instead)
+        h->n_dblocks = h->n_dsuper = 0;
+        h->used_cap = ncap / 10 * 7;
+        HIP_TRY(hipMemcpyAsync(&P->d_ctl->n_dblocks, &h->n_dblocks, 2 * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(&P->d_ctl->used_cap, &h->used_cap, sizeof h->used_cap,
+                               hipMemcpyHostToDevice, s));
+        PixBufs B = P->B;
+        B.dblocks = dblocks;
+        B.dsuper = dsuper;
+        k_pix_bmax_all<<<4096, 256, 0, s>>>(T);
+        k_pix_sbmax<<<1024, 256, 0, s>>>(T, B, P->d_ctl, 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h->err) return fail(BPE_ERR_STATE, "bpe native: position index: rehash overflow");
+        for (void *q : {(void *)P->T.keys, (void *)P->T.cnt, (void *)P->T.off, (void *)P->T.len,
+                        (void *)P->T.fill, (void *)P->T.bmax, (void *)P->T.sbmax, (void *)P->T.bdirty,
+                        (void *)P->T.sbdirty, (void *)P->B.dblocks, (void *)P->B.dsuper}) {
+            P->owned.erase(std::find(P->owned.begin(), P->owned.end(), q));
+            dfree(q);
+        }
+        for (void *q : fresh) P->owned.push_back(q);
+        P->T = T;
+        P->B = B;
+        P->cap = ncap;
+    }
+    return BPE_OK;
+}
+
+int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned long long *xchg,
+                   unsigned long long *tie, int rank, int world, int64_t *n_words) {
+    int rc;
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    if ((rc = pix_reserve(c))) return rc;
+    const int64_t base = (int64_t)c->h_len16.size();
+    if ((rc = ensure_len16_cap(c, base + LOOP_BATCH))) return rc;
+    if ((rc = sync_len16(c, 1))) return rc;
+    P->T.len16 = c->d_len16;
+    if (P->max_length != max_length) {
+        // (the selection keys filter on max_length: every block max again)
+        P->max_length = max_length;
+        P->T.ml = max_length;
+        k_pix_bmax_all<<<4096, 256, 0, s>>>(P->T);
+        k_pix_sbmax<<<1024, 256, 0, s>>>(P->T, P->B, P->d_ctl, 1);
+    }
+    P->T.delta = xchg;
+    const int64_t nw = XCHG_HDR + DELTA_ROWS * std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
+    // (delta pending: the last batch's last merge's rows are in xchg, for this batch's first
+    // all-reduce; else all of it zero: the rows past this batch's words are read by later ones)
+    if (!c->rl_delta_pending)
+        HIP_TRY(hipMemsetAsync(xchg, 0, XCHG_WORDS * sizeof(unsigned long long), s));
+    k_pix_rank_begin<<<1, 1, 0, s>>>(P->d_ctl, LOOP_BATCH, (int32_t)base,
+                                     min_weight == 0 ? 2 : min_weight);   // core.ts:256
+    HIP_TRY(hipGetLastError());
+    c->opt_max_length = max_length;
+    c->rl_table = xchg;
+    c->rl_tie = tie;
+    c->rl_rank = rank;
+    c->rl_world = world;
+    c->rl_base = base;
+    c->rl_enqueued = 0;
+    c->rl_max_length = max_length;
+    c->rl_open = true;
+    *n_words = nw;
+    return BPE_OK;
+}
+
+int pix_rank_select(bpe_ctx *c) {
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    hipEvent_t e = span_begin(c);
+    k_pix_apply_delta<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->rl_table);
+    k_pix_dirty<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+    k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
+    k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
+    k_pix_export<<<1, 64, 0, s>>>(P->d_ctl, c->rl_table, c->rl_tie, c->rl_rank);
+    HIP_TRY(hipGetLastError());
+    return span_end(c, e, 1);
+}
+
+int pix_rank_decide(bpe_ctx *c) {
+    k_pix_decide<<<1, 1, 0, c->stream>>>(c->pix->d_ctl, c->rl_tie);
+    HIP_TRY(hipGetLastError());
+    return BPE_OK;
+}
+
+int pix_rank_count(bpe_ctx *c) {
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    hipEvent_t e = span_begin(c);
+    k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+    k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, P->d_log);
+    HIP_TRY(hipGetLastError());
+    c->rl_enqueued += 1;
+    return span_end(c, e, 0);
+}
+
+int pix_rank_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *status) {
+    c->rl_open = false;
+    PixState *P = c->pix;
+    hipStream_t s = c->stream;
+    PixCtl *h = P->h_ctl;
+    HIP_TRY(hipMemcpyAsync(h, P->d_ctl, sizeof *h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(P->h_log, P->d_log, PIX_LOG * std::max<int64_t>(1, c->rl_enqueued) * sizeof(long long),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->status == PIX_ERROR) {
+        const int err = h->err;
+        const unsigned long long got = h->n_check, W = h->W;
+        LEAVE_GLOBAL(c);
+        char msg[200];
+        if (err == 21)
+            snprintf(msg, sizeof msg, "bpe native: rank loop (incremental): the shards' replacement "
+                     "counts sum to %llu, not W = %llu", got, W);
+        else
+            snprintf(msg, sizeof msg, "bpe native: rank loop (incremental): position index "
+                     "inconsistent (code %d)", err);
+        return fail(BPE_ERR_STATE, msg);
+    }
+    const int64_t nd = h->n_done;
+    if (nd < 0 || nd > c->rl_enqueued) return fail(BPE_ERR_STATE, "bpe native: rank loop: bad merge count");
+    const int64_t base = c->rl_base;
+    c->h_len16.resize(base + nd, 1);
+    c->h_count.resize(base + nd, 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        const long long *m = P->h_log + PIX_LOG * i;
+        const int32_t a = (int32_t)m[0], b = (int32_t)m[1];
+        const int64_t W = m[2], R = m[3];
+        const int64_t cc = base + i;
+        c->h_len16[cc] = c->h_len16[a] + c->h_len16[b];                // core.ts:318
+        if (c->stats_on) {
+            c->stats.iterations += 1;
+            c->stats.live_tokens += c->n_live;
+            c->stats.pix_merges += 1;
+        }
+        c->n_live -= R;
+        c->live_slots -= R;
+        c->h_count[a] -= R;
+        c->h_count[b] -= R;
+        c->h_count[cc] += R;
+        if (i < cap) {
+            out[4 * i] = a;
+            out[4 * i + 1] = b;
+            out[4 * i + 2] = W;
+            out[4 * i + 3] = R;
+        }
+    }
+    c->len16_lo = base + nd;   // (pix_commit wrote the new lengths on the device)
+    const int st = h->status == PIX_DONE ? LOOP_DONE : h->status == PIX_HOST ? LOOP_HOST : LOOP_RUN;
+    if (st != LOOP_RUN) {
+        static const bool dbg = getenv("BPE_DEBUG_PIX") != nullptr;
+        if (dbg)
+            fprintf(stderr, "[bpe debug] rank %d: incremental rank loop hands over after %lld merges "
+                    "(status %d, code %d, used %llu of %llu, pool %llu of %llu, candidates %u)\n",
+                    c->rl_rank, (long long)nd, h->status, h->err, h->used, h->used_cap, h->pool_top,
+                    h->pool_cap, h->n_cand);
+        if (c->stats_on && st == LOOP_HOST) c->stats.pix_host += 1;
+        LEAVE_GLOBAL(c);   // (the host takes over: the corpus back to the chunk layout)
+    } else {
+        c->rl_delta_pending = h->merged != 0;
+    }
+    *n_done = nd;
+    *status = st;
+    return BPE_OK;
 }
 
 #define MULTI(call) \
@@ -2550,7 +2873,7 @@ int bpe_merge_until(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t 
 }
 
 int bpe_set_mode(bpe_ctx *c, int mode) {
-    NOT_MULTI;
+    if (mode == BPE_MODE_STREAM || mode == BPE_MODE_INCREMENTAL) MULTI(set_mode(c->multi, mode));
     if (!c || (mode != BPE_MODE_STREAM && mode != BPE_MODE_INCREMENTAL))
         return fail(BPE_ERR_ARG, "bpe native: bad mode");
     c->use_pix = mode == BPE_MODE_INCREMENTAL;
@@ -2562,7 +2885,7 @@ int bpe_export_counts(bpe_ctx *c, uint64_t *table) {
     if (!c || !table) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     if (!table_ok(c))
         if ((rc = run_pass(c, false, 0, 0, 0, nullptr))) return rc;
@@ -2578,7 +2901,7 @@ int bpe_heavy_counts(bpe_ctx *c, const uint64_t *table, int64_t max_length, uint
     if (!c || !table || !n_cold || cap < 0) return fail(BPE_ERR_ARG, "bpe native: null argument");
     int rc = set_device(c);
     if (rc) return rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     if ((rc = sync_len16(c, max_length))) return rc;
     hipStream_t s = c->stream;
@@ -2697,16 +3020,49 @@ int bpe_recount(bpe_ctx *c) {
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
     if (rc) return rc;
-    leave_global(c);
+    LEAVE_GLOBAL(c);
     if ((rc = settle(c))) return rc;
     return run_pass(c, false, 0, 0, 0, nullptr);
+}
+
+// (internal, bpe_multi.cpp) the exchange of shards that share one device: the sum (or max) of the
+// shards' buffers written back to every one of them, on `stream` (which the caller orders after
+// every shard's producer and before every shard's consumer with events).  No host copies.
+}  // extern "C"
+namespace {
+struct ShardBufs {
+    unsigned long long *p[BPE_MAX_SHARDS_ONE_DEVICE];
+};
+__global__ void __launch_bounds__(256) k_sum_shards(ShardBufs b, int n, size_t count, int take_max) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long v = b.p[0][i];
+        for (int r = 1; r < n; ++r) {
+            const unsigned long long x = b.p[r][i];
+            v = take_max ? (x > v ? x : v) : v + x;
+        }
+        for (int r = 0; r < n; ++r) b.p[r][i] = v;
+    }
+}
+}  // namespace
+extern "C" {
+int bpe_sum_shards(unsigned long long *const *bufs, int n, size_t count, int take_max, void *stream) {
+    if (n < 1 || n > BPE_MAX_SHARDS_ONE_DEVICE) return fail(BPE_ERR_ARG, "bpe native: too many shards on one device");
+    ShardBufs b{};
+    for (int r = 0; r < n; ++r) b.p[r] = bufs[r];
+    const unsigned grid = (unsigned)std::min<size_t>(1024, (count + 255) / 256 + 1);
+    k_sum_shards<<<grid, 256, 0, (hipStream_t)stream>>>(b, n, count, take_max);
+    HIP_TRY(hipGetLastError());
+    return BPE_OK;
 }
 
 // (internal, bpe_multi.cpp) the corpus of one shard changed outside the rank loop: every shard
 // leaves the replicated global tables, so the next batch starts from the table state on all alike
 int bpe_leave_global(bpe_ctx *c) {
     if (!c || c->multi) return fail(BPE_ERR_ARG, "bpe native: bad shard context");
-    leave_global(c);
+    const int rc = set_device(c);
+    if (rc) return rc;
+    LEAVE_GLOBAL(c);
     return BPE_OK;
 }
 

@@ -32,6 +32,8 @@
 #include <string>
 #include <vector>
 
+extern "C" int bpe_leave_global(bpe_ctx *c);
+
 namespace {
 
 constexpr int64_t RANK_SHIFT = 40;   // as sharded.py / k_tie_export: rank << 40 | position
@@ -67,8 +69,18 @@ struct bpe_multi {
     // host-protocol iterations in a row that needed exact cold counts (two: enter that state)
     bool maintained = false;
     int heavy_streak = 0;
+    // the incremental mode (bpe_set_mode): the global state lives in every shard's position
+    // index, entered at the first batch; entries counts them (one index build each), and a run
+    // whose batches keep handing over goes on in the streaming mode (pix_off)
+    bool pix = false, pix_off = false;
+    int64_t pix_entries = 0;
     std::vector<ncclComm_t> comms;
     Rccl rccl;
+    // shards sharing one device (the one-GPU test box, BPE_REDUCE_HOST): the exchange is a device
+    // kernel on shard 0's stream, ordered by events, with no host copies or syncs
+    bool one_device = false;
+    std::vector<hipEvent_t> ev;
+    hipEvent_t ev_done = nullptr;
 };
 
 namespace {
@@ -128,7 +140,19 @@ int all_reduce(bpe_multi *m, std::vector<unsigned long long *> &buf, size_t coun
         }
         return nccl_check(m, m->rccl.group_end(), "ncclGroupEnd");
     }
-    // host copies (shards sharing a device): after each shard's stream has produced its part
+    if (m->one_device) {
+        MHIP(hipSetDevice(m->dev[0]));
+        for (int r = 0; r < m->n; ++r) {
+            MHIP(hipEventRecord(m->ev[r], m->st[r]));
+            MHIP(hipStreamWaitEvent(m->st[0], m->ev[r], 0));
+        }
+        MTRY(bpe_sum_shards(buf.data(), m->n, count, max ? 1 : 0, m->st[0]));
+        MHIP(hipEventRecord(m->ev_done, m->st[0]));
+        for (int r = 1; r < m->n; ++r) MHIP(hipStreamWaitEvent(m->st[r], m->ev_done, 0));
+        return BPE_OK;
+    }
+    // host copies (shards on several devices without RCCL): after each shard's stream has
+    // produced its part
     for (int r = 0; r < m->n; ++r) {
         MHIP(hipSetDevice(m->dev[r]));
         MHIP(hipMemcpyAsync(m->h_buf, buf[r], count * 8, hipMemcpyDeviceToHost, m->st[r]));
@@ -239,6 +263,18 @@ int multi_create(bpe_multi **out, int n, const int *devices, int reduce) {
             hipMemset(m->d_tie[r], 0xA5, BPE_TIE_WORDS * 8) != hipSuccess)
             return bail(bpe_fail(BPE_ERR_OOM, "bpe native: multi-device buffers"));
     }
+    m->one_device = reduce == BPE_REDUCE_HOST && n <= BPE_MAX_SHARDS_ONE_DEVICE &&
+                    std::all_of(m->dev.begin(), m->dev.end(), [&](int d) { return d == m->dev[0]; }) &&
+                    !getenv("BPE_HOST_EXCHANGE");   // (A/B knob: the host-copy exchange)
+    if (m->one_device) {
+        (void)hipSetDevice(m->dev[0]);
+        m->ev.assign(n, nullptr);
+        for (int r = 0; r < n; ++r)
+            if (hipEventCreateWithFlags(&m->ev[r], hipEventDisableTiming) != hipSuccess)
+                return bail(bpe_fail(BPE_ERR_HIP, "bpe native: hipEventCreate failed"));
+        if (hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess)
+            return bail(bpe_fail(BPE_ERR_HIP, "bpe native: hipEventCreate failed"));
+    }
     if (hipHostMalloc((void **)&m->h_buf, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&m->h_sum, BPE_XCHG_WORDS * 8, hipHostMallocDefault) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_OOM, "bpe native: pinned host buffers"));
@@ -267,6 +303,9 @@ int multi_destroy(bpe_multi *m) {
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
     }
+    for (auto e : m->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (m->ev_done) (void)hipEventDestroy(m->ev_done);
     if (m->h_buf) (void)hipHostFree(m->h_buf);
     if (m->h_sum) (void)hipHostFree(m->h_sum);
     if (m->rccl.so) dlclose(m->rccl.so);
@@ -279,6 +318,16 @@ int multi_shard_count(bpe_multi *m, int *n) {
     return BPE_OK;
 }
 
+int multi_set_mode(bpe_multi *m, int mode) {
+    for (auto s : m->sh) MTRY(bpe_set_mode(s, mode));
+    m->pix = mode == BPE_MODE_INCREMENTAL;
+    m->pix_off = false;
+    m->maintained = false;   // (the next batch enters the mode's own global state)
+    m->heavy_streak = 0;
+    for (auto s : m->sh) MTRY(bpe_leave_global(s));
+    return BPE_OK;
+}
+
 // ---- vocabulary and corpus ------------------------------------------------------------------------
 int multi_set_token_len16(bpe_multi *m, int32_t id, int32_t len16) {
     for (auto s : m->sh) MTRY(bpe_set_token_len16(s, id, len16));
@@ -286,8 +335,6 @@ int multi_set_token_len16(bpe_multi *m, int32_t id, int32_t len16) {
 }
 
 int check_vocab(bpe_multi *m, int32_t *n_tokens);
-
-extern "C" int bpe_leave_global(bpe_ctx *c);
 
 // A sample added to the last shard reseals only that shard, which drops its replicated global
 // tables (the maintained state).  Every shard must leave that state alike, or the next batch's
@@ -633,7 +680,7 @@ int enter_maintained(bpe_multi *m) {
     m->maintained = true;
     m->heavy_streak = 0;
     static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
-    if (dbg) MTRY(debug_compare_global(m, -1));
+    if (dbg && !m->pix) MTRY(debug_compare_global(m, -1));
     return BPE_OK;
 }
 
@@ -720,7 +767,16 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
         int status = 2;
         bool batch_maintained = false;
         if (want > 0) {
-            if (!m->maintained && m->heavy_streak >= 2) MTRY(enter_maintained(m));
+            // (the incremental mode enters its global state, the shards' position indexes, at
+            // once; the streaming mode when the cold pairs outgrow the sketch)
+            const bool pix = m->pix && !m->pix_off;
+            if (!m->maintained && (m->heavy_streak >= 2 || pix)) {
+                if (pix && ++m->pix_entries > 64 && m->pix_entries > n / 16) {
+                    m->pix_off = true;   // (the index keeps handing over here: the stream goes on)
+                    for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
+                }
+                MTRY(enter_maintained(m));
+            }
             batch_maintained = m->maintained;
             int64_t nw = -1;
             for (int r = 0; r < m->n; ++r) {
@@ -758,7 +814,7 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                 put((int32_t)log[0][4 * i], (int32_t)log[0][4 * i + 1], log[0][4 * i + 2]);
             }
             static const bool dbg = getenv("BPE_DEBUG_GLOBAL") != nullptr;
-            if (dbg && batch_maintained && status == 0) MTRY(debug_compare_global(m, n));
+            if (dbg && batch_maintained && status == 0 && !m->pix) MTRY(debug_compare_global(m, n));
             if (status != 0) m->maintained = false;   // (the shards left the global state)
             if (status == 1) break;                                        // no pair qualifies
             if (status == 0) {
@@ -818,6 +874,10 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.tie_lone += x.tie_lone;
         acc.loop_host = std::max(acc.loop_host, x.loop_host);
         acc.fused_passes += x.fused_passes;
+        acc.pix_builds += x.pix_builds;
+        acc.pix_merges += x.pix_merges;
+        acc.pix_host = std::max(acc.pix_host, x.pix_host);
+        acc.pix_build_ms = std::max(acc.pix_build_ms, x.pix_build_ms);
     }
     *out = acc;
     return BPE_OK;

@@ -35,6 +35,12 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out);
 int multi_reset_stats(bpe_multi *m);
 int multi_get_stream(bpe_multi *m, void **stream);
 int multi_shard_count(bpe_multi *m, int *n);
+int multi_set_mode(bpe_multi *m, int mode);
+
+// shards that share one device exchange through a device kernel (bpe_engine.hip)
+constexpr int BPE_MAX_SHARDS_ONE_DEVICE = 16;
+extern "C" int bpe_sum_shards(unsigned long long *const *bufs, int n, size_t count, int take_max,
+                              void *stream);
 
 // error reporting shared with bpe_engine.hip
 int bpe_fail(int code, const char *msg);

@@ -38,6 +38,9 @@ constexpr int PIX_SB = 256;                   // blocks per superblock
 constexpr int PIX_WALK = 1 << 16;             // longest run / chain one thread walks
 constexpr int PIX_PROBE = 4096;               // longest probe sequence in the table
 constexpr int PIX_GRID = 1024;                // blocks of the grid-stride kernels
+constexpr uint32_t PIX_MAX_SLOTS = 0xFFFF0000u;  // largest slot array (u32 positions, PIX_NONE free)
+
+constexpr int PIX_LOG = 4;                    // log words per merge: a, b, W, this shard's sites
 
 // PIX_PAUSE: the batch's merges are done (the next batch goes on)
 enum PixStatus { PIX_RUN = 0, PIX_DONE = 1, PIX_HOST = 2, PIX_ERROR = 3, PIX_PAUSE = 4 };
@@ -49,6 +52,10 @@ struct PixCorpus {
 };
 
 struct PixTable {
+    // A shard of a sharded corpus (the rank loop): cnt holds the GLOBAL counts, kept merge by merge
+    // from the summed delta rows (include/bpe.h BPE_XCHG_*); this shard's count changes go to its
+    // delta rows (delta != nullptr) instead of cnt.  The lists stay this shard's own.
+    unsigned long long *delta;
     int32_t *len16;          // UTF-16 lengths (max_length filter)
     long long ml;            // max_length of this index's selections
     uint32_t *keys;
@@ -84,6 +91,9 @@ struct PixCtl {
     unsigned long long used, used_cap; // table claims / the claims it may hold
     uint32_t cand_slot[MAX_CAND];
     unsigned long long last[MAX_CAND];
+    // sharded (delta rows): the last merge's rows are still to be added (k_pix_apply_delta); this
+    // shard's sites of the merge being made (the header word the shards' sum must equal W in)
+    uint32_t merged, pad1;
 };
 
 __device__ __forceinline__ uint32_t pix_key(int32_t u, int32_t v) {
@@ -166,8 +176,22 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
 // only matters to the entry that was its block's max, whose block is then recomputed after the
 // merge's count changes (k_pix_alloc).  (The block max is read beside the add: no block max
 // changes while k_pix_sites runs.)
+// A shard of a sharded corpus: the change goes to this shard's delta row of the pair (every pair a
+// merge (a, b) -> c changes has a side in {a, b, c}: delta_slot), summed over the shards and added
+// to every shard's global counts by k_pix_apply_delta.
+__device__ __forceinline__ void pix_delta(const PixTable &t, const PixCtl *ctl, uint32_t key,
+                                          long long d) {
+    if (d) atomicAdd(&t.delta[delta_slot((int32_t)(key >> 16), (int32_t)(key & 0xFFFFu), ctl->a,
+                                         ctl->b, ctl->c)],
+                     (unsigned long long)d);
+}
+
 __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
                                             uint32_t key, long long d, PixProbe pr) {
+    if (t.delta) {   // (sharded: no slot needed, the count is global)
+        pix_delta(t, ctl, key, d);
+        return PIX_NONE;
+    }
     const uint32_t s = pix_slot(t, ctl, key, true, false, pr);
     if (s == PIX_NONE) {
         pix_fail(ctl, 1);
@@ -192,17 +216,29 @@ __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B,
 }
 
 // A new adjacency (u, v) at slot pos (u or v is c): its count, one more slot in its segment, the
-// entry at index e of this merge's entry list (e = ~0u: the next free one).  The entry that
-// opened the pair's segment carries PIX_OWNER: k_pix_alloc places the segment from it.
+// entry at index e of this merge's entry list (e = ~0u: the next free one), (table slot, pos).
+// The entry that opened the pair's segment carries PIX_OWNER in its table slot (the table holds
+// fewer than 2^31 slots, so that bit is free; positions use all 32 bits): k_pix_alloc places the
+// segment from it.
 constexpr uint32_t PIX_OWNER = 0x80000000u;
 __device__ __forceinline__ void pix_entry(const PixTable &t, const PixBufs &B, PixCtl *ctl,
                                           uint32_t key, uint32_t pos, long long d, uint32_t e,
                                           PixProbe pr) {
-    const uint32_t s = pix_add(t, B, ctl, key, d, pr);
-    if (s == PIX_NONE) return;
+    uint32_t s;
+    if (t.delta) {   // sharded: the list entry needs this shard's slot, the count a delta row
+        s = pix_slot(t, ctl, key, true, false, pr);
+        if (s == PIX_NONE) {
+            pix_fail(ctl, 1);
+            return;
+        }
+        pix_delta(t, ctl, key, d);
+    } else {
+        s = pix_add(t, B, ctl, key, d, pr);
+        if (s == PIX_NONE) return;
+    }
     const uint32_t owner = atomicAdd(&t.len[s], 1u) == 0u ? PIX_OWNER : 0u;
     if (e == ~0u) e = atomicAdd(&ctl->n_ent, 1u);
-    if (e < B.ent_cap) B.ent[e] = make_uint2(s, pos | owner);
+    if (e < B.ent_cap) B.ent[e] = make_uint2(s | owner, pos);
     else pix_fail(ctl, 3);
 }
 
@@ -237,9 +273,10 @@ __device__ __forceinline__ bool pix_tok_is(const PixCorpus &C, uint32_t p, int32
 // position with global atomics (65536 hot addresses, 2 atomics per position: 150 ms at C3).
 constexpr int PB = 4096;          // positions per build block
 
-__device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t *red) {
+// (run starts are u32 positions; 0 is the identity of their max: position 0 always starts a run)
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *red) {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     v = max(max(red[0], red[1]), max(red[2], red[3]));
@@ -247,28 +284,28 @@ __device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t *red) {
     return v;
 }
 
-__global__ void __launch_bounds__(256) k_pix_build_links(PixCorpus C, int32_t *__restrict__ blast) {
-    __shared__ int32_t red[4];
+__global__ void __launch_bounds__(256) k_pix_build_links(PixCorpus C, uint32_t *__restrict__ blast) {
+    __shared__ uint32_t red[4];
     const uint32_t nblk = (C.n + PB - 1) / PB;
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const uint32_t i0 = blk * PB, i1 = min(i0 + PB, C.n);
-        int32_t m = -1;
+        uint32_t m = 0;
         for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) {
             const int32_t t = C.tok[i];
-            if (i == 0 || C.tok[i - 1] != t) m = (int32_t)i;   // (i grows: the last one wins)
+            if (i == 0 || C.tok[i - 1] != t) m = i;   // (i grows: the last one wins)
             C.nxt[i] = i + 1 < C.n ? i + 1 : PIX_NONE;
             C.prv[i] = i > 0 ? i - 1 : PIX_NONE;
         }
-        m = block_max_i32(m, red);
+        m = block_max_u32(m, red);
         if (threadIdx.x == 0) blast[blk] = m;
     }
 }
 
-// In place: v[b] <- max(v[0 .. b-1]) (-1 for b = 0).  One block of 1024.
-__global__ void __launch_bounds__(1024) k_pix_scan_max(int32_t *__restrict__ v, uint32_t n) {
-    __shared__ int32_t part[1024];
+// In place: v[b] <- max(v[0 .. b-1]) (0 for b = 0).  One block of 1024.
+__global__ void __launch_bounds__(1024) k_pix_scan_max(uint32_t *__restrict__ v, uint32_t n) {
+    __shared__ uint32_t part[1024];
     const uint32_t per = (n + 1023) / 1024, t = threadIdx.x;
-    int32_t acc = -1;
+    uint32_t acc = 0;
     for (uint32_t k = 0; k < per; ++k) {
         const uint32_t i = t * per + k;
         if (i < n) acc = max(acc, v[i]);
@@ -276,16 +313,16 @@ __global__ void __launch_bounds__(1024) k_pix_scan_max(int32_t *__restrict__ v, 
     part[t] = acc;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const int32_t o = t >= d ? part[t - d] : -1;
+        const uint32_t o = t >= d ? part[t - d] : 0u;
         __syncthreads();
         part[t] = max(part[t], o);
         __syncthreads();
     }
-    int32_t run = t ? part[t - 1] : -1;
+    uint32_t run = t ? part[t - 1] : 0u;
     for (uint32_t k = 0; k < per; ++k) {
         const uint32_t i = t * per + k;
         if (i < n) {
-            const int32_t x = v[i];
+            const uint32_t x = v[i];
             v[i] = run;
             run = max(run, x);
         }
@@ -366,12 +403,12 @@ __device__ __forceinline__ void ph_put(int32_t *tk, const PhNext &r) {
 }
 
 template <bool RS>
-__device__ __forceinline__ int32_t ph_runs(const PixCorpus &C, int32_t *tk, int32_t *sc,
-                                           uint32_t blk, int32_t carry);
+__device__ __forceinline__ uint32_t ph_runs(const PixCorpus &C, int32_t *tk, uint32_t *sc,
+                                            uint32_t blk, uint32_t carry);
 
 template <bool RS>
-__device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int32_t *sc,
-                                           uint32_t blk, int32_t carry) {
+__device__ __forceinline__ uint32_t ph_span(const PixCorpus &C, int32_t *tk, uint32_t *sc,
+                                            uint32_t blk, uint32_t carry) {
     const uint32_t b0 = blk * PB;
     for (uint32_t k = threadIdx.x; k <= (uint32_t)PB; k += PH_T) {
         const uint32_t i = b0 + k;
@@ -383,29 +420,29 @@ __device__ __forceinline__ int32_t ph_span(const PixCorpus &C, int32_t *tk, int3
 
 // The run start that this thread's first position continues (tk staged)
 template <bool RS>
-__device__ __forceinline__ int32_t ph_runs(const PixCorpus &C, int32_t *tk, int32_t *sc,
-                                           uint32_t blk, int32_t carry) {
-    if (!RS) return -1;
+__device__ __forceinline__ uint32_t ph_runs(const PixCorpus &C, int32_t *tk, uint32_t *sc,
+                                            uint32_t blk, uint32_t carry) {
+    if (!RS) return 0;
     const uint32_t b0 = blk * PB;
     const uint32_t l0 = threadIdx.x * PH_PER;
-    int32_t last = -1;
+    uint32_t last = 0;   // (0: none here; the max over the positions before still holds one)
 #pragma unroll
     for (int k = 0; k < PH_PER; ++k) {
         const uint32_t l = l0 + k, i = b0 + l;
-        if (i < C.n && (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != tk[l])) last = (int32_t)i;
+        if (i < C.n && (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != tk[l])) last = i;
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int32_t v = last;
+    uint32_t v = last;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const int32_t o = __shfl_up(v, d);
+        const uint32_t o = __shfl_up(v, d);
         if (lane >= d) v = max(v, o);
     }
     if (lane == 63) sc[wv] = v;
     __syncthreads();
-    int32_t rs = carry;
+    uint32_t rs = carry;
     for (int w = 0; w < wv; ++w) rs = max(rs, sc[w]);
-    const int32_t ex = __shfl_up(v, 1);
+    const uint32_t ex = __shfl_up(v, 1);
     return lane ? max(rs, ex) : rs;
 }
 
@@ -414,12 +451,12 @@ __device__ __forceinline__ int32_t ph_runs(const PixCorpus &C, int32_t *tk, int3
 // whose adds saw some half at >= 0x4000 ends with a sweep that moves every such half into the
 // workgroup's slab entry (global, zeroed by the host), so no half passes 0x4000 + PB.
 __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t, PixCtl *ctl,
-                                                        const int32_t *__restrict__ carry,
+                                                        const uint32_t *__restrict__ carry,
                                                         uint32_t *__restrict__ slab,
                                                         unsigned long long *__restrict__ oddxx) {
     __shared__ uint32_t cnt[32768];
     __shared__ int32_t tk[PB + 1];
-    __shared__ int32_t sc[PH_T / 64];
+    __shared__ uint32_t sc[PH_T / 64];
     __shared__ uint32_t odd[256];
     __shared__ uint32_t s_sweep;
     const uint32_t G = gridDim.x;
@@ -438,7 +475,7 @@ __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t,
         if (threadIdx.x == 0) s_sweep = 0;
         ph_put(tk, nx);
         if (blk + G < nblk) ph_fetch(C, blk + G, nx);
-        int32_t rs = ph_runs<true>(C, tk, sc, blk, carry[blk]);
+        uint32_t rs = ph_runs<true>(C, tk, sc, blk, carry[blk]);
         const uint32_t l0 = threadIdx.x * PH_PER, i0 = blk * PB + l0;
         uint32_t seen = 0;
 #pragma unroll
@@ -446,9 +483,9 @@ __global__ void __launch_bounds__(PH_T) k_pix_hot_count(PixCorpus C, PixTable t,
             const uint32_t l = l0 + k, i = i0 + k;
             if (i >= C.n) break;
             const int32_t x = tk[l], y = i + 1 < C.n ? tk[l + 1] : SEP;
-            if (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != x) rs = (int32_t)i;
+            if (i == 0 || (l ? tk[l - 1] : C.tok[i - 1]) != x) rs = i;
             if ((x | y) < 0) continue;
-            const bool uncounted = x == y && ((i - (uint32_t)rs) & 1u);
+            const bool uncounted = x == y && ((i - rs) & 1u);
             if ((x | y) < 256) {
                 const uint32_t p = ((uint32_t)x << 8) | (uint32_t)y;
                 seen |= atomicAdd(&cnt[p >> 1], 1u << ((p & 1u) << 4));
@@ -904,7 +941,9 @@ __global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long
 // and k_pix_apply do nothing; the next k_pix_select commits the decided pair.  (A separate tie
 // launch cost 5.5 us per merge for the 372 ties among the 8000 C3 merges; one block scanning the
 // lists took ~240 us per tie.)
-enum PixTie { PIX_TIE_NONE = 0, PIX_TIE_SCAN = 1, PIX_TIE_DECIDED = 2 };
+// Sharded: the scan leaves this shard's last counted occurrences (PIX_TIE_WAIT); k_pix_decide takes
+// the earliest of the all-reduced (shard << 40 | position) after the exchange.
+enum PixTie { PIX_TIE_NONE = 0, PIX_TIE_SCAN = 1, PIX_TIE_DECIDED = 2, PIX_TIE_WAIT = 3 };
 
 // The merge of pair slot s (key `key`, list length len): vocabulary and table-room checks, then
 // the decision every later kernel reads.  (Thread 0 of k_pix_select.)
@@ -914,8 +953,10 @@ __device__ void pix_commit(const PixTable &t, PixCtl *ctl, uint32_t s, uint32_t 
         ctl->err = 5;
         return;
     }
-    // room for this merge's claims (<= 2 per site) within the table's fill limit
-    if (ctl->used + 2 * (unsigned long long)len + 64 > ctl->used_cap) {
+    // room for this merge's claims (<= 2 per site; sharded: also the pairs other shards create,
+    // <= 2 per global occurrence) within the table's fill limit
+    const unsigned long long need = 2 * max((unsigned long long)len, t.delta ? ctl->W : 0ull) + 64;
+    if (ctl->used + need > ctl->used_cap) {
         ctl->status = PIX_HOST;
         ctl->err = 6;
         return;
@@ -990,6 +1031,7 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         ctl->n_sites = ctl->n_ent = ctl->n_dblocks = ctl->n_dsuper = 0;
         ctl->n_cand = 0;
         ctl->n_check = 0;
+        ctl->merged = 0;   // (sharded: its delta rows were added by k_pix_apply_delta)
         n_lst = n_blk = n_cs = 0;
     }
     if (s_go == 1) {
@@ -1054,6 +1096,17 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         }
         ctl->best = best;
         ctl->W = (unsigned long long)W;
+        // (sorted by key: the shards of a sharded corpus index their tie words alike)
+        for (uint32_t i = 1; i < nc; ++i)
+            for (uint32_t j = i; j > 0 && cs_key[j - 1] > cs_key[j]; --j) {
+                const uint32_t k0 = cs_key[j], s0 = cs[j], l0 = cs_len[j];
+                cs_key[j] = cs_key[j - 1];
+                cs[j] = cs[j - 1];
+                cs_len[j] = cs_len[j - 1];
+                cs_key[j - 1] = k0;
+                cs[j - 1] = s0;
+                cs_len[j - 1] = l0;
+            }
         if (nc == 1) {
             pix_commit(t, ctl, cs[0], cs_key[0], cs_len[0]);
         } else {
@@ -1124,10 +1177,18 @@ __device__ void pix_tie_scan(const PixCorpus &C, const PixTable &t, const PixBuf
             }
             if (k & 1) m = (unsigned long long)C.prv[p] + 1;
         }
+        if (t.delta) {
+            ctl->last[q] = m;   // (this shard's; the decision waits for the exchange)
+            continue;
+        }
         if (m && m < bp) {
             bp = m;
             bj = q;
         }
+    }
+    if (t.delta) {
+        ctl->tie = PIX_TIE_WAIT;
+        return;
     }
     if (bp == ~0ull) {
         ctl->status = PIX_ERROR;
@@ -1379,8 +1440,8 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
         const uint32_t i = i0 + threadIdx.x;
         uint2 e = make_uint2(PIX_NONE, 0);
         if (i < ne) e = B.ent[i];
-        const bool own = e.x != PIX_NONE && (e.y & PIX_OWNER);
-        const unsigned long long len = own ? t.len[e.x] : 0;
+        const bool own = e.x != PIX_NONE && (e.x & PIX_OWNER);
+        const unsigned long long len = own ? t.len[e.x & ~PIX_OWNER] : 0;
         unsigned long long incl = len;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -1408,9 +1469,10 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
             pix_fail(ctl, 16);
             continue;
         }
-        const uint32_t s = e.x;
+        const uint32_t s = e.x & ~PIX_OWNER;
         t.off[s] = (uint32_t)o;
         t.fill[s] = 0;
+        if (t.delta) continue;   // (sharded: the counts and maxima move in k_pix_apply_delta)
         const unsigned long long sel = pix_sel(t, s);
         const uint32_t blk = s / PIX_B;
         if (sel > t.bmax[blk]) {
@@ -1422,7 +1484,7 @@ __global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl
     // by pix_commit).  A new pair lifted above keeps its block's max either way: the recompute
     // reads its final count, so its store is >= the lift.  (No merge, no dirty block: k_pix_select
     // zeroes n_dblocks.)
-    pix_bmax_dirty(t, B, ctl, gridDim.x - 1 - blockIdx.x);
+    if (!t.delta) pix_bmax_dirty(t, B, ctl, gridDim.x - 1 - blockIdx.x);
 }
 
 // The corpus rewrite: c at every site, its right slot merged away, the links around it; the new
@@ -1432,7 +1494,10 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
                                                    long long *log) {
     if (ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE) return;   // (a tie scan: no merge)
     const unsigned long long W = ctl->W;
-    if (ctl->n_sites != W || (ctl->a == ctl->b && ctl->n_check != W)) {
+    // (sharded: this shard's sites; their sum over the shards is checked against W by
+    // k_pix_apply_delta)
+    const unsigned long long nw = t.delta ? ctl->n_sites : W;
+    if (ctl->n_sites != nw || (ctl->a == ctl->b && ctl->n_check != nw)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             ctl->status = PIX_ERROR;
             ctl->err = 20;
@@ -1441,7 +1506,7 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
     }
     const int32_t c = ctl->c;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
-    for (uint32_t i = tid; i < (uint32_t)W; i += stride) {
+    for (uint32_t i = tid; i < (uint32_t)nw; i += stride) {
         const uint32_t p = B.sites[i];
         const uint32_t q = C.nxt[p];
         const uint32_t r = C.nxt[q];
@@ -1451,20 +1516,23 @@ __global__ void __launch_bounds__(256) k_pix_apply(PixCorpus C, PixTable t, PixB
         if (r != PIX_NONE) C.prv[r] = p;
     }
     // (a != b: two entries per site, some empty; a == b: packed)
-    const uint32_t ne = min(ctl->a != ctl->b ? 2 * (uint32_t)W : ctl->n_ent, B.ent_cap);
+    const uint32_t ne = min(ctl->a != ctl->b ? 2 * (uint32_t)nw : ctl->n_ent, B.ent_cap);
     for (uint32_t i = tid; i < ne; i += stride) {
         const uint2 e = B.ent[i];
         if (e.x == PIX_NONE) continue;
-        const uint32_t k = atomicAdd(&t.fill[e.x], 1u);
-        B.pool[t.off[e.x] + k] = e.y & ~PIX_OWNER;
+        const uint32_t sl = e.x & ~PIX_OWNER;
+        const uint32_t k = atomicAdd(&t.fill[sl], 1u);
+        B.pool[t.off[sl] + k] = e.y;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const long long k = ctl->n_done;
-        log[3 * k] = ctl->a;
-        log[3 * k + 1] = ctl->b;
-        log[3 * k + 2] = (long long)W;
+        log[PIX_LOG * k] = ctl->a;
+        log[PIX_LOG * k + 1] = ctl->b;
+        log[PIX_LOG * k + 2] = (long long)W;
+        log[PIX_LOG * k + 3] = (long long)nw;   // (this shard's replacements)
         ctl->n_done = k + 1;
         ctl->next_id = c + 1;
+        ctl->merged = t.delta ? 1u : 0u;
     }
 }
 
@@ -1509,6 +1577,196 @@ __global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restr
             o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
             __syncthreads();
         }
+    }
+}
+
+// ---- a shard of a sharded corpus: the index inside the rank loop (include/bpe.h bpe_rank_loop_*) --
+// Every shard indexes its own samples (pairs never cross samples, core.ts:265-267) and holds the
+// GLOBAL count of every pair in its table, so every shard selects the same merge.  Per iteration,
+// on each shard's stream, between the caller's two all-reduces:
+//   [all-reduce(SUM) of the exchange: the last merge's delta rows]
+//   rank_loop_select   k_pix_apply_delta (the summed rows into the counts, the replacement check),
+//                      k_pix_dirty, k_pix_select, k_pix_sites (this shard's sites and count changes
+//                      into its delta rows; or the tie scan), k_pix_export (tie words and vote)
+//   [all-reduce(MAX) of the tie words]
+//   rank_loop_decide   k_pix_decide (a vote hands the iteration to the host on every shard alike; a
+//                      tie goes to the earliest (shard << 40 | last counted occurrence))
+//   rank_loop_count    k_pix_alloc, k_pix_apply (this shard's corpus and lists)
+constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
+
+// the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on
+__global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight) {
+    if (ctl->status == PIX_PAUSE) ctl->status = PIX_RUN;
+    ctl->n_done = 0;
+    ctl->n_want = n;
+    ctl->next_id = next_id;
+    ctl->min_weight = min_weight;
+}
+
+// The summed delta rows of the last merge (a, b) -> c into this shard's global counts: a fall marks
+// the block when the entry was its max, a rise (only pairs with c rise) lifts the block and
+// superblock maxima; a pair new to this shard gets a slot (no list here).  The rows read are zeroed
+// for this iteration's own changes; the header's first word, the shards' replacements summed, must
+// equal W.
+__global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, PixCtl *ctl,
+                                                         unsigned long long *__restrict__ xchg) {
+    __shared__ uint32_t s_go;
+    if (threadIdx.x == 0) s_go = ctl->status == PIX_RUN && ctl->merged;
+    __syncthreads();
+    if (!s_go) return;
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long got = xchg[0];
+        if (got != ctl->W) {
+            ctl->status = PIX_ERROR;
+            ctl->err = 21;
+            ctl->n_check = got;
+        }
+    }
+    unsigned long long *d = xchg + XCHG_HDR;
+    const uint32_t n = (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);   // other tokens <= c
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned long long v = d[i];
+        if (!v) continue;
+        d[i] = 0;
+        const uint32_t row = i % DELTA_ROWS;
+        const int32_t o = (int32_t)(i / DELTA_ROWS);
+        const int32_t m = row == 0 || row == 2 ? a : row == 1 || row == 3 ? b : c;
+        const bool left = row == 0 || row == 1 || row == 4;   // (m, o), else (o, m)
+        const uint32_t key = pix_key(left ? m : o, left ? o : m);
+        const bool rise = (long long)v > 0;
+        const uint32_t s = pix_slot(t, ctl, key, rise, true);
+        if (s == PIX_NONE) {   // (a fall of a pair no shard holds: the tables disagree)
+            if (rise) pix_fail(ctl, 1);
+            else if (atomicCAS(&ctl->status, PIX_RUN, PIX_ERROR) == PIX_RUN) ctl->err = 22;
+            continue;
+        }
+        const unsigned long long bm = t.bmax[s / PIX_B];
+        const unsigned long long old = atomicAdd(&t.cnt[s], v);
+        if (rise) {
+            const unsigned long long sel = pix_sel_of(t, key, old + v);
+            const uint32_t blk = s / PIX_B;
+            if (sel > bm) {
+                atomicMax(&t.bmax[blk], sel);
+                atomicMax(&t.sbmax[blk / PIX_SB], sel);
+            }
+        } else {
+            const unsigned long long sel = pix_sel_of(t, key, old);
+            if (sel && sel >= bm) pix_mark(t, B, ctl, s);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) xchg[0] = 0;
+}
+
+// The blocks whose max entry fell (marked by k_pix_sites and k_pix_apply_delta)
+__global__ void __launch_bounds__(256) k_pix_dirty(PixTable t, PixBufs B, PixCtl *ctl) {
+    pix_bmax_dirty(t, B, ctl, blockIdx.x);
+}
+
+// This iteration's exchange words: this shard's sites of the merge (the header's first word; the
+// rows hold its count changes), the tie scan's last counted occurrences as (shard << 40 | position)
+// and the hand-off vote.  Every tie word is written, each iteration.
+__global__ void k_pix_export(PixCtl *ctl, unsigned long long *__restrict__ xchg,
+                             unsigned long long *__restrict__ tie, int rank) {
+    const int i = threadIdx.x;
+    if (i == 0 && ctl->status == PIX_RUN && ctl->tie == PIX_TIE_NONE) {
+        // the pool must take this merge's new entries (k_pix_alloc): a shard that cannot votes
+        // now, before any shard applies the merge
+        const unsigned long long ne = ctl->a != ctl->b ? 2ull * ctl->n_sites : ctl->n_ent;
+        if (ctl->pool_top + ne > ctl->pool_cap) {
+            ctl->status = PIX_HOST;
+            ctl->err = 16;
+        }
+    }
+    __syncthreads();
+    const int st = ctl->status;
+    if (i < MAX_CAND) {
+        const unsigned long long m = ctl->tie == PIX_TIE_WAIT && i < (int)ctl->n_cand ? ctl->last[i] : 0;
+        tie[i] = m ? ((unsigned long long)rank << 40) | m : 0ull;
+    } else if (i == PIX_VOTE) {
+        tie[i] = st == PIX_HOST ? 1ull : 0ull;
+    } else if (i < 32) {
+        tie[i] = 0;
+    }
+    if (i == 0) xchg[0] = st == PIX_RUN && ctl->tie == PIX_TIE_NONE ? ctl->n_sites : 0u;
+}
+
+// After the all-reduce(MAX) of the tie words, alike on every shard: a vote hands the iteration to
+// the host (the corpus is still the last merge's: k_pix_apply has not run), a tie scan's winner is
+// the candidate whose last counted occurrence is earliest (R3, core.ts:294-305), committed by the
+// next k_pix_select.
+__global__ void k_pix_decide(PixCtl *ctl, const unsigned long long *__restrict__ tie) {
+    if (ctl->status == PIX_ERROR || ctl->status == PIX_DONE || ctl->status == PIX_PAUSE) return;
+    if (tie[PIX_VOTE]) {
+        if (ctl->status == PIX_RUN) {
+            ctl->status = PIX_HOST;
+            ctl->err = 30;
+        }
+        return;
+    }
+    if (ctl->status != PIX_RUN || ctl->tie != PIX_TIE_WAIT) return;
+    unsigned long long bp = ~0ull;
+    uint32_t bj = 0;
+    for (uint32_t q = 0; q < min(ctl->n_cand, (uint32_t)MAX_CAND); ++q)
+        if (tie[q] && tie[q] < bp) {
+            bp = tie[q];
+            bj = q;
+        }
+    if (bp == ~0ull) {
+        ctl->status = PIX_ERROR;
+        ctl->err = 8;
+        return;
+    }
+    ctl->pair_slot = ctl->cand_slot[bj];
+    ctl->tie = PIX_TIE_DECIDED;
+}
+
+// The global counts into a freshly built index (bpe_set_global_counts): the hot bins of the summed
+// table and every shard's cold (key, count) entries (duplicates summed), over counts zeroed first;
+// a pair no list of this shard holds gets a slot.
+__global__ void __launch_bounds__(256) k_pix_load_global(PixTable t, PixCtl *ctl,
+                                                         const unsigned long long *__restrict__ hot,
+                                                         const uint32_t *__restrict__ keys,
+                                                         const unsigned long long *__restrict__ counts,
+                                                         int64_t n) {
+    const int64_t total = (int64_t)HOT_BINS + n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t key;
+        unsigned long long v;
+        if (i < HOT_BINS) {
+            v = hot[i];
+            const uint32_t x = (uint32_t)i & 255u, y = (uint32_t)i >> 8;   // (hot_bin: y << 8 | x)
+            key = pix_key((int32_t)x, (int32_t)y);
+        } else {
+            key = keys[i - HOT_BINS];
+            v = counts[i - HOT_BINS];
+        }
+        if (!v || key == PIX_NONE) continue;
+        const uint32_t s = pix_slot(t, ctl, key, true, true);
+        if (s == PIX_NONE) {
+            atomicOr(&ctl->err, 9);
+            continue;
+        }
+        atomicAdd(&t.cnt[s], v);
+    }
+}
+
+// Growth in place, between batches (pix_reserve): every claimed pair into a table twice as large,
+// with its count and its list; the block maxima are then recomputed in full.
+__global__ void __launch_bounds__(256) k_pix_rehash(PixTable o, PixTable t, PixCtl *ctl, uint32_t ocap) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ocap; s += gridDim.x * blockDim.x) {
+        const uint32_t key = o.keys[s];
+        if (key == PIX_NONE) continue;
+        const uint32_t ns = pix_slot(t, ctl, key, true, false);
+        if (ns == PIX_NONE) {
+            atomicOr(&ctl->err, 9);
+            continue;
+        }
+        t.cnt[ns] = o.cnt[s];
+        t.off[ns] = o.off[s];
+        t.len[ns] = o.len[s];
+        t.fill[ns] = o.fill[s];
     }
 }
 

@@ -190,6 +190,15 @@ class ShardedTrainer:
         # host iterations in a row that needed exact cold counts (two: enter that state)
         self._maintained = False
         self._heavy_streak = 0
+        # the incremental mode: the global state lives in every rank's position index (entered at
+        # once, the tables' counts exchanged as signed delta rows: bpe_pix.hip.h)
+        self.pix = False
+
+    def set_mode(self, mode):
+        """'stream' or 'incremental' (bpe_set_mode) for this rank's engine; every rank alike."""
+        self.engine.set_mode(mode)
+        self.pix = mode == 'incremental'
+        self._maintained = False
 
     @classmethod
     def synthetic(cls, device, rank, world, bytes_per_rank, sample_bytes, seed, alphabet, base,
@@ -336,7 +345,7 @@ class ShardedTrainer:
         batch = LOOP_BATCH      # (as bpe_merge_until: about twice what an early-ended batch did)
         while len(ms) < n:
             k = min(batch, n - len(ms))
-            if not self._maintained and self._heavy_streak >= 2:
+            if not self._maintained and (self._heavy_streak >= 2 or self.pix):
                 self.enter_maintained()
             batch_maintained = self._maintained
             with torch.cuda.stream(stream):

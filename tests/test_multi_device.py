@@ -2,6 +2,7 @@
 the drop-in's BPE_NUM_GPUS path.  On the one-GPU test box the shards share device 0 and exchange
 their tables through host copies (BPE_REDUCE_HOST); the RCCL exchange (one shard per device) runs
 only where several devices exist.  Every result must equal the oracle's on the whole corpus."""
+import os
 import random
 
 import numpy as np
@@ -14,6 +15,9 @@ from test_gpu_parity import check_sample_index, random_corpus
 
 pytestmark = pytest.mark.gpu
 
+# (RCCL's warnings, if a communicator fails to come up, land in the failing test's captured output)
+os.environ.setdefault('NCCL_DEBUG', 'WARN')
+
 
 def multi_engine(samples, len16, n_shards, mode_devices=None):
     e = pkg.Engine(devices=mode_devices or [0] * n_shards, reduce='host')
@@ -25,7 +29,9 @@ def multi_engine(samples, len16, n_shards, mode_devices=None):
 
 
 def run(e, opts, mode, n_tokens):
-    if mode == 'loop':
+    if mode == 'pix':
+        e.set_mode('incremental')
+    if mode in ('loop', 'pix'):
         return e.merge_until(opts.get('max_length') or 0, opts.get('min_weight') or 0,
                              opts.get('max_iterations') or 0)
     out = []
@@ -41,7 +47,7 @@ def run(e, opts, mode, n_tokens):
     return out
 
 
-@pytest.mark.parametrize('mode', ['host', 'loop'])
+@pytest.mark.parametrize('mode', ['host', 'loop', 'pix'])
 @pytest.mark.parametrize('seed', range(8))
 def test_sharded_context_vs_oracle(seed, mode):
     """Random corpora (runs, cold ids >= 256, ties, max_length / min_weight) over 2-4 shards:
@@ -65,9 +71,10 @@ def test_sharded_context_vs_oracle(seed, mode):
     e.close()
 
 
-def test_golden_cases_over_two_shards():
+@pytest.mark.parametrize('mode', ['loop', 'pix'])
+def test_golden_cases_over_two_shards(mode):
     """The reference-generated golden cases (tests/golden/small_cases.json) through a 2-shard
-    context: merges and final corpus."""
+    context, in the streaming and the incremental mode: merges and final corpus."""
     bad = []
     for case in load_small()[::3]:
         c = Corpus()
@@ -75,7 +82,7 @@ def test_golden_cases_over_two_shards():
             c.add(s)
         e = multi_engine(c.samples, c.len16, 2)
         o = case['opts']
-        got = run(e, o, 'loop', len(c.chars))
+        got = run(e, o, mode, len(c.chars))
         if [list(m) for m in got] != case['merges'] or e.samples() != case['final_ids']:
             bad.append(case['name'])
         e.close()
@@ -247,8 +254,36 @@ def test_maintained_state_over_shards_on_zipf_words(shards, mib, n, max_length):
     multi.close()
 
 
+@pytest.mark.parametrize('shards,corpus,n,max_length', [(3, 'zipf', 900, 0), (4, 'uniform', 700, 0),
+                                                       (2, 'zipf', 500, 6)])
+def test_incremental_mode_over_shards(shards, corpus, n, max_length):
+    """The incremental mode over shards: every shard's position index holds its own lists and
+    the global counts, each merge's count changes exchanged as signed delta rows (the rank loop's
+    all-reduce), ties decided from every shard's last counted occurrences.  Same merges and corpus
+    as one context; every merge on the indexes."""
+    data = (pkg.synth_zipf(6 << 20, seed=12345) if corpus == 'zipf' else
+            pkg.synth_latin1(8 << 20, seed=4242, A=64, base=32))
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    want = one.merge_until(max_length, 2, n)
+    ids1, off1 = one.read_corpus()
+    one.close()
+    multi = pkg.Engine(devices=[0] * shards, reduce='host')
+    multi.add_latin1(data, sample_bytes=1 << 20)
+    multi.set_mode('incremental')
+    multi.stats_enable(True)
+    got = multi.merge_until(max_length, 2, n)
+    st = multi.stats()
+    assert got == want
+    ids, off = multi.read_corpus()
+    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    assert st['pix_merges'] >= shards * (n - 8 * (st['pix_host'] + 1)), st
+    multi.close()
+
+
 @pytest.mark.slow
-def test_eight_shards_to_the_32k_vocabulary():
+@pytest.mark.parametrize('mode', ['stream', 'pix'])
+def test_eight_shards_to_the_32k_vocabulary(mode):
     """8 shards of the C5 stream on one device (host-copy exchange, the same rank loop as RCCL
     over 8 GPUs) taken to the 32k-token vocabulary: past the sketch's reach the shards keep the
     global tables themselves (maintained state), so the iterations stay in the device loop
@@ -263,6 +298,8 @@ def test_eight_shards_to_the_32k_vocabulary():
     multi = pkg.Engine(devices=[0] * 8, reduce='host')
     multi.add_latin1(data, sample_bytes=1 << 20)
     del data
+    if mode == 'pix':
+        multi.set_mode('incremental')
     multi.stats_enable(True)
     got = multi.merge_until(0, 2, 32768 - nt)
     st = multi.stats()
@@ -271,5 +308,8 @@ def test_eight_shards_to_the_32k_vocabulary():
     ids, _ = multi.read_corpus()
     assert np.array_equal(ids, ids1)
     assert st['loop_host'] <= 24, st
-    assert st['fused_passes'] > 8 * 10000, st   # (summed over the 8 shards)
+    if mode == 'pix':   # (summed over the 8 shards)
+        assert st['pix_merges'] > 8 * 30000, st
+    else:
+        assert st['fused_passes'] > 8 * 10000, st
     multi.close()

@@ -136,3 +136,25 @@ def test_config5_shard_to_the_32k_vocabulary():
     cpu.close()
     assert e.find_next_merge(0, 2) == nxt
     e.close()
+
+
+def test_config5_shard_to_the_32k_vocabulary_incremental():
+    """The same 2 GiB C5 shard (2^31 + 2048 slots: positions past 2^31) to the 32k-token vocabulary
+    in the incremental mode: every merge on the position index, the same merges and corpus as the
+    streaming mode."""
+    n = 2 << 30
+    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
+    e, cmap, nt = engine(data)
+    e2, _, _ = engine(data)
+    del data
+    want = e.merge_until(0, 2, 32768 - nt)
+    ids1, off1 = e.read_corpus()
+    e.close()
+    e2.set_mode('incremental')
+    got = e2.merge_until(0, 2, 32768 - nt)
+    st = e2.stats()
+    assert got == want
+    assert st['pix_merges'] >= len(want) - 64 * (st['pix_host'] + 1), st
+    ids, off = e2.read_corpus()
+    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    e2.close()

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
-           mib=3, corpus='uniform', backend='gloo'):
+           mib=3, corpus='uniform', backend='gloo', engine_mode='stream'):
     import importlib
     import sys
     import torch
@@ -32,6 +32,8 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
                                               seed=seed, alphabet=A, base=base, dist=dist,
                                               corpus=corpus, rank_loop=True)
         assert tr.exchange and dist.get_backend() == backend
+        if engine_mode != 'stream':
+            tr.set_mode(engine_mode)
         tr.engine.stats_enable(True)
         if mode == 'step':
             for _ in range(n):
@@ -64,6 +66,7 @@ def run_ranks(world, **kw):
 
 
 def single_engine(world, n=60, max_length=0, seed=777, A=40, base=60, mib=3, corpus='uniform', **_):
+    # (the reference result: one context, the streaming mode)
     from bpe_amd import pkg
     if corpus == 'zipf':
         data = pkg.synth_zipf((mib * world) << 20, seed=seed, sample_bytes=1 << 20)
@@ -141,3 +144,26 @@ def test_rccl_host_protocol_one_rank():
     """The host protocol (exchange_and_select: table all-reduce, heavy-bucket all-gathers, tie
     all-reduce) over a 1-rank RCCL group, iteration by iteration."""
     check(1, mode='step', n=120, seed=4242, A=12, base=97, mib=2, backend='nccl')
+
+
+# ---- the incremental mode over ranks: every rank's position index holds its own lists and the
+# global counts; each merge's count changes cross as signed delta rows in the rank loop's
+# all-reduce(SUM), R3 ties as the ranks' last counted occurrences in the all-reduce(MAX) ---------
+
+def test_incremental_rank_loop_two_ranks():
+    st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=4, engine_mode='incremental')
+    assert all(s['pix_merges'] >= 250 for s in st), st
+
+
+def test_incremental_rank_loop_three_ranks_zipf_max_length():
+    st = check(3, mode='loop', n=400, corpus='zipf', mib=2, seed=99, max_length=6,
+               engine_mode='incremental')
+    assert all(s['pix_merges'] >= 300 for s in st), st
+
+
+def test_rccl_incremental_rank_loop_one_rank():
+    """The incremental mode's rank loop over a 1-rank RCCL group (the delta rows and tie words
+    through RCCL on the engine's stream): the same merges and corpus as one context."""
+    st = check(1, mode='loop', n=500, corpus='zipf', mib=8, seed=12345, backend='nccl',
+               engine_mode='incremental')
+    assert st[0]['pix_merges'] >= 400, st

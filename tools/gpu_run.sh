@@ -30,9 +30,13 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
   tests)
+    # (a heartbeat under gpurun_out/ while a long test runs: pytest -v prints only at a test's end;
+    # each test still has its own 400 s limit)
+    ( while sleep 50; do date +%T >> "$OUT/heartbeat"; done ) & HB=$!
     timeout -k 10 1100 python3 -u -m pytest ${PYTEST_PATHS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -v \
-        --maxfail=5 --timeout 400 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
-        || fail tests "$OUT/pytest_gpu.log"
+        --maxfail=5 --timeout 400 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+    rc=$?; kill $HB 2>/dev/null
+    [ $rc -eq 0 ] || fail tests "$OUT/pytest_gpu.log"
     tail -3 "$OUT/pytest_gpu.log" ;;
   smoke)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Progress of a sharded run on one device (shards exchanging through the device kernel): the C5
+stream over S shards merged in chunks, printing per chunk the time, the index entries (builds),
+hand-offs and merges on the index, for the streaming or the incremental mode.
+Usage: python tools/multi_pix_probe.py MiB shards merges chunk [stream|incremental]"""
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    mib, shards, total, chunk = (int(x) for x in sys.argv[1:5])
+    mode = sys.argv[5] if len(sys.argv) > 5 else 'incremental'
+    pkg = importlib.import_module('bpe-tokenizer_amd')
+    data = pkg.synth_latin1(mib << 20, seed=12345, A=256, base=0)
+    e = pkg.Engine(devices=[0] * shards, reduce='host')
+    _, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
+    del data
+    e.set_mode(mode)
+    e.stats_enable(True)
+    done = 0
+    t_all = time.perf_counter()
+    while done < total:
+        k = min(chunk, total - done)
+        t0 = time.perf_counter()
+        got = e.merge_until(0, 2, k)
+        dt = time.perf_counter() - t0
+        done += len(got)
+        st = e.stats()
+        print(json.dumps({'merges': done, 'chunk_s': round(dt, 3), 'ms_per_merge': dt * 1e3 / max(1, len(got)),
+                          'last_w': got[-1][2] if got else None, 'pix_merges': st['pix_merges'],
+                          'pix_builds': st['pix_builds'], 'pix_host': st['pix_host'],
+                          'loop_host': st['loop_host']}), flush=True)
+        if len(got) < k:
+            break
+    print(json.dumps({'total_s': time.perf_counter() - t_all, 'merges': done, 'mode': mode,
+                      'shards': shards, 'corpus_mib': mib}), flush=True)
+
+
+if __name__ == '__main__':
+    main()
