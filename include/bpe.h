@@ -197,7 +197,12 @@ int bpe_tie_positions(bpe_ctx *ctx, const int32_t *cand, int64_t n, uint64_t *la
  *   - after bpe_set_global_counts (the maintained state: every rank holds the GLOBAL hot and cold
  *     tables and keeps them merge by merge), BPE_DELTA_ROWS delta rows per token id: this shard's
  *     recount of every pair the merge (a, b) -> c touched, at HDR + 6 * other + row, rows
- *     (a, .) (b, .) (., a) (., b) (c, .) (., c) in this order of precedence.
+ *     (a, .) (b, .) (., a) (., b) (c, .) (., c) in this order of precedence.  In the
+ *     incremental mode (bpe_set_mode) the global state lives in the shard's position index instead
+ *     (every pair's global count beside this shard's own lists) and the same rows carry each
+ *     merge's signed count CHANGES (two's complement u64; a sum of them is the global change).
+ *     A tie there takes one iteration of its own: the scan's positions cross in `tie`, and the
+ *     next iteration commits the winner, so a batch may merge fewer times than it iterates.
  * tie: the tied candidates' last positions (rank << 40 | position, rule R3: rank r's occurrences
  * come after rank r-1's) in words 0..15, and word 16 this rank's vote for the host path (facts of
  * its own copy of the maintained tables: fill, dead claims, room).  A tie between pairs X Y is
@@ -230,7 +235,9 @@ int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abwr, int64_t cap, int64_t *n_m
  * the lists of ALL ranks gathered (e.g. all-gather) and bpe_set_global_counts with the global table
  * (all-reduced bpe_export_counts) and the gathered lists (device pointers; duplicate keys summed).
  * The next rank loop batches keep those global tables up to date with delta rows (above); any
- * per-shard entry point (find/apply/export/...) drops the state. */
+ * per-shard entry point (find/apply/export/...) drops the state.  In the incremental mode
+ * bpe_set_global_counts builds the shard's position index and loads the global counts into it
+ * (enter at once: a driver need not wait for the cold pairs to outgrow the sketch). */
 int bpe_cold_counts(bpe_ctx *ctx, uint32_t *keys, uint64_t *counts, int64_t cap, int64_t *n);
 int bpe_set_global_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *keys,
                           const uint64_t *counts, int64_t n);
@@ -242,8 +249,10 @@ int bpe_set_global_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *k
  * merge only the W match sites and their neighbours are touched, O(W) instead of O(N).  Same
  * merges, counts and corpus; it changes what pair-scans/s measures, so it is reported apart.
  * Built per call by a hand-written counting scatter of the corpus's positions into per-pair lists
- * (one count pass, one exclusive scan, two fill passes; no sort); needs < 2^31 live slots.  Env
- * BPE_PIX=1 selects it for new contexts.  Single-device contexts only. */
+ * (one count pass, one exclusive scan, two fill passes; no sort); 32-bit positions, so up to
+ * 0xFFFF0000 live slots per context or shard.  Env BPE_PIX=1 selects it for new contexts.  On a
+ * multi-device context (bpe_create_multi) the mode applies to every shard: each shard indexes its
+ * own samples inside the rank loop (above). */
 #define BPE_MODE_STREAM 0
 #define BPE_MODE_INCREMENTAL 1
 int bpe_set_mode(bpe_ctx *ctx, int mode);

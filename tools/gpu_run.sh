@@ -33,6 +33,8 @@ for step in "$@"; do
     # (a heartbeat under gpurun_out/ while a long test runs: pytest -v prints only at a test's end;
     # each test still has its own 400 s limit)
     ( while sleep 50; do date +%T >> "$OUT/heartbeat"; done ) & HB=$!
+    # (RCCL's warnings to a file: a communicator that fails to come up leaves its reason there)
+    export NCCL_DEBUG=${NCCL_DEBUG:-WARN} NCCL_DEBUG_FILE=${NCCL_DEBUG_FILE:-$OUT/nccl.%p.log}
     timeout -k 10 1100 python3 -u -m pytest ${PYTEST_PATHS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -v \
         --maxfail=5 --timeout 400 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
     rc=$?; kill $HB 2>/dev/null
