@@ -36,6 +36,8 @@ C_API = [
     'bpe_heavy_counts', 'bpe_select_counts', 'bpe_tie_positions', 'bpe_rank_loop_begin',
     'bpe_rank_loop_select', 'bpe_rank_loop_decide', 'bpe_rank_loop_count', 'bpe_rank_loop_end',
     'bpe_cold_counts', 'bpe_set_global_counts',
+    'bpe_encoder_create', 'bpe_encoder_destroy', 'bpe_encoder_add_merges', 'bpe_encoder_clear',
+    'bpe_encoder_num_merges', 'bpe_encode_batch', 'bpe_encoder_get_stats', 'bpe_encoder_reset_stats',
 ]
 HOT_BINS = 65536
 TABLE_BINS = 81920
@@ -69,6 +71,17 @@ class Stats(ctypes.Structure):
         ('pix_build_ms', ctypes.c_double), ('cold_used', ctypes.c_int64),
         ('sel_blocks', ctypes.c_int64),
     ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class EncoderStats(ctypes.Structure):
+    """bpe_encoder_stats (include/bpe.h)."""
+    _fields_ = [('kernel_ms', ctypes.c_double), ('calls', ctypes.c_int64),
+                ('texts_rank', ctypes.c_int64), ('texts_replay', ctypes.c_int64),
+                ('tokens_in', ctypes.c_int64), ('tokens_out', ctypes.c_int64),
+                ('steps', ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -141,6 +154,14 @@ def lib():
         'bpe_rank_loop_count': ([vp], ctypes.c_int),
         'bpe_rank_loop_end': ([vp, i64p, ctypes.c_int64, i64p, ctypes.POINTER(ctypes.c_int)],
                               ctypes.c_int),
+        'bpe_encoder_create': ([ctypes.POINTER(vp), ctypes.c_int], ctypes.c_int),
+        'bpe_encoder_destroy': ([vp], ctypes.c_int),
+        'bpe_encoder_add_merges': ([vp, i32p, ctypes.c_int64], ctypes.c_int),
+        'bpe_encoder_clear': ([vp], ctypes.c_int),
+        'bpe_encoder_num_merges': ([vp, i64p], ctypes.c_int),
+        'bpe_encode_batch': ([vp, i32p, i64p, ctypes.c_int64, i32p, i64p], ctypes.c_int),
+        'bpe_encoder_get_stats': ([vp, ctypes.POINTER(EncoderStats)], ctypes.c_int),
+        'bpe_encoder_reset_stats': ([vp], ctypes.c_int),
         'bpe_synth_zipf': ([ctypes.c_uint32, ctypes.c_double, ctypes.c_uint32, ctypes.c_uint64,
                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
         'bpe_synth_latin1': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
@@ -446,6 +467,78 @@ class Engine:
 
     def reset_stats(self):
         _check(lib().bpe_reset_stats(self._ctx), 'bpe_reset_stats')
+
+
+class Encoder:
+    """encodeToCode (core.ts:392-409) for batches of texts with a trained merge list, apart from
+    any corpus (bpe_encoder_*, include/bpe.h): the merge list lives on the device as a rank table;
+    texts up to 16384 tokens are encoded by the merge-rank kernel (csrc/bpe_encode.hip), longer
+    ones by apply-only replay passes.  No CPU fallback."""
+
+    def __init__(self, device=0, merges=None):
+        p = ctypes.c_void_p()
+        _check(lib().bpe_encoder_create(ctypes.byref(p), int(device)), 'bpe_encoder_create')
+        self._enc = p
+        if merges is not None and len(merges):
+            self.add_merges(merges)
+
+    def close(self):
+        if self._enc:
+            lib().bpe_encoder_destroy(self._enc)
+            self._enc = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_merges(self, merges):
+        """Appends (a, b, c) triples in list order (merge_codes, core.ts:91,352)."""
+        abc = _i32(np.asarray(merges, dtype=np.int32).reshape(-1))
+        _check(lib().bpe_encoder_add_merges(self._enc, abc.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                            len(abc) // 3), 'bpe_encoder_add_merges')
+
+    def clear(self):
+        _check(lib().bpe_encoder_clear(self._enc), 'bpe_encoder_clear')
+
+    def num_merges(self):
+        n = ctypes.c_int64()
+        _check(lib().bpe_encoder_num_merges(self._enc, ctypes.byref(n)), 'bpe_encoder_num_merges')
+        return n.value
+
+    def encode_flat(self, ids, off):
+        """Flat form: texts ids[off[k]:off[k+1]] -> (ids_out, out_off) numpy arrays."""
+        ids = _i32(ids)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        n = len(off) - 1
+        total = int(off[-1] - off[0]) if n > 0 else 0
+        out = np.zeros(max(total, 1), dtype=np.int32)
+        out_off = np.zeros(max(n + 1, 1), dtype=np.int64)
+        src = ids if ids.size else np.zeros(1, np.int32)
+        i32p, i64p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)
+        _check(lib().bpe_encode_batch(self._enc, src.ctypes.data_as(i32p), off.ctypes.data_as(i64p),
+                                      n, out.ctypes.data_as(i32p), out_off.ctypes.data_as(i64p)),
+               'bpe_encode_batch')
+        return out[:out_off[n] if n > 0 else 0], out_off
+
+    def encode(self, texts):
+        """texts: a list of id sequences -> list of encoded int32 arrays."""
+        lens = [len(t) for t in texts]
+        off = np.zeros(len(texts) + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        ids = np.concatenate([np.asarray(t, dtype=np.int32) for t in texts]) if texts and off[-1] \
+            else np.zeros(0, np.int32)
+        out, oo = self.encode_flat(ids, off)
+        return [out[oo[k]:oo[k + 1]].copy() for k in range(len(texts))]
+
+    def stats(self):
+        s = EncoderStats()
+        _check(lib().bpe_encoder_get_stats(self._enc, ctypes.byref(s)), 'bpe_encoder_get_stats')
+        return s.as_dict()
+
+    def reset_stats(self):
+        _check(lib().bpe_encoder_reset_stats(self._enc), 'bpe_encoder_reset_stats')
 
 
 def encode_samples(samples, merges, len16, device=0):

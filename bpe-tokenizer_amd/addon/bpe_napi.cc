@@ -364,76 +364,95 @@ napi_value MergeUntil(napi_env env, napi_callback_info info) {
     return out;
 }
 
-// The encoder's scratch engine: one per environment (the addon is context-aware: each
-// worker_threads environment that loads it gets its own instance data, so two workers never share
-// an engine), created on first use and destroyed with its environment (napi_set_instance_data's
-// finalizer).  Each environment's calls come from its one JS thread.
-struct AddonData {
-    bpe_ctx *scratch = nullptr;
-};
-
-void finalize_addon(napi_env, void *data, void *) {
-    AddonData *d = static_cast<AddonData *>(data);
-    if (d->scratch) bpe_destroy(d->scratch);
-    delete d;
+// An encoder handle (bpe_encoder_*: the merge list as a rank table on the device, encodeToCode
+// core.ts:392-409) behind a JS external, freed by its finalizer.  Each tokenizer holds its own, so
+// worker_threads environments never share one.
+void finalize_encoder(napi_env, void *data, void *) {
+    if (data) bpe_encoder_destroy(static_cast<bpe_encoder *>(data));
 }
 
-bpe_ctx *scratch_engine(napi_env env) {
+bpe_encoder *get_encoder(napi_env env, napi_value v) {
     void *p = nullptr;
-    if (napi_get_instance_data(env, &p) != napi_ok || !p) return nullptr;
-    AddonData *d = static_cast<AddonData *>(p);
-    if (!d->scratch && bpe_create(&d->scratch, 0) != BPE_OK) {
-        d->scratch = nullptr;
-        return nullptr;
-    }
-    return d->scratch;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return nullptr;
+    return static_cast<bpe_encoder *>(p);
 }
 
-// encodeMerges(Int32Array ids, Int32Array abc) -> Int32Array: one text through a run of merges
-// (a, b, c) on the scratch engine (bpe_apply_merges: encodeToCode's replay, core.ts:392-409)
-napi_value EncodeMerges(napi_env env, napi_callback_info info) {
+// createEncoder([device]) -> external handle
+napi_value CreateEncoder(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    size_t argc = 1;
+    napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+    const int device = argc >= 1 ? (int)get_i64(env, argv[0]) : 0;
+    bpe_encoder *enc = nullptr;
+    if (bpe_encoder_create(&enc, device) != BPE_OK) return throw_native(env, "bpe_encoder_create");
+    napi_value ext;
+    napi_create_external(env, enc, finalize_encoder, nullptr, &ext);
+    return ext;
+}
+
+// encoderAddMerges(enc, Int32Array abc): appends (a, b, c) triples in merge_codes order
+napi_value EncoderAddMerges(napi_env env, napi_callback_info info) {
     napi_value argv[2];
-    if (!get_args(env, info, 2, argv)) return throw_arg(env, "encodeMerges(Int32Array, Int32Array)");
+    if (!get_args(env, info, 2, argv)) return throw_arg(env, "encoderAddMerges(enc, Int32Array)");
+    napi_typedarray_type t;
+    size_t n = 0, o = 0;
+    void *abc = nullptr;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[1], &t, &n, &abc, &ab, &o) != napi_ok ||
+        t != napi_int32_array || n % 3 != 0)
+        return throw_arg(env, "encoderAddMerges expects (a, b, c) triples in an Int32Array");
+    if (bpe_encoder_add_merges(get_encoder(env, argv[0]), static_cast<const int32_t *>(abc),
+                               (int64_t)(n / 3)) < 0)
+        return throw_native(env, "bpe_encoder_add_merges");
+    return nullptr;
+}
+
+// encoderClear(enc)
+napi_value EncoderClear(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_arg(env, "encoderClear(enc)");
+    if (bpe_encoder_clear(get_encoder(env, argv[0])) < 0) return throw_native(env, "bpe_encoder_clear");
+    return nullptr;
+}
+
+// encodeBatch(enc, Int32Array ids, Float64Array offsets) -> [Int32Array ids, Float64Array offsets]
+// (bpe_encode_batch: text k = ids[offsets[k] .. offsets[k+1]))
+napi_value EncodeBatch(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return throw_arg(env, "encodeBatch(enc, Int32Array, Float64Array)");
     napi_typedarray_type t1, t2;
     size_t n1 = 0, n2 = 0, o1 = 0, o2 = 0;
-    void *ids = nullptr, *abc = nullptr;
+    void *ids = nullptr, *offd = nullptr;
     napi_value ab1, ab2;
-    if (napi_get_typedarray_info(env, argv[0], &t1, &n1, &ids, &ab1, &o1) != napi_ok ||
+    if (napi_get_typedarray_info(env, argv[1], &t1, &n1, &ids, &ab1, &o1) != napi_ok ||
         t1 != napi_int32_array ||
-        napi_get_typedarray_info(env, argv[1], &t2, &n2, &abc, &ab2, &o2) != napi_ok ||
-        t2 != napi_int32_array || n2 % 3 != 0)
-        return throw_arg(env, "encodeMerges expects Int32Array ids and (a, b, c) triples");
-    const int32_t *m = static_cast<const int32_t *>(abc);
-    int32_t vocab = 0;
-    for (size_t i = 0; i < n1; ++i) vocab = std::max(vocab, static_cast<const int32_t *>(ids)[i] + 1);
-    for (size_t i = 0; i < n2; ++i) vocab = std::max(vocab, m[i] + 1);
-    // one scratch engine per addon instance, emptied between calls (its stream, tables and
-    // pinned buffers are set up once, and token lengths registered once per id)
-    bpe_ctx *ctx = scratch_engine(env);
-    if (!ctx) return throw_native(env, "bpe_create");
-    struct Guard {
-        bpe_ctx *c;
-        ~Guard() { bpe_clear_corpus(c); }
-    } guard{ctx};
-    if (bpe_clear_corpus(ctx) < 0) return throw_native(env, "bpe_clear_corpus");
-    // lengths only matter to the max_length filter of a find, which never runs here
-    int32_t known = 0;
-    if (bpe_num_tokens(ctx, &known) < 0) return throw_native(env, "bpe_num_tokens");
-    for (int32_t i = known; i < vocab; ++i)
-        if (bpe_set_token_len16(ctx, i, 1) < 0) return throw_native(env, "bpe_set_token_len16");
-    if (bpe_add_sample(ctx, static_cast<const int32_t *>(ids), (int64_t)n1) < 0 ||
-        bpe_apply_merges(ctx, m, (int64_t)(n2 / 3), nullptr, 0) < 0)
-        return throw_native(env, "bpe_apply_merges");
-    int64_t ns = 0, nt = 0;
-    if (bpe_corpus_size(ctx, &ns, &nt) < 0) return throw_native(env, "bpe_corpus_size");
-    void *out_data = nullptr;
-    napi_value out_ab, out;
-    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(nt, 1) * 4, &out_data, &out_ab);
-    int64_t off[2];
-    if (bpe_read_corpus(ctx, static_cast<int32_t *>(out_data), std::max<int64_t>(nt, 1), off, 2) < 0)
-        return throw_native(env, "bpe_read_corpus");
-    napi_create_typedarray(env, napi_int32_array, (size_t)nt, out_ab, 0, &out);
-    return out;
+        napi_get_typedarray_info(env, argv[2], &t2, &n2, &offd, &ab2, &o2) != napi_ok ||
+        t2 != napi_float64_array || n2 < 1)
+        return throw_arg(env, "encodeBatch expects Int32Array ids and Float64Array offsets");
+    const int64_t n_texts = (int64_t)n2 - 1;
+    std::vector<int64_t> off(n2);
+    const double *od = static_cast<const double *>(offd);
+    for (size_t k = 0; k < n2; ++k) {
+        off[k] = (int64_t)od[k];
+        if (off[k] < 0 || (size_t)off[k] > n1) return throw_arg(env, "encodeBatch: offset out of range");
+    }
+    const int64_t total = off[n_texts] - off[0];
+    void *out_data = nullptr, *oo_data = nullptr;
+    napi_value out_ab, oo_ab, out, oo, pair;
+    napi_create_arraybuffer(env, (size_t)std::max<int64_t>(total, 1) * 4, &out_data, &out_ab);
+    std::vector<int64_t> out_off(n2);
+    if (bpe_encode_batch(get_encoder(env, argv[0]), static_cast<const int32_t *>(ids), off.data(),
+                         n_texts, static_cast<int32_t *>(out_data), out_off.data()) < 0)
+        return throw_native(env, "bpe_encode_batch");
+    napi_create_typedarray(env, napi_int32_array, (size_t)out_off[n_texts], out_ab, 0, &out);
+    napi_create_arraybuffer(env, n2 * 8, &oo_data, &oo_ab);
+    double *ood = static_cast<double *>(oo_data);
+    for (size_t k = 0; k < n2; ++k) ood[k] = (double)out_off[k];
+    napi_create_typedarray(env, napi_float64_array, n2, oo_ab, 0, &oo);
+    napi_create_array_with_length(env, 2, &pair);
+    napi_set_element(env, pair, 0, out);
+    napi_set_element(env, pair, 1, oo);
+    return pair;
 }
 
 napi_value Init(napi_env env, napi_value exports) {
@@ -448,19 +467,14 @@ napi_value Init(napi_env env, napi_value exports) {
         {"corpusSize", CorpusSize}, {"readCorpus", ReadCorpus},
         {"findNextMerge", FindNextMerge}, {"applyMerge", ApplyMerge},
         {"applyMerges", ApplyMerges}, {"mergeUntil", MergeUntil},
-        {"encodeMerges", EncodeMerges}, {"sampleLengths", SampleLengths},
-        {"readSamples", ReadSamples},
+        {"sampleLengths", SampleLengths}, {"readSamples", ReadSamples},
+        {"createEncoder", CreateEncoder}, {"encoderAddMerges", EncoderAddMerges},
+        {"encoderClear", EncoderClear}, {"encodeBatch", EncodeBatch},
     };
     for (auto &f : fns) {
         napi_value fn;
         napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn);
         napi_set_named_property(env, exports, f.name, fn);
-    }
-    AddonData *d = new AddonData();
-    if (napi_set_instance_data(env, d, finalize_addon, nullptr) != napi_ok) {
-        delete d;
-        napi_throw_error(env, nullptr, "bpe native: napi_set_instance_data failed");
-        return nullptr;
     }
     return exports;
 }

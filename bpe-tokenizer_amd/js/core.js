@@ -20,8 +20,9 @@ const {
   loadNative,
   maxLengthArg,
   minWeightArg,
-  ENCODE_ON_DEVICE_CHARS,
-  ENCODE_ON_DEVICE_MERGES,
+  encodeOnDevice,
+  encodeIdsOnDevice,
+  idsToCode,
 } = require('./native')
 
 /** @description file separator (core.ts:36) */
@@ -59,6 +60,11 @@ function linesTrimmedToCorpus(text) {
 /** `String.prototype.replaceAll(p, r)` for the single-code-point replacements used here. */
 function replaceAll(s, from, to) {
   return s.split(from).join(to)
+}
+
+/** a merge_tokens entry [a, b, c] -> its token indices (the encoder's (a, b, c) triple) */
+function tokenTriple(merge) {
+  return [merge[0].index, merge[1].index, merge[2].index]
 }
 
 class BPETokenizer {
@@ -386,42 +392,28 @@ class BPETokenizer {
 
   /**
    * @description encode to binary string (core.ts:392-409).
-   * A long text with many merges is encoded on the GPU: the merges are replayed in order by
-   * apply-only passes over the text in HBM (bpe_apply_merges), one per merge, in place of one
-   * `replaceAll` per merge over a JS string.
+   * With enough merges the text is encoded on the GPU by the merge-rank encoder (bpe_encode_batch:
+   * the lowest-ranked merge present is rewritten until none is, which equals the reference's
+   * in-order replaceAll of every merge; texts over 16384 tokens are replayed by apply-only passes
+   * over HBM).  Short merge lists keep the reference's replay here (see native.js).
    */
   encodeToCode(content) {
     let { char_to_token } = this
 
     let content_in_code = ''
-    let ids = null
-    let long = content.length >= ENCODE_ON_DEVICE_CHARS && this.merge_tokens.length >= ENCODE_ON_DEVICE_MERGES
-    if (long) ids = []
+    let ids = []
     for (let char of content) {
       let token = char_to_token[char]
       if (!token) {
         throw new Error('unknown token, char: ' + JSON.stringify(char))
       }
-      if (long) ids.push(token.index)
-      else content_in_code += token.code
+      ids.push(token.index)
+      content_in_code += token.code
     }
 
-    if (long) {
-      let abc = new Int32Array(3 * this.merge_tokens.length)
-      this.merge_tokens.forEach(([a, b, c], i) => {
-        abc[3 * i] = a.index
-        abc[3 * i + 1] = b.index
-        abc[3 * i + 2] = c.index
-      })
-      let out = loadNative().encodeMerges(Int32Array.from(ids), abc)
-      let parts = []
-      for (let i = 0; i < out.length; i += 8192) {
-        let part = []
-        let end = Math.min(out.length, i + 8192)
-        for (let j = i; j < end; j++) part.push(out[j] + 1)
-        parts.push(String.fromCodePoint.apply(null, part))
-      }
-      return parts.join('')
+    if (encodeOnDevice(ids.length, this.merge_tokens.length)) {
+      let out = encodeIdsOnDevice(this, this.merge_tokens, tokenTriple, ids)
+      return idsToCode(out, 0, out.length)
     }
 
     for (let [from_code, to_code] of this.merge_codes) {

@@ -32,8 +32,9 @@ const {
   loadNative,
   maxLengthArg,
   minWeightArg,
-  ENCODE_ON_DEVICE_CHARS,
-  ENCODE_ON_DEVICE_MERGES,
+  encodeOnDevice,
+  encodeIdsOnDevice,
+  idsToCode,
 } = require('./native')
 const { EOF } = require('./core')
 
@@ -194,16 +195,10 @@ function codeToIds(code) {
   return Int32Array.from(ids)
 }
 
-/** engine ids -> code point string */
-function idsToCode(ids, begin, end) {
-  let parts = []
-  for (let i = begin; i < end; i += 8192) {
-    let part = []
-    let stop = Math.min(end, i + 8192)
-    for (let j = i; j < stop; j++) part.push(ids[j] + 1)
-    parts.push(String.fromCodePoint.apply(null, part))
-  }
-  return parts.join('')
+/** a merge_codes entry [from_code, to_code] -> its (a, b, c) token indices (id - 1) */
+function codeTriple(merge) {
+  let pair = Array.from(merge[0])
+  return [pair[0].codePointAt(0) - 1, pair[1].codePointAt(0) - 1, merge[1].codePointAt(0) - 1]
 }
 
 class BPETokenizerDB {
@@ -597,8 +592,8 @@ class BPETokenizerDB {
   }
 
   /**
-   * @description encode to binary string (db/core.ts:450-467); long texts with many merges are
-   * encoded on the GPU as in core.js.
+   * @description encode to binary string (db/core.ts:450-467); with enough merges on the GPU's
+   * merge-rank encoder, as in core.js.
    */
   encodeToCode(content) {
     let { char_to_token } = this
@@ -612,15 +607,8 @@ class BPETokenizerDB {
       ids.push(token.id - 1)
       content_in_code += token.code
     }
-    if (content.length >= ENCODE_ON_DEVICE_CHARS && this.merge_codes.length >= ENCODE_ON_DEVICE_MERGES) {
-      let abc = new Int32Array(3 * this.merge_codes.length)
-      this.merge_codes.forEach(([from_code, to_code], i) => {
-        let pair = Array.from(from_code)
-        abc[3 * i] = pair[0].codePointAt(0) - 1
-        abc[3 * i + 1] = pair[1].codePointAt(0) - 1
-        abc[3 * i + 2] = to_code.codePointAt(0) - 1
-      })
-      let out = loadNative().encodeMerges(Int32Array.from(ids), abc)
+    if (encodeOnDevice(ids.length, this.merge_codes.length)) {
+      let out = encodeIdsOnDevice(this, this.merge_codes, codeTriple, ids)
       return idsToCode(out, 0, out.length)
     }
     for (let [from_code, to_code] of this.merge_codes) {

@@ -279,7 +279,8 @@ typedef struct {
                                  buckets, > BPE_MAX_CAND tied pairs, >= 2 tied pairs missing from
                                  the tail window, the vocabulary limit) */
     int64_t fused_passes;     /* merge passes that also refreshed the maintained cold-pair table */
-    int64_t pix_builds;       /* incremental mode: position-index builds (one sort of the corpus) */
+    int64_t pix_builds;       /* incremental mode: position-index builds (one counting scatter of
+                                 the corpus's positions) */
     int64_t pix_merges;       /* incremental mode: merges made on the index (O(W) each) */
     int64_t pix_host;         /* incremental mode: iterations the index handed to the stream */
     double pix_build_ms;      /* incremental mode: wall time of those builds (host clock, synced) */
@@ -295,6 +296,45 @@ int bpe_reset_stats(bpe_ctx *ctx);
 /* Raw device pointer of the context's HIP stream (hipStream_t), for callers that order their own
  * work (collectives, events) against the engine. */
 int bpe_get_stream(bpe_ctx *ctx, void **stream);
+
+/* ---- encoding ----------------------------------------------------------------------------------
+ * encodeToCode (core.ts:392-409) for a batch of texts with a trained merge list, apart from any
+ * corpus: `for (let [from_code, to_code] of this.merge_codes) content_in_code =
+ * content_in_code.replaceAll(from_code, to_code)` (core.ts:404-406) on every text.  An encoder
+ * holds the merge list as a rank table on one device.  A text of up to
+ * 16384 tokens is encoded by one workgroup in LDS: the lowest-ranked merge present is rewritten
+ * (all its leftmost non-overlapping occurrences) until none is, which equals the in-order replay
+ * whenever no merge's new token c is an input (a or b) of itself or an earlier merge — every list
+ * the reference makes (c is a fresh index, core.ts:315,484).  Longer texts, and lists that break
+ * that rule (checked as merges are added), are replayed merge by merge by apply-only streaming
+ * passes (bpe_apply_merges on a scratch engine of the encoder).  Output is identical either way. */
+typedef struct bpe_encoder bpe_encoder;
+typedef struct {
+    double kernel_ms;         /* HIP-event time of the merge-rank kernels (per call: launch to end) */
+    int64_t calls;            /* bpe_encode_batch calls */
+    int64_t texts_rank;       /* texts encoded by the merge-rank kernels */
+    int64_t texts_replay;     /* texts replayed by apply-only passes (long, or a non-greedy list) */
+    int64_t tokens_in;        /* ids in */
+    int64_t tokens_out;       /* ids out */
+    int64_t steps;            /* merge-rank kernels: greedy steps (ranks rewritten), all texts */
+} bpe_encoder_stats;
+
+/* An encoder with no merges on HIP device `device` (fails with BPE_ERR_HIP without one). */
+int bpe_encoder_create(bpe_encoder **out, int device);
+int bpe_encoder_destroy(bpe_encoder *enc);
+/* Appends n merges (a, b, c) in list order (`merge_codes`, core.ts:91,352; restoreMerge
+ * core.ts:477-494 and fromJSON core.ts:163-169 append the same way).  Ids < BPE_MAX_VOCAB. */
+int bpe_encoder_add_merges(bpe_encoder *enc, const int32_t *abc, int64_t n);
+/* Drops every merge (fromJSON of another tokenizer, core.ts:140-145). */
+int bpe_encoder_clear(bpe_encoder *enc);
+int bpe_encoder_num_merges(bpe_encoder *enc, int64_t *n);
+/* Encodes n_texts texts: text k = ids[off[k] .. off[k+1]) (token ids, `token.index`).  Writes the
+ * encoded texts back to back into ids_out (capacity off[n_texts] - off[0]: a text never grows) and
+ * n_texts + 1 offsets into out_off (out_off[0] = 0). */
+int bpe_encode_batch(bpe_encoder *enc, const int32_t *ids, const int64_t *off, int64_t n_texts,
+                     int32_t *ids_out, int64_t *out_off);
+int bpe_encoder_get_stats(bpe_encoder *enc, bpe_encoder_stats *out);
+int bpe_encoder_reset_stats(bpe_encoder *enc);
 
 #ifdef __cplusplus
 }

@@ -152,6 +152,18 @@ int64_t oracle_apply_merge(int32_t *ids, int64_t *off, int64_t n_samples, int32_
 }
 
 /* ---------------------------------------------------------------------------------------------
+ * encodeToCode's merge replay — core.ts:404-406:
+ *     for (let [from_code, to_code] of this.merge_codes)
+ *       content_in_code = content_in_code.replaceAll(from_code, to_code)
+ * every text (sample) through the n merges abc[3i..3i+2] = (a, b, c), in list order, each one a
+ * leftmost non-overlapping rewrite (oracle_apply_merge).  In place; off[] updated.
+ * ------------------------------------------------------------------------------------------- */
+void oracle_encode(int32_t *ids, int64_t *off, int64_t n_texts, const int32_t *abc, int64_t n) {
+    for (int64_t i = 0; i < n; i++)
+        oracle_apply_merge(ids, off, n_texts, abc[3 * i], abc[3 * i + 1], abc[3 * i + 2]);
+}
+
+/* ---------------------------------------------------------------------------------------------
  * mergeUntil — core.ts:365-383.  max_iterations 0 == falsy == unlimited (core.ts:376).
  * New token index = current token-table length (core.ts:315), UTF-16 length of its chars =
  * len16[a] + len16[b] (core.ts:318).  len16 must have room for n_tokens + merges entries.

@@ -46,6 +46,8 @@ def lib():
         L.oracle_xorshift_corpus.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_void_p, ctypes.c_int64]
         L.oracle_xorshift_corpus.restype = None
+        L.oracle_encode.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int64]
+        L.oracle_encode.restype = None
         _lib = L
     return _lib
 
@@ -164,6 +166,25 @@ class OracleState:
         if n < 0:
             raise RuntimeError('oracle_count_pairs failed %d' % n)
         return pa[:n], pb[:n], pc[:n], pl[:n]
+
+
+def encode(texts, merges):
+    """encodeToCode's replay (core.ts:404-406) of the (a, b, c) merges over each text, in list
+    order: the checker of the device encoder (bpe_encode_batch)."""
+    off = np.zeros(len(texts) + 1, dtype=np.int64)
+    np.cumsum([len(t) for t in texts], out=off[1:])
+    ids = np.zeros(max(int(off[-1]), 1), dtype=np.int32)
+    if off[-1]:
+        ids[:off[-1]] = np.concatenate([np.asarray(t, dtype=np.int32) for t in texts])
+    abc = np.ascontiguousarray(np.asarray(merges, dtype=np.int32).reshape(-1))
+    if abc.size == 0:
+        abc = np.zeros(3, np.int32)
+        n = 0
+    else:
+        n = abc.size // 3
+    lib().oracle_encode(_p(ids, ctypes.c_int32), _p(off, ctypes.c_int64), len(texts),
+                        _p(abc, ctypes.c_int32), n)
+    return [ids[off[k]:off[k + 1]].copy() for k in range(len(texts))]
 
 
 def xorshift_corpus(seed, A, base, n):

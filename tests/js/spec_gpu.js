@@ -195,6 +195,53 @@ it('long texts are encoded on the device (encodeToCode, core.ts:392-409)', () =>
   assert.throws(() => t.encodeToCode(text + '\u00e9'), e => e.message === 'unknown token, char: "\u00e9"')
 })
 
+// the device encoder (merge-rank kernel, bpe_encode_batch) against the reference's replay for
+// short and mid-length texts, a merge list grown by restoreMerge in between, and fromJSON
+it('device encoder = replaceAll replay (core.ts:392-409)', () => {
+  const t = new BPETokenizer()
+  let x = 99
+  const rnd = () => { x ^= x << 13; x ^= x >>> 17; x ^= x << 5; return (x >>> 0) / 4294967296 }
+  const word = () => { let w = ''; const l = 1 + Math.floor(rnd() * 6); for (let i = 0; i < l; i++) w += 'abcdefghij'[Math.floor(rnd() * 10)]; return w }
+  const text = n => { let s = ''; while (s.length < n) s += word() + ' '; return s.slice(0, n) }
+  for (let i = 0; i < 40; i++) t.addToCorpus(text(2000))
+  t.mergeUntil({ min_weight: 2, max_iterations: 600 })
+  assert(t.merge_tokens.length >= 300, 'merges ' + t.merge_tokens.length)
+  const replay = s => {
+    let want = ''
+    for (const ch of s) want += t.char_to_token[ch].code
+    for (const [from_code, to_code] of t.merge_codes) want = want.split(from_code).join(to_code)
+    return want
+  }
+  for (const n of [0, 1, 2, 3, 10, 100, 511, 513, 3000, 5000, 17000]) {
+    const s = text(n)
+    assert.strictEqual(t.encodeToCode(s), replay(s), 'len ' + n)
+  }
+  // restoreMerge-style growth (the encoder appends), then a fromJSON (the encoder rebuilds)
+  const json = t.toJSON()
+  const u = new BPETokenizer()
+  u.fromJSON(json)
+  for (const n of [50, 700, 4000]) {
+    const s = text(n)
+    assert.strictEqual(u.encodeToCode(s), replay(s))
+    assert.deepStrictEqual(u.encodeToVector(s), t.encodeToVector(s))
+  }
+  const v = new BPETokenizer()
+  v.fromJSON(Object.assign({}, json, { merge_codes: json.merge_codes.slice(0, 200) }))
+  const w = new BPETokenizer()
+  w.fromJSON(Object.assign({}, json, { merge_codes: json.merge_codes.slice(0, 200) }))
+  const s = text(900)
+  const before = v.encodeToCode(s)
+  for (const [a, b, c] of json.merge_codes.slice(200, 300)) {
+    const tok = u.code_to_token[c]
+    v.restoreMerge([a, b, tok.original_weight])
+  }
+  let want = ''
+  for (const ch of s) want += v.char_to_token[ch].code
+  for (const [from_code, to_code] of v.merge_codes) want = want.split(from_code).join(to_code)
+  assert.strictEqual(v.encodeToCode(s), want)
+  assert.strictEqual(w.encodeToCode(s), before)
+})
+
 // reference-generated golden cases through the whole JS surface
 const golden = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'small_cases.json')))
 let g = 0

@@ -31,14 +31,20 @@ def test_addon_builds_and_exports():
     out = subprocess.check_output([NODE, '-e', "const a=require(process.argv[1]);"
                                    "console.log(Object.keys(a).sort().join(','))",
                                    os.path.join(ADDON_DIR, 'bpe_napi.node')], text=True)
-    assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEngine,destroyEngine,'
-                           'deviceCount,encodeMerges,findNextMerge,mergeUntil,readCorpus,'
+    assert out.strip() == ('addLatin1,addSample,applyMerge,applyMerges,clearCorpus,corpusSize,createEncoder,'
+                           'createEngine,destroyEngine,deviceCount,encodeBatch,encoderAddMerges,'
+                           'encoderClear,findNextMerge,mergeUntil,readCorpus,'
                            'readSamples,sampleLengths,setTokenLen16')
+
+
+# (no device here: encodeToCode keeps the reference's JS replay for every merge-list length;
+# the GPU tests run the same golden vectors through the device encoder)
+HOST_ONLY = {'BPE_ENCODE_MIN_MERGES': '1e9'}
 
 
 def test_host_logic_against_golden():
     build_addon()
-    assert 'host_only ok' in run_node('host_only.js')
+    assert 'host_only ok' in run_node('host_only.js', env=HOST_ONLY)
 
 
 def test_db_twin_host_logic_over_sqlite():
@@ -46,7 +52,7 @@ def test_db_twin_host_logic_over_sqlite():
     tests/js/sqlite_bridge.js): schema, JSON round trips and golden encode/decode vectors, token
     rows and weights, the proxy views, error messages.  No device needed."""
     build_addon()
-    assert 'db_host_only ok' in run_node('db_host_only.js')
+    assert 'db_host_only ok' in run_node('db_host_only.js', env=HOST_ONLY)
 
 
 @pytest.mark.gpu

@@ -15,6 +15,9 @@
 #   sq         two SQ counter passes (300 C3 merges), summarised by tools/sq_loop_summary.py
 #   probe      tools/probe/bin/stream_probe3 (loads in flight x VALU work per chunk)
 #   rccl       the RCCL legs at world 1: tools/sharded_overhead.py (per-iteration cost)
+#   encode     the device encoder: tools/encode_bench.py (uniform and zipf merges, 100k short
+#              texts) and tools/encode_crossover.js (JS replay vs device per call)
+#   profenc    rocprofv3 --kernel-trace --stats of tools/encode_bench.py (zipf)
 # Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), BPE_LIB (A/B builds)
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -96,6 +99,20 @@ for step in "$@"; do
           || fail rccl "$OUT/rccl.err"
     done
     cat "$OUT/rccl_overhead.jsonl" ;;
+  encode)
+    for c in uniform zipf; do
+      timeout -k 10 300 python3 -u tools/encode_bench.py --corpus $c >> "$OUT/encode.jsonl" 2>> "$OUT/encode.err" \
+          || fail encode "$OUT/encode.err"
+    done
+    cat "$OUT/encode.jsonl"
+    timeout -k 10 300 node tools/encode_crossover.js > "$OUT/crossover.json" 2>> "$OUT/encode.err" \
+        || fail crossover "$OUT/encode.err"
+    cat "$OUT/crossover.json" ;;
+  profenc)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/enc" -o run --output-format csv \
+        -- python3 tools/encode_bench.py --corpus zipf > "$OUT/enc.jsonl" 2> "$OUT/enc.err" \
+        || fail profenc "$OUT/enc.err"
+    cat "$OUT/enc.jsonl"; prof_stats "$OUT/enc" ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
