@@ -51,6 +51,7 @@ XCHG_HDR = 8        # BPE_XCHG_HDR
 DELTA_ROWS = 6      # BPE_DELTA_ROWS
 XCHG_WORDS = XCHG_HDR + DELTA_ROWS * MAX_VOCAB   # BPE_XCHG_WORDS
 TIE_WORDS = 32      # BPE_TIE_WORDS
+ENCODE_LDS_TOKENS = 16384   # BPE_ENCODE_LDS_TOKENS: longer texts are replayed by apply passes
 
 
 class BpeError(RuntimeError):
@@ -472,7 +473,7 @@ class Engine:
 class Encoder:
     """encodeToCode (core.ts:392-409) for batches of texts with a trained merge list, apart from
     any corpus (bpe_encoder_*, include/bpe.h): the merge list lives on the device as a rank table;
-    texts up to 16384 tokens are encoded by the merge-rank kernel (csrc/bpe_encode.hip), longer
+    texts up to ENCODE_LDS_TOKENS tokens are encoded by the merge-rank kernel (csrc/bpe_encode.hip), longer
     ones by apply-only replay passes.  No CPU fallback."""
 
     def __init__(self, device=0, merges=None):

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,11 +42,13 @@
 
 namespace {
 
-constexpr uint32_t NO_RANK = 0xFFFFu;
-// tokens per workgroup buffer of each launch shape (LDS: 9 bytes per token)
-constexpr int CAP_64 = 512;       //   4.5 KiB, one wave
-constexpr int CAP_256 = 4096;     //  36 KiB
-constexpr int CAP_1024 = 16384;   // 144 KiB of the CU's 160 KiB
+// A pair's rank and the merge's new token in one word, rank << 16 | c: the minimum over a text is
+// the next merge together with its c (no dependent load of c), and NO_RANK is above every one.
+constexpr uint32_t NO_RANK = 0xFFFFFFFFu;
+// tokens per workgroup of each launch shape (LDS: 6 bytes per token, u16 id + u32 rank word)
+constexpr int CAP_MAX = 16384;   // 96 KiB (the largest launch shape below)
+static_assert(CAP_MAX == BPE_ENCODE_LDS_TOKENS, "include/bpe.h");
+constexpr size_t LDS_BYTES = 160 * 1024 - 256;   // per workgroup (the static words aside)
 
 #define ENC_TRY(expr)                                                                      \
     do {                                                                                   \
@@ -57,40 +60,42 @@ constexpr int CAP_1024 = 16384;   // 144 KiB of the CU's 160 KiB
     } while (0)
 
 struct RankTab {
-    const unsigned long long *slots;   // (a << 16 | b) << 32 | rank; empty = ~0
+    const unsigned long long *slots;   // (a << 16 | b) << 32 | rank << 16 | c; empty = ~0
     uint32_t mask;
     uint32_t shift;                    // 32 - log2(slots)
-    const uint16_t *c_of;              // rank -> new token id
 };
 
 __host__ __device__ __forceinline__ uint32_t rank_home(uint32_t key, uint32_t shift) {
     return (key * 0x9E3779B1u) >> shift;
 }
 
-__device__ __forceinline__ uint32_t rank_of(const RankTab &t, uint32_t x, uint32_t y) {
-    const uint32_t key = (x << 16) | y;
-    uint32_t h = rank_home(key, t.shift);
-    for (;;) {
-        const unsigned long long e = t.slots[h];
-        if ((uint32_t)(e >> 32) == key) return (uint32_t)e & 0xFFFFu;
-        if (e == ~0ull) return NO_RANK;
-        h = (h + 1) & t.mask;
-    }
+// Wave reductions on the VALU: DPP row rotations / shifts inside each 16-lane row, then the four
+// row results through v_readlane (no LDS crossbar round trips, unlike __shfl_*).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d));
-    return v;
+    v = min(v, dpp<0x128>(v, v));   // row_ror:8
+    v = min(v, dpp<0x124>(v, v));   // row_ror:4
+    v = min(v, dpp<0x122>(v, v));   // row_ror:2
+    v = min(v, dpp<0x121>(v, v));   // row_ror:1
+    const uint32_t a = __builtin_amdgcn_readlane((int)v, 0), b = __builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane((int)v, 32), d = __builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
 }
 
 __device__ __forceinline__ int wave_incl(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(v, d);
-        if (lane >= d) v += o;
-    }
-    return v;
+    uint32_t u = (uint32_t)v;
+    u += dpp<0x111>(u, 0);   // row_shr:1 (lanes without a source add 0)
+    u += dpp<0x112>(u, 0);   // row_shr:2
+    u += dpp<0x114>(u, 0);   // row_shr:4
+    u += dpp<0x118>(u, 0);   // row_shr:8
+    const int r = lane >> 4;
+    const int t0 = __builtin_amdgcn_readlane((int)u, 15), t1 = __builtin_amdgcn_readlane((int)u, 31);
+    const int t2 = __builtin_amdgcn_readlane((int)u, 47);
+    return (int)u + (r >= 1 ? t0 : 0) + (r >= 2 ? t1 : 0) + (r >= 3 ? t2 : 0);
 }
 
 // minimum over the workgroup (one barrier; `m` holds one word per wave)
@@ -113,7 +118,7 @@ __device__ __forceinline__ int block_scan(int v, int *s, int &total) {
     const int lane = threadIdx.x & 63;
     const int incl = wave_incl(v, lane);
     if (WG == 64) {
-        total = __shfl(incl, 63);
+        total = __builtin_amdgcn_readlane(incl, 63);
         __syncthreads();   // (this step's flags, written by other lanes, are read next)
         return incl - v;
     }
@@ -131,18 +136,91 @@ __device__ __forceinline__ int block_scan(int v, int *s, int &total) {
     return before + incl - v;
 }
 
-// One text per workgroup: which[blockIdx.x] indexes the texts of this launch shape.  Output at the
-// text's own input offsets (never longer than the input) plus its length.
-template <int WG>
+// The rank table copied into LDS (the latency form: few texts per call, each on a CU of its own):
+// keys[m] u32 (a << 16 | b per rank), cs[m] u16 (c per rank, padded to an even count), slot[S] u32
+// (fingerprint << 16 | rank + 1, or 0 = empty; S a power of two >= 2m, linear probing from
+// rank_home).  A probe reads one slot; only a fingerprint match reads the key and c (one more LDS
+// round).  14 B per merge: 8000 merges take 111 KiB.
+struct LdsTab {
+    const uint32_t *img;   // the image above in HBM, copied word by word
+    uint32_t words;        // its size in u32 words
+    uint32_t m;            // merges
+    uint32_t mask, shift;  // slot table: S = mask + 1, home = rank_home(key, shift)
+};
+
+__host__ __device__ __forceinline__ uint32_t fingerprint(uint32_t key) {
+    return (key * 0x85EBCA6Bu) >> 16;
+}
+
+template <bool TAB_LDS>
+struct Lookup {
+    RankTab g;
+    const uint32_t *keys, *slot;
+    const uint16_t *cs;
+    uint32_t mask, shift;
+    __device__ __forceinline__ uint32_t operator()(uint32_t key) const {
+        if constexpr (!TAB_LDS) {
+            uint32_t h = rank_home(key, g.shift);
+            for (;;) {
+                const unsigned long long e = g.slots[h];
+                if ((uint32_t)(e >> 32) == key) return (uint32_t)e;
+                if (e == ~0ull) return NO_RANK;
+                h = (h + 1) & g.mask;
+            }
+        } else {
+            const uint32_t fp = fingerprint(key);
+            uint32_t h = rank_home(key, shift);
+            for (;;) {
+                const uint32_t e = slot[h];
+                if (!e) return NO_RANK;
+                if ((e >> 16) == fp) {
+                    const uint32_t r = (e & 0xFFFFu) - 1;
+                    if (keys[r] == key) return (r << 16) | cs[r];
+                }
+                h = (h + 1) & mask;
+            }
+        }
+    }
+};
+
+// One text per workgroup: which[blockIdx.x] indexes the texts of this launch shape; up to
+// WG * (KMAX - 1) tokens, held in LDS as u16 ids + u32 rank words, rewritten in place.  Each greedy step:
+//   - every thread loads its segment [s, s + k) (k <= KMAX) plus two tokens of look-ahead and one
+//     rank word of look-behind into registers (one batch of LDS reads), and flags the counted
+//     occurrences of rank r there (the chain parity comes from the look-behind; a chain crossing
+//     into the segment is walked back in LDS, which only x == y runs do);
+//   - an exclusive scan of the counts gives the segment's destination (barrier: every read of this
+//     step is done before any write);
+//   - the segment is written back compacted; the pairs that now touch c get their rank word again,
+//     one request per lane per round, so a wave's probes run side by side;
+//   - the minimum rank word written is the next step's merge (barrier).
+template <int WG, int KMAX, bool TAB_LDS>
 __global__ void __launch_bounds__(WG)
 k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
          const int32_t *__restrict__ which, int32_t *__restrict__ out, int32_t *__restrict__ out_len,
-         RankTab t, int cap, unsigned long long *__restrict__ steps_total) {
-    extern __shared__ uint16_t lds16[];
+         RankTab t, LdsTab lt, unsigned long long *__restrict__ steps_total) {
+    static_assert(KMAX & 1, "odd segment lengths");
+    constexpr int CAP = WG * (KMAX - 1);
+    constexpr int H = KMAX + 2;   // segment + look-ahead
+    extern __shared__ uint32_t lds32[];
     __shared__ uint32_t red[WG / 64];
     __shared__ int scn[WG / 64];
-    uint16_t *tok = lds16, *rk = lds16 + cap, *tok2 = lds16 + 2 * cap, *rk2 = lds16 + 3 * cap;
-    uint8_t *fl = reinterpret_cast<uint8_t *>(lds16 + 4 * cap);
+    uint32_t *rk = lds32;
+    uint16_t *tok = reinterpret_cast<uint16_t *>(lds32 + CAP);
+    Lookup<TAB_LDS> look;
+    look.g = t;
+    if constexpr (TAB_LDS) {
+        uint32_t *tw = lds32 + CAP + CAP / 2;
+        const uint32_t w4 = lt.words & ~3u;
+        for (uint32_t w = 4 * threadIdx.x; w < w4; w += 4 * WG)
+            *reinterpret_cast<uint4 *>(tw + w) = *reinterpret_cast<const uint4 *>(lt.img + w);
+        for (uint32_t w = w4 + threadIdx.x; w < lt.words; w += WG) tw[w] = lt.img[w];
+        look.keys = tw;
+        look.cs = reinterpret_cast<const uint16_t *>(tw + lt.m);
+        look.slot = tw + lt.m + ((lt.m + 1) >> 1);
+        look.mask = lt.mask;
+        look.shift = lt.shift;
+    }
 
     const int text = which[blockIdx.x];
     const int64_t base = off[text];
@@ -153,82 +231,143 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
     __syncthreads();
     uint32_t lmin = NO_RANK;
     for (int i = tid; i < n; i += WG) {
-        const uint32_t r = i + 1 < n ? rank_of(t, tok[i], tok[i + 1]) : NO_RANK;
-        rk[i] = (uint16_t)r;
+        const uint32_t r = i + 1 < n ? look(((uint32_t)tok[i] << 16) | tok[i + 1]) : NO_RANK;
+        rk[i] = r;
         lmin = min(lmin, r);
     }
     uint32_t r = block_min<WG>(lmin, red);
-    if (WG == 64) __syncthreads();
+    __syncthreads();
     int steps = 0;
+#if BPE_ENC_TIMING
+    // (timing probe: shader cycles per phase of a step, thread 0, summed into steps_total[1..6])
+    long long tk[6] = {0, 0, 0, 0, 0, 0};
+    long long tprev = clock64();
+#define ENC_TICK(q)                                  \
+    do {                                             \
+        const long long now_ = clock64();            \
+        tk[q] += now_ - tprev;                       \
+        tprev = now_;                                \
+    } while (0)
+#else
+#define ENC_TICK(q) \
+    do {            \
+    } while (0)
+#endif
 
     while (r != NO_RANK) {   // (uniform: every thread holds the same r)
         ++steps;
-        const uint32_t c = t.c_of[r];
-        const int k = (n + WG - 1) / WG;
-        const int s = min(n, tid * k), e = min(n, s + k);
-        // 1. counted occurrences of rank r in [s, e): even offsets inside an r-chain (x == y runs;
-        //    for x != y a chain has length 1)
+        ENC_TICK(0);
+        const uint32_t c = r & 0xFFFFu;
+        // segment length: odd, so that lane t's j-th word (t * k + j) falls in a bank of its own
+        // (an even stride would put 2..16 lanes on one bank)
+        const int k = max(3, (n + WG - 1) / WG) | 1;   // (<= KMAX: n <= WG * (KMAX - 1))
+        const int s = tid * k;
+        const int len = max(0, min(k, n - s));       // segment [s, s + len)
+        uint32_t T[H], R[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const bool in_seg = j < k + 2 && s + j < n;
+            T[j] = in_seg ? tok[s + j] : 0u;
+            R[j] = in_seg ? rk[s + j] : NO_RANK;
+        }
+        const uint32_t rb = (len > 0 && s > 0) ? rk[s - 1] : NO_RANK;
+        // chain parity at the segment start: d = r-pairs right before s
+        int d = 0;
+        bool fprev = false;   // is s - 1 counted (s deleted)?
+        if (rb == r) {
+            for (int j = s - 1; j >= 0 && rk[j] == r; --j) ++d;
+            fprev = !((d - 1) & 1);
+        }
+        uint32_t F = 0;   // counted flags of [s, s + k + 2)
         int cnt = 0;
-        {
-            int d = 0;
-            if (s < e)
-                for (int j = s - 1; j >= 0 && rk[j] == r; --j) ++d;
-            for (int i = s; i < e; ++i) {
-                const bool m = rk[i] == r;
-                const bool f = m && !(d & 1);
-                fl[i] = f;
-                cnt += f;
-                d = m ? d + 1 : 0;
-            }
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const bool m = R[j] == r;
+            const bool f = m && !(d & 1);
+            F |= (uint32_t)f << j;
+            cnt += (f && j < len) ? 1 : 0;
+            d = m ? d + 1 : 0;
         }
-        // 2. destination of the segment: i - #counted in [0, i - 1) for its first live position
+        ENC_TICK(1);
         int total = 0;
-        const int before = block_scan<WG>(cnt, scn, total);   // (barrier: flags visible)
-        int p = s - before + (s > 0 && s < e ? fl[s - 1] : 0);
-        // 3. compacted rewrite; pairs touching c get their rank again
+        const int before = block_scan<WG>(cnt, scn, total);   // (barrier: all reads done)
+        ENC_TICK(2);
+        const int p0 = s - before + (fprev ? 1 : 0);
+        // live positions of the segment: j is dead when j - 1 is counted
+        const uint32_t live = ~((F << 1) | (fprev ? 1u : 0u)) & ((1u << len) - 1u);
+        int p = p0;
         lmin = NO_RANK;
-        for (int i = s; i < e; ++i) {
-            if (i > 0 && fl[i - 1]) continue;   // the b of a counted (a, b)
-            const bool fi = fl[i];
-            const uint32_t tv = fi ? c : tok[i];
-            const int nx = fi ? i + 2 : i + 1;
-            uint32_t rv = NO_RANK;
-            if (nx < n) {
-                const bool fn = fl[nx];
-                rv = (fi || fn) ? rank_of(t, tv, fn ? c : tok[nx]) : rk[i];
+        uint32_t K[KMAX];
+        uint32_t req = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            K[j] = 0;
+            if ((live >> j) & 1) {   // (else: the b of a counted (a, b), or past the segment)
+                const bool fi = (F >> j) & 1;
+                const uint32_t tv = fi ? c : T[j];
+                const int nx = fi ? j + 2 : j + 1;
+                uint32_t rv = NO_RANK;
+                if (s + nx < n) {
+                    const bool fn = (F >> nx) & 1;
+                    const uint32_t tn = fi ? T[j + 2] : T[j + 1];
+                    if (fi || fn) {
+                        K[j] = (tv << 16) | (fn ? c : tn);
+                        req |= 1u << j;
+                    }
+                    rv = R[j];
+                }
+                tok[p] = (uint16_t)tv;
+                if (!((req >> j) & 1)) {
+                    rk[p] = rv;
+                    lmin = min(lmin, rv);
+                }
+                ++p;
             }
-            tok2[p] = (uint16_t)tv;
-            rk2[p] = (uint16_t)rv;
-            ++p;
-            lmin = min(lmin, rv);
         }
+        // the new pairs' rank words: one request per lane per round (its position: p0 + the live
+        // positions before it)
+        while (__ballot(req != 0)) {
+            if (req) {
+                const int j = __builtin_ctz(req);
+                uint32_t key = 0;
+#pragma unroll
+                for (int jj = 0; jj < KMAX; ++jj)
+                    if (jj == j) key = K[jj];
+                const int pp = p0 + __builtin_popcount(live & ((1u << j) - 1u));
+                const uint32_t rv = look(key);
+                rk[pp] = rv;
+                lmin = min(lmin, rv);
+                req &= req - 1;
+            }
+        }
+        ENC_TICK(4);
         n -= total;
-        uint16_t *x = tok;
-        tok = tok2;
-        tok2 = x;
-        x = rk;
-        rk = rk2;
-        rk2 = x;
-        r = block_min<WG>(lmin, red);   // (barrier: the new buffer visible, the old one free)
-        if (WG == 64) __syncthreads();
+        r = block_min<WG>(lmin, red);   // (barrier: the rewritten text visible)
+        __syncthreads();
+        ENC_TICK(5);
     }
 
     for (int i = tid; i < n; i += WG) out[base + i] = tok[i];
     if (tid == 0) {
         out_len[text] = n;
         if (steps_total && steps) atomicAdd(steps_total, (unsigned long long)steps);
+#if BPE_ENC_TIMING
+        for (int q = 0; q < 6; ++q) atomicAdd(steps_total + 1 + q, (unsigned long long)tk[q]);
+#endif
     }
 }
 
-template <int WG>
-constexpr int cap_of() {
-    return WG == 64 ? CAP_64 : WG == 256 ? CAP_256 : CAP_1024;
-}
+// launch shapes (WG threads x KMAX tokens each), by text length: the smallest that holds the text,
+// so the unrolled segment loops do little masked-off work
+constexpr int N_SHAPES = 8;
+constexpr int SHAPE_WG[N_SHAPES] = {64, 64, 64, 256, 256, 256, 1024, 1024};
+constexpr int SHAPE_K[N_SHAPES] = {3, 5, 9, 5, 9, 17, 9, 17};
 
-template <int WG>
-constexpr size_t lds_of() {
-    return (size_t)cap_of<WG>() * 9;
-}
+constexpr int shape_cap(int i) { return SHAPE_WG[i] * (SHAPE_K[i] - 1); }
+constexpr size_t shape_lds(int i) { return (size_t)shape_cap(i) * 6; }
+// shorter texts take the HBM table even in the few-texts form (the LDS copy costs more than its
+// faster probes save over their few steps)
+constexpr int LDS_TAB_MIN_TOKENS = 128;
 
 }  // namespace
 
@@ -243,12 +382,15 @@ struct bpe_encoder {
     // rank table (host copy; uploaded when dirty)
     std::vector<unsigned long long> slots;
     uint32_t bits = 0;
-    std::vector<uint16_t> c_of;
+    std::vector<uint16_t> c_of;               // rank -> c
     bool dirty = true;
     unsigned long long *d_slots = nullptr;
     size_t d_slots_n = 0;
-    uint16_t *d_c = nullptr;
-    size_t d_c_n = 0;
+    // the same merges as the LDS image (LdsTab), for calls of few texts
+    std::vector<uint32_t> limg;
+    uint32_t *d_limg = nullptr;
+    size_t d_limg_n = 0;
+    LdsTab lt{};
     unsigned long long *d_steps = nullptr;
     // staging: pinned host and device, grown as needed
     char *h_buf = nullptr, *d_buf = nullptr;
@@ -266,7 +408,7 @@ void table_insert(bpe_encoder *E, uint32_t key, uint32_t rank) {
     for (;;) {
         unsigned long long &s = E->slots[h];
         if (s == ~0ull) {
-            s = ((unsigned long long)key << 32) | rank;
+            s = ((unsigned long long)key << 32) | (rank << 16) | E->c_of[rank];
             return;
         }
         if ((uint32_t)(s >> 32) == key) return;   // a repeated pair: its first rank wins (the
@@ -295,18 +437,83 @@ int grow_dev(T **p, size_t *have, size_t want) {
     return BPE_OK;
 }
 
+// the LDS image of the merges (LdsTab): keys, cs, slots
+void build_lds_image(bpe_encoder *E) {
+    const uint32_t m = (uint32_t)E->c_of.size();
+    uint32_t bits = 1;
+    while ((1u << bits) < 2 * m) ++bits;
+    const uint32_t S = 1u << bits, m2 = (m + 1) & ~1u;
+    E->limg.assign(m + m2 / 2 + S, 0u);
+    uint32_t *keys = E->limg.data();
+    uint16_t *cs = reinterpret_cast<uint16_t *>(keys + m);
+    uint32_t *slot = keys + m + m2 / 2;
+    for (uint32_t r = 0; r < m; ++r) {
+        const uint32_t key = ((uint32_t)E->abc[3 * r] << 16) | (uint32_t)E->abc[3 * r + 1];
+        keys[r] = key;
+        cs[r] = E->c_of[r];
+        uint32_t h = rank_home(key, 32 - bits);
+        while (slot[h] && keys[(slot[h] & 0xFFFFu) - 1] != key) h = (h + 1) & (S - 1);
+        if (!slot[h]) slot[h] = (fingerprint(key) << 16) | (r + 1);   // (a repeated pair keeps its first rank)
+    }
+    E->lt.words = (uint32_t)E->limg.size();
+    E->lt.m = m;
+    E->lt.mask = S - 1;
+    E->lt.shift = 32 - bits;
+}
+
 int upload_table(bpe_encoder *E) {
     if (!E->dirty) return BPE_OK;
     int rc;
     if ((rc = grow_dev(&E->d_slots, &E->d_slots_n, E->slots.size()))) return rc;
-    if ((rc = grow_dev(&E->d_c, &E->d_c_n, std::max<size_t>(E->c_of.size(), 1)))) return rc;
     ENC_TRY(hipMemcpyAsync(E->d_slots, E->slots.data(), E->slots.size() * 8, hipMemcpyHostToDevice,
                            E->stream));
-    if (!E->c_of.empty())
-        ENC_TRY(hipMemcpyAsync(E->d_c, E->c_of.data(), E->c_of.size() * 2, hipMemcpyHostToDevice,
-                               E->stream));
+    build_lds_image(E);
+    if ((rc = grow_dev(&E->d_limg, &E->d_limg_n, E->limg.size()))) return rc;
+    ENC_TRY(hipMemcpyAsync(E->d_limg, E->limg.data(), E->limg.size() * 4, hipMemcpyHostToDevice,
+                           E->stream));
+    E->lt.img = E->d_limg;
     E->dirty = false;
     return BPE_OK;
+}
+
+// texts per call up to which each gets a CU of its own, so the LDS copy of the table pays
+constexpr size_t LATENCY_TEXTS = 256;
+
+template <int I, bool TAB_LDS>
+hipError_t set_lds_attr() {
+    return hipFuncSetAttribute((const void *)k_encode<SHAPE_WG[I], SHAPE_K[I], TAB_LDS>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(TAB_LDS ? LDS_BYTES : shape_lds(I)));
+}
+
+template <int I>
+hipError_t set_lds_attrs() {
+    hipError_t e = set_lds_attr<I, true>();
+    if (e == hipSuccess) e = set_lds_attr<I, false>();
+    if constexpr (I + 1 < N_SHAPES) {
+        if (e == hipSuccess) e = set_lds_attrs<I + 1>();
+    }
+    return e;
+}
+
+template <int I>
+void launch_one(bpe_encoder *E, unsigned n, bool tab_lds, const int32_t *ids, const int64_t *off,
+                const int32_t *which, int32_t *out, int32_t *len) {
+    constexpr int WG = SHAPE_WG[I], KM = SHAPE_K[I];
+    const RankTab t{E->d_slots, (1u << E->bits) - 1, 32 - E->bits};
+    if (tab_lds)
+        k_encode<WG, KM, true><<<n, WG, shape_lds(I) + (size_t)E->lt.words * 4, E->stream>>>(
+            ids, off, which, out, len, t, E->lt, E->d_steps);
+    else
+        k_encode<WG, KM, false><<<n, WG, shape_lds(I), E->stream>>>(ids, off, which, out, len, t,
+                                                                    E->lt, E->d_steps);
+}
+
+template <int I = 0>
+void launch_shape(int i, bpe_encoder *E, unsigned n, bool tab_lds, const int32_t *ids,
+                  const int64_t *off, const int32_t *which, int32_t *out, int32_t *len) {
+    if (i == I) return launch_one<I>(E, n, tab_lds, ids, off, which, out, len);
+    if constexpr (I + 1 < N_SHAPES) launch_shape<I + 1>(i, E, n, tab_lds, ids, off, which, out, len);
 }
 
 int grow_stage(bpe_encoder *E, size_t bytes) {
@@ -393,13 +600,10 @@ int bpe_encoder_create(bpe_encoder **out, int device) {
         hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&E->ev0) != hipSuccess || hipEventCreate(&E->ev1) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_HIP, "bpe native: encoder stream/events"));
-    if (hipMalloc((void **)&E->d_steps, 8) != hipSuccess ||
-        hipMemset(E->d_steps, 0, 8) != hipSuccess)
+    if (hipMalloc((void **)&E->d_steps, 64) != hipSuccess ||
+        hipMemset(E->d_steps, 0, 64) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_OOM, "bpe native: encoder counters"));
-    if (hipFuncSetAttribute((const void *)k_encode<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds_of<1024>()) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_encode<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds_of<256>()) != hipSuccess)
+    if (set_lds_attrs<0>() != hipSuccess)
         return bail(bpe_fail(BPE_ERR_HIP, "bpe native: encoder LDS attribute"));
     table_rebuild(E, 10);
     *out = E;
@@ -412,7 +616,7 @@ int bpe_encoder_destroy(bpe_encoder *E) {
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     if (E->scratch) bpe_destroy(E->scratch);
     if (E->d_slots) (void)hipFree(E->d_slots);
-    if (E->d_c) (void)hipFree(E->d_c);
+    if (E->d_limg) (void)hipFree(E->d_limg);
     if (E->d_steps) (void)hipFree(E->d_steps);
     if (E->d_buf) (void)hipFree(E->d_buf);
     if (E->h_buf) (void)hipHostFree(E->h_buf);
@@ -491,21 +695,24 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     std::vector<int64_t> len((size_t)n_texts);
     std::vector<int32_t> out((size_t)std::max<int64_t>(total, 1));
     const int64_t m = (int64_t)E->c_of.size();
-    // launch shape of every text: 0/1/2 = k_encode<64/256/1024>, 3 = the apply-pass route
-    std::vector<int32_t> lists[3];
+    // launch shape of every text (the smallest that holds it), or the apply-pass route
+    std::vector<int32_t> lists[N_SHAPES];
     std::vector<int64_t> replay;
     for (int64_t k = 0; k < n_texts; ++k) {
         const int64_t l = off[k + 1] - off[k];
         if (m == 0 || l < 2) {
             std::memcpy(out.data() + (off[k] - base), ids + off[k], (size_t)l * 4);
             len[k] = l;
-        } else if (!E->greedy_ok || l > CAP_1024) {
+        } else if (!E->greedy_ok || l > CAP_MAX) {
             replay.push_back(k);
         } else {
-            lists[l <= CAP_64 ? 0 : l <= CAP_256 ? 1 : 2].push_back((int32_t)k);
+            int i = 0;
+            while (shape_cap(i) < l) ++i;
+            lists[i].push_back((int32_t)k);
         }
     }
-    const int64_t n_rank = (int64_t)(lists[0].size() + lists[1].size() + lists[2].size());
+    int64_t n_rank = 0;
+    for (auto &L : lists) n_rank += (int64_t)L.size();
     int rc;
     if (n_rank) {
         if ((rc = upload_table(E))) return rc;
@@ -530,20 +737,17 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         const int32_t *d_which = reinterpret_cast<const int32_t *>(d + b_ids + b_off);
         int32_t *d_out = reinterpret_cast<int32_t *>(d + up);
         int32_t *d_len = reinterpret_cast<int32_t *>(d + up + b_ids);
-        RankTab t{E->d_slots, (1u << E->bits) - 1, 32 - E->bits, E->d_c};
+        // few texts: each has a CU to itself, and the table is read from LDS (when it fits)
+        const size_t tab = (size_t)E->lt.words * 4;
+        const bool few = (size_t)n_rank <= LATENCY_TEXTS;
         ENC_TRY(hipEventRecord(E->ev0, E->stream));
         at = 0;
-        if (!lists[0].empty())
-            k_encode<64><<<(unsigned)lists[0].size(), 64, lds_of<64>(), E->stream>>>(
-                d_ids, d_off, d_which + at, d_out, d_len, t, CAP_64, E->d_steps);
-        at += lists[0].size();
-        if (!lists[1].empty())
-            k_encode<256><<<(unsigned)lists[1].size(), 256, lds_of<256>(), E->stream>>>(
-                d_ids, d_off, d_which + at, d_out, d_len, t, CAP_256, E->d_steps);
-        at += lists[1].size();
-        if (!lists[2].empty())
-            k_encode<1024><<<(unsigned)lists[2].size(), 1024, lds_of<1024>(), E->stream>>>(
-                d_ids, d_off, d_which + at, d_out, d_len, t, CAP_1024, E->d_steps);
+        for (int i = 0; i < N_SHAPES; ++i) {
+            if (lists[i].empty()) continue;
+            const bool tab_lds = few && shape_cap(i) > LDS_TAB_MIN_TOKENS && shape_lds(i) + tab <= LDS_BYTES;
+            launch_shape(i, E, (unsigned)lists[i].size(), tab_lds, d_ids, d_off, d_which + at, d_out, d_len);
+            at += lists[i].size();
+        }
         ENC_TRY(hipGetLastError());
         ENC_TRY(hipEventRecord(E->ev1, E->stream));
         ENC_TRY(hipMemcpyAsync(h + up, d + up, b_ids + b_len, hipMemcpyDeviceToHost, E->stream));
@@ -578,9 +782,15 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
 int bpe_encoder_get_stats(bpe_encoder *E, bpe_encoder_stats *out) {
     if (!E || !out) return bpe_fail(BPE_ERR_ARG, "bpe native: null argument");
     ENC_TRY(hipSetDevice(E->device));
-    unsigned long long steps = 0;
-    ENC_TRY(hipMemcpy(&steps, E->d_steps, 8, hipMemcpyDeviceToHost));
-    E->st.steps = (int64_t)steps;
+    unsigned long long steps[8] = {};
+    ENC_TRY(hipMemcpy(steps, E->d_steps, 64, hipMemcpyDeviceToHost));
+    E->st.steps = (int64_t)steps[0];
+#if BPE_ENC_TIMING
+    fprintf(stderr, "[enc timing] cycles per step: read+flags %.0f scan %.0f write %.0f lookups %.0f min %.0f (pre %.0f)\n",
+            (double)steps[2] / std::max(1ull, steps[0]), (double)steps[3] / std::max(1ull, steps[0]),
+            (double)steps[4] / std::max(1ull, steps[0]), (double)steps[5] / std::max(1ull, steps[0]),
+            (double)steps[6] / std::max(1ull, steps[0]), (double)steps[1] / std::max(1ull, steps[0]));
+#endif
     *out = E->st;
     return BPE_OK;
 }
@@ -588,7 +798,7 @@ int bpe_encoder_get_stats(bpe_encoder *E, bpe_encoder_stats *out) {
 int bpe_encoder_reset_stats(bpe_encoder *E) {
     if (!E) return bpe_fail(BPE_ERR_ARG, "bpe native: null argument");
     ENC_TRY(hipSetDevice(E->device));
-    ENC_TRY(hipMemset(E->d_steps, 0, 8));
+    ENC_TRY(hipMemset(E->d_steps, 0, 64));
     E->st = bpe_encoder_stats{};
     return BPE_OK;
 }

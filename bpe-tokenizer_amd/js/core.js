@@ -394,7 +394,7 @@ class BPETokenizer {
    * @description encode to binary string (core.ts:392-409).
    * With enough merges the text is encoded on the GPU by the merge-rank encoder (bpe_encode_batch:
    * the lowest-ranked merge present is rewritten until none is, which equals the reference's
-   * in-order replaceAll of every merge; texts over 16384 tokens are replayed by apply-only passes
+   * in-order replaceAll of every merge; texts over ENCODE_LDS_TOKENS tokens are replayed by apply-only passes
    * over HBM).  Short merge lists keep the reference's replay here (see native.js).
    */
   encodeToCode(content) {

@@ -12,20 +12,30 @@ function loadNative() {
 }
 
 /**
- * encodeToCode (core.ts:392-409) runs on the GPU (the merge-rank encoder, bpe_encode_batch) for a
- * merge list of at least ENCODE_ON_DEVICE_MERGES merges, or a text of at least
- * ENCODE_ON_DEVICE_CHARS chars with at least ENCODE_ON_DEVICE_MIN_MERGES merges.  Below that the
- * reference's own replay (one split/join per merge, ~0.45 us per merge on a short text in Node)
- * finishes before one device round trip would (profiles/r04_encode_crossover.json).
- * BPE_ENCODE_MIN_MERGES overrides the first threshold (e.g. host-only runs without a device).
+ * encodeToCode (core.ts:392-409) runs on the GPU (bpe_encode_batch: the merge-rank encoder for
+ * texts up to ENCODE_LDS_TOKENS tokens, apply-only replay passes above) when a per-call cost model
+ * fitted to the measured crossover (profiles/r04_encode_crossover.json, MI355X + Node on the box's
+ * host) says it beats the reference's own replay (one split/join per merge, kept below):
+ *   JS replay     ~ 0.11 us per merge + chars x (0.03 + 0.00005 x merges) us
+ *   device (LDS)  ~ 30 us per call + 1.6 us per greedy step (at most min(merges, 0.4 x chars))
+ *                   + 0.05 us per char (id and code conversions, copies)
+ *   device (long) ~ 10 us per merge (one replay pass each) + 0.05 us per char
+ * In practice: long merge lists with short texts, and long texts.  BPE_ENCODE_DEVICE=0 keeps every
+ * call on the JS replay (host-only runs without a device), =1 sends every call with a merge to the
+ * device (tests).
  */
-const ENCODE_ON_DEVICE_CHARS = 1 << 16
-const ENCODE_ON_DEVICE_MIN_MERGES = 16
-const ENCODE_ON_DEVICE_MERGES = +process.env.BPE_ENCODE_MIN_MERGES || 128
+const ENCODE_LDS_TOKENS = 16384
+const ENCODE_DEVICE = process.env.BPE_ENCODE_DEVICE
 
 function encodeOnDevice(n_chars, n_merges) {
-  if (n_chars < 2 || n_merges < ENCODE_ON_DEVICE_MIN_MERGES) return false
-  return n_merges >= ENCODE_ON_DEVICE_MERGES || n_chars >= ENCODE_ON_DEVICE_CHARS
+  if (n_chars < 2 || n_merges < 1 || ENCODE_DEVICE === '0') return false
+  if (ENCODE_DEVICE === '1') return true
+  const js = 0.11 * n_merges + n_chars * (0.03 + 0.00005 * n_merges)
+  const dev =
+    n_chars <= ENCODE_LDS_TOKENS
+      ? 30 + 1.6 * Math.min(n_merges, 0.4 * n_chars) + 0.05 * n_chars
+      : 10 * n_merges + 0.05 * n_chars
+  return dev < js
 }
 
 /**

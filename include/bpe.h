@@ -302,12 +302,13 @@ int bpe_get_stream(bpe_ctx *ctx, void **stream);
  * corpus: `for (let [from_code, to_code] of this.merge_codes) content_in_code =
  * content_in_code.replaceAll(from_code, to_code)` (core.ts:404-406) on every text.  An encoder
  * holds the merge list as a rank table on one device.  A text of up to
- * 16384 tokens is encoded by one workgroup in LDS: the lowest-ranked merge present is rewritten
+ * BPE_ENCODE_LDS_TOKENS tokens is encoded by one workgroup in LDS: the lowest-ranked merge present is rewritten
  * (all its leftmost non-overlapping occurrences) until none is, which equals the in-order replay
  * whenever no merge's new token c is an input (a or b) of itself or an earlier merge — every list
  * the reference makes (c is a fresh index, core.ts:315,484).  Longer texts, and lists that break
  * that rule (checked as merges are added), are replayed merge by merge by apply-only streaming
  * passes (bpe_apply_merges on a scratch engine of the encoder).  Output is identical either way. */
+#define BPE_ENCODE_LDS_TOKENS 16384
 typedef struct bpe_encoder bpe_encoder;
 typedef struct {
     double kernel_ms;         /* HIP-event time of the merge-rank kernels (per call: launch to end) */

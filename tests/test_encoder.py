@@ -5,7 +5,7 @@
     running core.ts itself: oracle/gen_golden.py), and
   - the C restatement of the replay (oracle_encode: every merge in order, core.ts:404-406) on
     seeded random merge lists and texts, at every launch shape (k_encode<64/256/1024>) and on the
-    apply-pass route (texts over 16384 tokens, merge lists the greedy cannot take).
+    apply-pass route (texts over ENCODE_LDS_TOKENS tokens, merge lists the greedy cannot take).
 
 The CPU-only test at the bottom checks the merge-rank greedy itself (the kernel's algorithm,
 restated in Python) against the replay, without a device.
@@ -96,16 +96,17 @@ def test_random_texts_every_launch_shape(seed):
     alphabet = [3, 12, 40][seed - 1]
     merges = trained_merges(rng, alphabet, 40, 300)
     assert len(merges) > 20
+    cap = pkg.ENCODE_LDS_TOKENS
     lengths = [0, 1, 2, 3, 63, 64, 65, 200, 511, 512, 513, 1000, 4095, 4096, 4097, 9000,
-               16383, 16384, 16385, 20000]
+               cap - 1, cap, cap + 1, 20000]
     texts = random_texts(rng, alphabet, lengths) + skewed_texts(rng, alphabet, lengths[:16])
     enc = pkg.Encoder(0, merges)
     enc.reset_stats()
     check(enc, texts, merges)
     st = enc.stats()
-    long = sum(1 for t in texts if len(t) > 16384)
+    long = sum(1 for t in texts if len(t) > cap)
     assert st['texts_replay'] == long
-    assert st['texts_rank'] == sum(1 for t in texts if 2 <= len(t) <= 16384)
+    assert st['texts_rank'] == sum(1 for t in texts if 2 <= len(t) <= cap)
     assert st['steps'] > 0
     enc.close()
 
@@ -147,6 +148,31 @@ def test_merges_added_in_batches_and_cleared():
     enc.clear()
     assert enc.num_merges() == 0
     assert [t.tolist() for t in enc.encode(texts)] == [t.tolist() for t in texts]
+    enc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('m', [3000, 20000])
+def test_synthetic_merge_lists_few_and_many_texts(m):
+    """Random valid merge lists (c = a fresh id, inputs any earlier id): 3000 merges keep the
+    table in LDS for a call of few texts, 20000 do not (the HBM table then); the same texts in a
+    call of many (the HBM table)."""
+    rng = np.random.default_rng(m)
+    A = 60
+    merges = [(int(rng.integers(0, A + k)), int(rng.integers(0, A + k)), A + k) for k in range(m)]
+    # texts built from merged tokens' expansions, so that deep merges fire
+    exp = [[i] for i in range(A)]
+    for a, b, _c in merges:
+        exp.append(exp[a] + exp[b] if len(exp[a]) + len(exp[b]) < 64 else exp[a])
+    texts = []
+    for l in [5, 50, 300, 600, 3000, 9000]:
+        t = []
+        while len(t) < l:
+            t += exp[int(rng.integers(0, len(exp)))]
+        texts.append(np.asarray(t[:l], np.int32))
+    enc = pkg.Encoder(0, merges)
+    check(enc, texts, merges)
+    check(enc, texts * 60, merges)   # 360 texts: past the few-texts form
     enc.close()
 
 

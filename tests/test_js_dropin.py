@@ -39,7 +39,7 @@ def test_addon_builds_and_exports():
 
 # (no device here: encodeToCode keeps the reference's JS replay for every merge-list length;
 # the GPU tests run the same golden vectors through the device encoder)
-HOST_ONLY = {'BPE_ENCODE_MIN_MERGES': '1e9'}
+HOST_ONLY = {'BPE_ENCODE_DEVICE': '0'}
 
 
 def test_host_logic_against_golden():
@@ -68,6 +68,15 @@ def test_db_twin_spec_golden_and_lockstep():
 def test_reference_spec_and_golden_through_js():
     build_addon()
     out = run_node('spec_gpu.js', '--expose-gc')
+    assert 'spec_gpu ok' in out
+
+
+@pytest.mark.gpu
+def test_reference_spec_and_golden_through_js_device_encoder():
+    """The same run with every encodeToCode that has a merge sent to the device encoder
+    (BPE_ENCODE_DEVICE=1): the golden vectors of all 1509 cases through bpe_encode_batch."""
+    build_addon()
+    out = run_node('spec_gpu.js', '--expose-gc', env={'BPE_ENCODE_DEVICE': '1'})
     assert 'spec_gpu ok' in out
 
 

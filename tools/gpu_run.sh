@@ -17,6 +17,7 @@
 #   rccl       the RCCL legs at world 1: tools/sharded_overhead.py (per-iteration cost)
 #   encode     the device encoder: tools/encode_bench.py (uniform and zipf merges, 100k short
 #              texts) and tools/encode_crossover.js (JS replay vs device per call)
+#   enclat     tools/encode_latency.py (one text per call: wall and kernel time per call)
 #   profenc    rocprofv3 --kernel-trace --stats of tools/encode_bench.py (zipf)
 # Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), BPE_LIB (A/B builds)
 set -o pipefail
@@ -108,6 +109,10 @@ for step in "$@"; do
     timeout -k 10 300 node tools/encode_crossover.js > "$OUT/crossover.json" 2>> "$OUT/encode.err" \
         || fail crossover "$OUT/encode.err"
     cat "$OUT/crossover.json" ;;
+  enclat)
+    timeout -k 10 300 python3 -u tools/encode_latency.py > "$OUT/latency.json" 2> "$OUT/latency.err" \
+        || fail enclat "$OUT/latency.err"
+    cat "$OUT/latency.json" ;;
   profenc)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/enc" -o run --output-format csv \
         -- python3 tools/encode_bench.py --corpus zipf > "$OUT/enc.jsonl" 2> "$OUT/enc.err" \
