@@ -542,18 +542,13 @@ class Encoder:
         _check(lib().bpe_encoder_reset_stats(self._enc), 'bpe_encoder_reset_stats')
 
 
-def encode_samples(samples, merges, len16, device=0):
+def encode_samples(samples, merges, len16=None, device=0):
     """Batch encoding with a trained merge list (encodeToCode, core.ts:392-409, for many texts at
-    once): the samples (base token ids) go into a fresh engine, the merges (a, b, c) are applied in
-    order by apply-only passes, and the encoded samples come back as id lists."""
-    e = Engine(device)
+    once): the device encoder (bpe_encode_batch) — the merge-rank kernel for samples up to
+    ENCODE_LDS_TOKENS tokens, apply-only replay passes for longer ones.  merges: (a, b, c) triples
+    in list order.  (len16 is accepted for the older signature; encoding never reads it.)"""
+    enc = Encoder(device, merges)
     try:
-        for i, l in enumerate(len16):
-            e.set_token_len16(i, int(l))
-        for s in samples:
-            e.add_sample(s)
-        if len(merges):
-            e.apply_merges(merges, count_after=False)
-        return e.samples()
+        return [x.tolist() for x in enc.encode([np.asarray(s, dtype=np.int32) for s in samples])]
     finally:
-        e.close()
+        enc.close()

@@ -100,10 +100,26 @@ namespace {
         if (rc_ < 0) return rc_;   \
     } while (0)
 
+// RCCL has to run on the same HIP runtime as libbpe.  A process can hold two: PyTorch's wheel
+// bundles libamdhip64 and librccl under the same sonames as /opt/rocm/lib, and when libbpe is
+// loaded before `import torch` both runtimes end up in the process.  A plain dlopen("librccl.so.1")
+// would then return torch's RCCL (already loaded, same soname), whose HIP runtime finds no device
+// ("ncclCommInitAll: unhandled cuda error").  So the RCCL in the directory of libbpe's own
+// libamdhip64 comes first, by path.
 int load_rccl(Rccl &r) {
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void *>(&hipGetDeviceCount), &info) && info.dli_fname) {
+        std::string dir(info.dli_fname);
+        const size_t slash = dir.rfind('/');
+        if (slash != std::string::npos) {
+            dir.resize(slash + 1);
+            for (const char *nm : {"librccl.so.1", "librccl.so"})
+                if ((r.so = dlopen((dir + nm).c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+        }
+    }
     const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
     for (const char *nm : names)
-        if ((r.so = dlopen(nm, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!r.so && (r.so = dlopen(nm, RTLD_NOW | RTLD_LOCAL))) break;
     if (!r.so) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL (librccl.so) not found");
     r.init_all = (decltype(r.init_all))dlsym(r.so, "ncclCommInitAll");
     r.all_reduce = (decltype(r.all_reduce))dlsym(r.so, "ncclAllReduce");

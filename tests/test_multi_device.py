@@ -174,6 +174,20 @@ def test_rccl_exchange_over_two_devices():
     assert two.merge_until(0, 2, 300) == one.merge_until(0, 2, 300)
 
 
+def test_rccl_context_when_libbpe_loads_before_torch():
+    """libbpe loaded (system HIP runtime) before `import torch` (torch's bundled HIP runtime and
+    RCCL, same sonames): the RCCL context must still come up, on the RCCL next to libbpe's own HIP
+    runtime (bpe_multi.cpp load_rccl).  Before the fix ncclCommInitAll picked torch's RCCL and
+    failed with 'unhandled cuda error' (this is the order pytest's collection produces)."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tools',
+                          'debug', 'rccl_after_torch.py')
+    out = subprocess.run([sys.executable, script, 'bpefirst', 'torch', 'work'], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0 and '\nok' in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+
+
 @pytest.mark.parametrize('corpus', ['uniform', 'zipf'])
 def test_rccl_one_device_context(corpus):
     """bpe_create_multi with RCCL on one device (ncclCommInitAll over [0]): the rank loop's
