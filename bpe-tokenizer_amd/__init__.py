@@ -38,6 +38,7 @@ C_API = [
     'bpe_cold_counts', 'bpe_set_global_counts',
     'bpe_encoder_create', 'bpe_encoder_destroy', 'bpe_encoder_add_merges', 'bpe_encoder_clear',
     'bpe_encoder_num_merges', 'bpe_encode_batch', 'bpe_encoder_get_stats', 'bpe_encoder_reset_stats',
+    'bpe_rccl_unique_id', 'bpe_rank_rccl_init', 'bpe_rank_loop_rccl', 'bpe_rank_rccl_destroy',
 ]
 HOT_BINS = 65536
 TABLE_BINS = 81920
@@ -75,6 +76,13 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def rccl_unique_id():
+    """ncclGetUniqueId of the RCCL beside libbpe's HIP runtime: 128 bytes (bpe_rccl_unique_id)."""
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().bpe_rccl_unique_id(buf, 128), 'bpe_rccl_unique_id')
+    return buf.raw
 
 
 class EncoderStats(ctypes.Structure):
@@ -155,6 +163,10 @@ def lib():
         'bpe_rank_loop_count': ([vp], ctypes.c_int),
         'bpe_rank_loop_end': ([vp, i64p, ctypes.c_int64, i64p, ctypes.POINTER(ctypes.c_int)],
                               ctypes.c_int),
+        'bpe_rccl_unique_id': ([vp, ctypes.c_size_t], ctypes.c_int),
+        'bpe_rank_rccl_init': ([vp, vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        'bpe_rank_loop_rccl': ([vp, vp, ctypes.c_int64, vp, ctypes.c_int], ctypes.c_int),
+        'bpe_rank_rccl_destroy': ([vp], ctypes.c_int),
         'bpe_encoder_create': ([ctypes.POINTER(vp), ctypes.c_int], ctypes.c_int),
         'bpe_encoder_destroy': ([vp], ctypes.c_int),
         'bpe_encoder_add_merges': ([vp, i32p, ctypes.c_int64], ctypes.c_int),
@@ -447,6 +459,17 @@ class Engine:
         k = n.value
         return ([tuple(int(v) for v in out[4 * i:4 * i + 3]) for i in range(k)],
                 [int(out[4 * i + 3]) for i in range(k)], st.value)
+
+    def rccl_init(self, unique_id, rank, world):
+        """This context's RCCL communicator (bpe_rank_rccl_init); unique_id: 128 bytes made by
+        rccl_unique_id() on rank 0 and broadcast."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        _check(lib().bpe_rank_rccl_init(self._ctx, buf, int(rank), int(world)), 'bpe_rank_rccl_init')
+
+    def rank_loop_rccl(self, xchg_ptr, xchg_words, tie_ptr, iterations):
+        """`iterations` rank-loop iterations with their all-reduces from C++ (bpe_rank_loop_rccl)."""
+        _check(lib().bpe_rank_loop_rccl(self._ctx, xchg_ptr, int(xchg_words), tie_ptr, int(iterations)),
+               'bpe_rank_loop_rccl')
 
     def cold_counts(self, keys_ptr, counts_ptr, cap):
         """This shard's exact count of every cold pair (one pass, kept for a second call): the

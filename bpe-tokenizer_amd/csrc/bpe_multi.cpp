@@ -47,6 +47,8 @@ struct Rccl {
     ncclResult_t (*group_end)() = nullptr;
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
 };
 
 }  // namespace
@@ -127,6 +129,8 @@ int load_rccl(Rccl &r) {
     r.group_end = (decltype(r.group_end))dlsym(r.so, "ncclGroupEnd");
     r.destroy = (decltype(r.destroy))dlsym(r.so, "ncclCommDestroy");
     r.error_string = (decltype(r.error_string))dlsym(r.so, "ncclGetErrorString");
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.so, "ncclGetUniqueId");
+    r.init_rank = (decltype(r.init_rank))dlsym(r.so, "ncclCommInitRank");
     if (!r.init_all || !r.all_reduce || !r.group_start || !r.group_end || !r.destroy)
         return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
     return BPE_OK;
@@ -905,3 +909,108 @@ int multi_reset_stats(bpe_multi *m) {
 }
 
 int multi_get_stream(bpe_multi *m, void **stream) { return bpe_get_stream(m->sh[0], stream); }
+
+// ---- one rank of a sharded corpus per process: the rank loop's collectives from C++ ---------------
+// (include/bpe.h bpe_rank_rccl_*): one RCCL communicator per context, its all-reduces issued on the
+// context's own stream between the rank loop's kernels, so a batch of iterations is enqueued by
+// one call with no host round trip and no cross-stream event per collective.
+namespace {
+struct RankComm {
+    Rccl rccl;
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+};
+std::map<bpe_ctx *, RankComm> &rank_comms() {
+    static std::map<bpe_ctx *, RankComm> m;
+    return m;
+}
+Rccl &id_rccl() {   // (the library ncclGetUniqueId comes from: loaded once, kept)
+    static Rccl r;
+    return r;
+}
+}  // namespace
+
+// (internal, bpe_engine.hip bpe_destroy) a context going away frees its communicator
+void rank_rccl_forget(bpe_ctx *ctx) {
+    auto &m = rank_comms();
+    auto it = m.find(ctx);
+    if (it == m.end()) return;
+    if (it->second.comm && it->second.rccl.destroy) it->second.rccl.destroy(it->second.comm);
+    m.erase(it);
+}
+
+extern "C" {
+
+int bpe_rccl_unique_id(void *id, size_t cap) {
+    if (!id || cap < sizeof(ncclUniqueId)) return bpe_fail(BPE_ERR_ARG, "bpe native: unique id buffer too small");
+    Rccl &r = id_rccl();
+    if (!r.so) MTRY(load_rccl(r));
+    if (!r.get_unique_id) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
+    ncclUniqueId u;
+    const ncclResult_t e = r.get_unique_id(&u);
+    if (e != ncclSuccess)
+        return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ncclGetUniqueId: ") +
+                                      (r.error_string ? r.error_string(e) : "RCCL error")).c_str());
+    std::memcpy(id, &u, sizeof u);
+    return BPE_OK;
+}
+
+int bpe_rank_rccl_init(bpe_ctx *ctx, const void *id, int rank, int world) {
+    if (!ctx || !id || world < 1 || rank < 0 || rank >= world)
+        return bpe_fail(BPE_ERR_ARG, "bpe native: bad rank communicator arguments");
+    int n_shards = 0;
+    MTRY(bpe_shard_count(ctx, &n_shards));
+    if (n_shards != 1) return bpe_fail(BPE_ERR_STATE, "bpe native: a rank communicator needs a single-device context");
+    rank_rccl_forget(ctx);
+    RankComm rc;
+    MTRY(load_rccl(rc.rccl));
+    if (!rc.rccl.init_rank) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    int dev = 0;
+    MHIP(hipGetDevice(&dev));
+    void *s = nullptr;
+    MTRY(bpe_get_stream(ctx, &s));
+    (void)s;
+    const ncclResult_t e = rc.rccl.init_rank(&rc.comm, world, u, rank);
+    if (e != ncclSuccess)
+        return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ncclCommInitRank: ") +
+                                      (rc.rccl.error_string ? rc.rccl.error_string(e) : "RCCL error")).c_str());
+    rc.rank = rank;
+    rc.world = world;
+    rank_comms()[ctx] = rc;
+    return BPE_OK;
+}
+
+int bpe_rank_loop_rccl(bpe_ctx *ctx, uint64_t *xchg, int64_t xchg_words, uint64_t *tie, int iterations) {
+    auto it = rank_comms().find(ctx);
+    if (it == rank_comms().end())
+        return bpe_fail(BPE_ERR_STATE, "bpe native: no rank communicator (bpe_rank_rccl_init)");
+    if (!xchg || !tie || xchg_words < 1 || iterations < 0)
+        return bpe_fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
+    RankComm &rc = it->second;
+    void *sp = nullptr;
+    MTRY(bpe_get_stream(ctx, &sp));
+    hipStream_t st = (hipStream_t)sp;
+    auto ar = [&](uint64_t *buf, size_t count, ncclRedOp_t op, const char *what) -> int {
+        const ncclResult_t e = rc.rccl.all_reduce(buf, buf, count, ncclUint64, op, rc.comm, st);
+        if (e == ncclSuccess) return BPE_OK;
+        return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ") + what + ": " +
+                                      (rc.rccl.error_string ? rc.rccl.error_string(e) : "RCCL error")).c_str());
+    };
+    for (int i = 0; i < iterations; ++i) {
+        MTRY(ar(xchg, (size_t)xchg_words, ncclSum, "ncclAllReduce(exchange)"));
+        MTRY(bpe_rank_loop_select(ctx));
+        MTRY(ar(tie, BPE_TIE_WORDS, ncclMax, "ncclAllReduce(tie)"));
+        MTRY(bpe_rank_loop_decide(ctx));
+        MTRY(bpe_rank_loop_count(ctx));
+    }
+    return BPE_OK;
+}
+
+int bpe_rank_rccl_destroy(bpe_ctx *ctx) {
+    rank_rccl_forget(ctx);
+    return BPE_OK;
+}
+
+}  // extern "C"

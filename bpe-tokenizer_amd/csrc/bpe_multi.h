@@ -42,5 +42,8 @@ constexpr int BPE_MAX_SHARDS_ONE_DEVICE = 16;
 extern "C" int bpe_sum_shards(unsigned long long *const *bufs, int n, size_t count, int take_max,
                               void *stream);
 
+// (bpe_multi.cpp) a context going away frees its rank communicator (bpe_rank_rccl_init)
+void rank_rccl_forget(bpe_ctx *ctx);
+
 // error reporting shared with bpe_engine.hip
 int bpe_fail(int code, const char *msg);

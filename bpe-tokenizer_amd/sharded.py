@@ -31,6 +31,7 @@ wraps libbpe on a HIP device, and tests/test_sharded_gloo.py drives the same pro
 with gloo.
 """
 import importlib
+import os
 
 import numpy as np
 
@@ -59,11 +60,28 @@ def first_appearance(data, alphabet_size=256):
     return first
 
 
+def hip_runtimes():
+    """The distinct libamdhip64 files mapped into this process.  PyTorch's wheel bundles its own
+    (same soname as /opt/rocm/lib's): imported BEFORE libbpe is loaded, libbpe binds to it and the
+    process has one HIP runtime; loaded after libbpe, the process holds two, and device pointers
+    and streams of one are not valid in the other."""
+    try:
+        with open('/proc/self/maps') as f:
+            return sorted({l.split()[-1] for l in f if 'libamdhip64' in l and '/' in l})
+    except OSError:
+        return []
+
+
 class GpuShard:
     """libbpe engine on one HIP device, exporting/selecting through torch device tensors."""
 
     def __init__(self, engine, device_index):
         import torch
+        rt = hip_runtimes()
+        if len(rt) > 1:
+            raise RuntimeError('libbpe and torch run on different HIP runtimes (%s): import torch '
+                               'before the first libbpe call in a process that shares device '
+                               'buffers between them' % ', '.join(rt))
         self.engine = engine
         self.torch = torch
         self.device = torch.device('cuda', device_index)
@@ -193,6 +211,10 @@ class ShardedTrainer:
         # the incremental mode: the global state lives in every rank's position index (entered at
         # once, the tables' counts exchanged as signed delta rows: bpe_pix.hip.h)
         self.pix = False
+        # RCCL backend: the rank loop's two all-reduces per iteration are issued from C++ on the
+        # engine's stream (bpe_rank_loop_rccl, one call per batch); BPE_RANK_LOOP=python keeps them
+        # as torch.distributed calls (A/B)
+        self._native = None
 
     def set_mode(self, mode):
         """'stream' or 'incremental' (bpe_set_mode) for this rank's engine; every rank alike."""
@@ -327,6 +349,21 @@ class ShardedTrainer:
         self._maintained = True
         self._heavy_streak = 0
 
+    def _native_rccl(self, gloo):
+        """The engine's own RCCL communicator for the rank loop (bpe_rank_rccl_init), made once: rank 0's
+        unique id broadcast over the process group."""
+        if self._native is None:
+            self._native = False
+            if not gloo and os.environ.get('BPE_RANK_LOOP', 'native') != 'python':
+                import torch
+                uid = torch.zeros(128, dtype=torch.uint8, device=self.shard.device)
+                if self.rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(pkg.rccl_unique_id()), dtype=torch.uint8))
+                self.dist.broadcast(uid, src=0)
+                self.engine.rccl_init(bytes(uid.cpu().numpy().tobytes()), self.rank, self.world)
+                self._native = True
+        return self._native
+
     def run_rank_loop(self, n, max_length=0, min_weight=0):
         """n iterations across the ranks with the exchange on the device (bpe_rank_loop_*): no
         host sync inside a batch of LOOP_BATCH iterations.  Returns the merges [(a, b, W)]."""
@@ -352,13 +389,16 @@ class ShardedTrainer:
                 nw = eng.rank_loop_begin(max_length, min_weight, xchg.data_ptr(), tie.data_ptr(),
                                          self.rank, self.world)
                 self._check_same_exchange(nw, gloo)
-                view = xchg[:nw]
-                for _ in range(k):
-                    all_reduce(view, dist.ReduceOp.SUM)
-                    eng.rank_loop_select()
-                    all_reduce(tie, dist.ReduceOp.MAX)
-                    eng.rank_loop_decide()
-                    eng.rank_loop_count()
+                if self._native_rccl(gloo):
+                    eng.rank_loop_rccl(xchg.data_ptr(), nw, tie.data_ptr(), k)
+                else:
+                    view = xchg[:nw]
+                    for _ in range(k):
+                        all_reduce(view, dist.ReduceOp.SUM)
+                        eng.rank_loop_select()
+                        all_reduce(tie, dist.ReduceOp.MAX)
+                        eng.rank_loop_decide()
+                        eng.rank_loop_count()
                 got, reps, status = eng.rank_loop_end()
             if got:
                 # every merge: the ranks' replacement counts sum to W (core.ts:356-359)

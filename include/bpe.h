@@ -239,6 +239,20 @@ int bpe_rank_loop_end(bpe_ctx *ctx, int64_t *out_abwr, int64_t cap, int64_t *n_m
  * bpe_set_global_counts builds the shard's position index and loads the global counts into it
  * (enter at once: a driver need not wait for the cold pairs to outgrow the sketch). */
 int bpe_cold_counts(bpe_ctx *ctx, uint32_t *keys, uint64_t *counts, int64_t cap, int64_t *n);
+
+/* The rank loop's collectives from C++ (one process per GPU): an RCCL
+ * communicator per context, and a batch's iterations enqueued by one call.  Rank 0 makes the id
+ * (bpe_rccl_unique_id, 128 bytes: NCCL_UNIQUE_ID_BYTES), the caller broadcasts it (e.g.
+ * torch.distributed), then every rank calls bpe_rank_rccl_init (collective).  Between
+ * bpe_rank_loop_begin and bpe_rank_loop_end, bpe_rank_loop_rccl(ctx, xchg, xchg_words, tie, k) runs
+ * k iterations of: ncclAllReduce(SUM, xchg[0 .. xchg_words)); bpe_rank_loop_select;
+ * ncclAllReduce(MAX, tie); bpe_rank_loop_decide; bpe_rank_loop_count — all on the context's
+ * stream (no host sync, no cross-stream events).  The RCCL is the one beside the HIP runtime libbpe
+ * runs on.  bpe_destroy frees the communicator; bpe_rank_rccl_destroy frees it earlier. */
+int bpe_rccl_unique_id(void *id, size_t cap);
+int bpe_rank_rccl_init(bpe_ctx *ctx, const void *id, int rank, int world);
+int bpe_rank_loop_rccl(bpe_ctx *ctx, uint64_t *xchg, int64_t xchg_words, uint64_t *tie, int iterations);
+int bpe_rank_rccl_destroy(bpe_ctx *ctx);
 int bpe_set_global_counts(bpe_ctx *ctx, const uint64_t *table, const uint32_t *keys,
                           const uint64_t *counts, int64_t n);
 

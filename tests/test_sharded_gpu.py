@@ -10,9 +10,10 @@ pytestmark = pytest.mark.gpu
 
 
 def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
-           mib=3, corpus='uniform', backend='gloo', engine_mode='stream'):
+           mib=3, corpus='uniform', backend='gloo', engine_mode='stream', rank_loop='native'):
     import importlib
     import sys
+    os.environ['BPE_RANK_LOOP'] = rank_loop
     import torch
     import torch.distributed as dist
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -32,6 +33,7 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
                                               seed=seed, alphabet=A, base=base, dist=dist,
                                               corpus=corpus, rank_loop=True)
         assert tr.exchange and dist.get_backend() == backend
+        native = rank_loop == 'native' and backend == 'nccl'
         if engine_mode != 'stream':
             tr.set_mode(engine_mode)
         tr.engine.stats_enable(True)
@@ -42,6 +44,8 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
         else:
             tr.run(n, max_length, 2)     # the device-resident rank loop
         ids, off = tr.engine.read_corpus()
+        if mode != 'step':
+            assert tr._native == native, (tr._native, native)   # (the path asked for ran)
         q.put((rank, tr.merges, ids.tolist(), off.tolist(), tr.engine.stats()))
     finally:
         dist.destroy_process_group()
@@ -125,10 +129,14 @@ def test_rank_loop_maintained_state_three_ranks_max_length():
 # all-reduce(SUM) of the exchange buffer and all-reduce(MAX) of the tie words go through RCCL on the
 # engine's stream, exactly as on 8 GPUs (core.ts:265-267 shards at samples).
 
-def test_rccl_rank_loop_one_rank_c3_slice():
+@pytest.mark.parametrize('impl', ['native', 'python'])
+def test_rccl_rank_loop_one_rank_c3_slice(impl):
     """64 MiB of the C3 stream (256-char alphabet), 400 merges through the rank loop over a 1-rank
-    RCCL group: the same merges and corpus as the single-context device loop."""
-    st = check(1, mode='loop', n=400, seed=12345, A=256, base=0, mib=64, backend='nccl')
+    RCCL group: the same merges and corpus as the single-context device loop.  native: the
+    all-reduces issued from C++ on the engine's own communicator (bpe_rank_loop_rccl); python:
+    torch.distributed calls per iteration."""
+    st = check(1, mode='loop', n=400, seed=12345, A=256, base=0, mib=64, backend='nccl',
+               rank_loop=impl)
     assert st[0]['tie_passes'] + st[0]['tie_tail'] > 0 or st[0]['iterations'] >= 400, st
 
 

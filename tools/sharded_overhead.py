@@ -3,9 +3,12 @@
 (SURVEY.md §8(e)).  The same C3-stream corpus is merged by:
   device_loop   the engine's single-context mergeUntil (no exchange at all);
   rank_loop     ShardedTrainer(rank_loop=True) over a 1-rank RCCL process group (torch.distributed
-                'nccl' = RCCL): per iteration an RCCL all-reduce(SUM) of the exchange buffer and an
-                all-reduce(MAX) of the tie words on the engine's stream, plus the three rank-loop
-                C-ABI calls (the one-process-per-GPU path bench.py's N>1 leg takes);
+                'nccl' = RCCL), the one-process-per-GPU path bench.py's N>1 leg takes: per iteration
+                an RCCL all-reduce(SUM) of the exchange buffer and an all-reduce(MAX) of the tie
+                words on the engine's stream, issued from C++ by one bpe_rank_loop_rccl call per
+                batch (the engine's own communicator, made from a broadcast unique id);
+  rank_loop_py  the same with the all-reduces as torch.distributed calls from Python and the
+                three rank-loop C-ABI calls per iteration (BPE_RANK_LOOP=python; round 4's path);
   multi_rccl    bpe_create_multi(devices=[0], reduce='rccl'): ncclCommInitAll over one device and
                 grouped ncclAllReduce calls from C++ (the drop-in's BPE_DEVICES path);
   protocol      ShardedTrainer.step: the host protocol of every iteration (table all-reduce,
@@ -53,15 +56,19 @@ def main():
     out['device_loop_ms_per_merge'] = t / n * 1e3
     e.close()
 
-    tr = sharded.ShardedTrainer.synthetic(device=0, rank=0, world=1, bytes_per_rank=mib << 20,
-                                          sample_bytes=1 << 20, seed=12345, alphabet=256, base=0,
-                                          dist=dist, rank_loop=True)
-    assert tr.exchange
-    tr.run(warm, 0, 2)
-    got, t = timed(lambda: tr.run(n, 0, 2))
-    assert [tuple(m) for m in got] == want, 'rank loop and device loop disagree'
-    out['rank_loop_ms_per_merge'] = t / n * 1e3
-    tr.engine.close()
+    for key, how in (('rank_loop', 'native'), ('rank_loop_py', 'python')):
+        os.environ['BPE_RANK_LOOP'] = how
+        tr = sharded.ShardedTrainer.synthetic(device=0, rank=0, world=1, bytes_per_rank=mib << 20,
+                                              sample_bytes=1 << 20, seed=12345, alphabet=256, base=0,
+                                              dist=dist, rank_loop=True)
+        assert tr.exchange
+        tr.run(warm, 0, 2)
+        assert tr._native == (how == 'native')
+        got, t = timed(lambda: tr.run(n, 0, 2))
+        assert [tuple(m) for m in got] == want, '%s and device loop disagree' % key
+        out[key + '_ms_per_merge'] = t / n * 1e3
+        tr.engine.close()
+    os.environ.pop('BPE_RANK_LOOP')
 
     m = pkg.Engine(devices=[0], reduce='rccl')
     m.add_latin1(data, sample_bytes=1 << 20)
@@ -82,6 +89,7 @@ def main():
     out['protocol_ms_per_merge'] = t / k * 1e3
     out['protocol_iterations'] = k
     out['rank_loop_overhead_ms'] = out['rank_loop_ms_per_merge'] - out['device_loop_ms_per_merge']
+    out['rank_loop_py_overhead_ms'] = out['rank_loop_py_ms_per_merge'] - out['device_loop_ms_per_merge']
     out['multi_rccl_overhead_ms'] = out['multi_rccl_ms_per_merge'] - out['device_loop_ms_per_merge']
     print(json.dumps(out), flush=True)
     dist.destroy_process_group()
