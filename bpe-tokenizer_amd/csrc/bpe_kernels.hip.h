@@ -568,6 +568,7 @@ constexpr int IH_BASE = 4 * INCR_RLIM / 2;             // dword index of the has
 static_assert(IH_BASE + 2 * IH_SLOTS == HIST_WORDS, "MODE_INCR LDS layout");
 
 // counters of a row in use: other tokens below the vocabulary size after the merge (mc + 1)
+static_assert(INCR_RLIM % 2 == 0, "a row's counters pair up in dwords");
 __device__ __forceinline__ int incr_vlim(int32_t mc) {
     const int v = (mc + 2) & ~1;
     return v < INCR_RLIM ? v : INCR_RLIM;
@@ -879,6 +880,13 @@ __device__ __forceinline__ unsigned long long lanes_upto(int n, int e) {
     return m >= 64 ? ~0ull : m <= 0 ? 0ull : ((1ull << m) - 1ull);
 }
 
+// Lanes whose t is one of ma, mb, mc: three compares straight into lane masks, OR'ed on the scalar
+// unit.  (A ballot of the OR of the three compares made the compiler materialise the OR as a 0/1
+// vector value and compare it again: two more VALU per token.)
+__device__ __forceinline__ unsigned long long member3(int32_t t, int32_t ma, int32_t mb, int32_t mc) {
+    return __ballot(t == ma) | __ballot(t == mb) | __ballot(t == mc);
+}
+
 // Wave-uniform facts of a freshly loaded chunk, from slot 255 (a live token, or the tail tag).
 __device__ __forceinline__ void finish_load(Chunk &c) {
     c.first = bcast(c.t[0], 0);
@@ -1001,11 +1009,9 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
                                               int32_t x3, int32_t r3, const int32_t (&x)[4],
                                               const int32_t (&y)[4]) {
     const int32_t ma = k.ma, mb = k.mb, mc = k.mc;
-    const unsigned long long M0 = __ballot((t0 == ma) | (t0 == mb) | (t0 == mc)),
-                             M1 = __ballot((t1 == ma) | (t1 == mb) | (t1 == mc)),
-                             M2 = __ballot((t2 == ma) | (t2 == mb) | (t2 == mc)),
-                             M3 = __ballot((x3 == ma) | (x3 == mb) | (x3 == mc)),
-                             M4 = __ballot((r3 == ma) | (r3 == mb) | (r3 == mc));
+    const unsigned long long M0 = member3(t0, ma, mb, mc), M1 = member3(t1, ma, mb, mc),
+                             M2 = member3(t2, ma, mb, mc), M3 = member3(x3, ma, mb, mc),
+                             M4 = member3(r3, ma, mb, mc);
     const unsigned long long W0 = M0 | M1, W1 = M1 | M2, W2 = M2 | M3, W3 = M3 | M4;
     if ((W0 | W1 | W2 | W3) == 0ull) return;
     const unsigned long long Wm[4] = {W0, W1, W2, W3};
@@ -1094,38 +1100,40 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             // only the pairs with a side in {ma, mb, mc}: membership masks per slot (compares into
             // lane masks, combined on the scalar unit), the LDS only for chunks that hold one
             const int32_t ma = k.ma, mb = k.mb, mc = k.mc;
-            const unsigned long long M0 = __ballot((t0 == ma) | (t0 == mb) | (t0 == mc)),
-                                     M1 = __ballot((t1 == ma) | (t1 == mb) | (t1 == mc)),
-                                     M2 = __ballot((t2 == ma) | (t2 == mb) | (t2 == mc)),
-                                     M3 = __ballot((x3 == ma) | (x3 == mb) | (x3 == mc)),
-                                     M4 = __ballot((r3 == ma) | (r3 == mb) | (r3 == mc));
+            const unsigned long long M0 = member3(t0, ma, mb, mc), M1 = member3(t1, ma, mb, mc),
+                                     M2 = member3(t2, ma, mb, mc), M3 = member3(x3, ma, mb, mc),
+                                     M4 = member3(r3, ma, mb, mc);
             const unsigned long long Wm[4] = {M0 | M1, M1 | M2, M2 | M3, M3 | M4};
             if ((Wm[0] | Wm[1] | Wm[2] | Wm[3]) != 0ull) {
                 // branch-free on the common route (a row counter): every lane adds, 0 when its
                 // pair is not touched (to a counter of its own: no two lanes on one address);
                 // pairs of mc, and other tokens past the rows, take the hash (rare)
-                uint32_t dw[4], sh[4];
                 unsigned long long hsh = 0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int32_t xx = x[e], yy = y[e];
-                    const bool act = lane_in(Wm[e]) & ((xx | yy) >= 0);
+                    const bool act = lane_in(Wm[e]);
                     const bool xa = xx == ma, xb = xx == mb, ya = yy == ma, yb = yy == mb;
                     const int row = xa ? 0 : xb ? 1 : ya ? 2 : 3;
                     const int idx = (xa | xb) ? yy : xx;
-                    const bool inrow = act & (xa | xb | ya | yb) & (idx < INCR_RLIM);
-                    const uint32_t cc = (uint32_t)(row * INCR_RLIM + idx);
-                    sh[e] = (cc & 1u) << 4;
-                    dw[e] = inrow ? (cc >> 1) : (uint32_t)lane;
+                    // (an unsigned bound: a pair with a negative side (SEP, dead) never has both a
+                    // member side and idx >= 0, so it never lands in a row; the rare branch below
+                    // drops such pairs from the hash)
+                    const bool inrow = act & (xa | xb | ya | yb) & ((uint32_t)idx < (uint32_t)INCR_RLIM);
+                    // counter cc = row * INCR_RLIM + idx: byte address of its dword (cc >> 1) * 4,
+                    // made as (2 cc) & ~3; its half (cc & 1) = (idx & 1) (INCR_RLIM is even)
+                    const uint32_t cc2 = (uint32_t)(row * (2 * INCR_RLIM)) + 2u * (uint32_t)idx;
+                    const uint32_t ba = inrow ? (cc2 & ~3u) : 4u * (uint32_t)lane;
                     // (the returns wait for the round's overflow screen; a lane's own dword
                     // `lane` is a row 0 counter, so its return can only raise a false alarm)
-                    df.o[e] = atomicAdd(&k.hist[dw[e]], (uint32_t)inrow << sh[e]);
+                    df.o[e] = atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + ba),
+                                        (uint32_t)inrow << (((uint32_t)idx & 1u) << 4));
                     hsh |= (unsigned long long)(act & !inrow) << e;
                 }
                 if (__ballot(hsh != 0ull) != 0ull) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if ((hsh >> e) & 1ull)
+                        if (((hsh >> e) & 1ull) && (x[e] | y[e]) >= 0)
                             incr_hash_add(k, ((uint32_t)x[e] << 16) | (uint32_t)y[e], 1u);
                 }
             }
