@@ -227,7 +227,14 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
     int n = (int)(off[text + 1] - base);
     const int tid = threadIdx.x;
 
-    for (int i = tid; i < n; i += WG) tok[i] = (uint16_t)in[base + i];
+    bool bad = false;
+    for (int i = tid; i < n; i += WG) {
+        const int32_t v = in[base + i];
+        bad |= (uint32_t)v >= (uint32_t)BPE_MAX_VOCAB;
+        tok[i] = (uint16_t)v;
+    }
+    // (an id out of range: counted in steps_total[7], the call fails; the text's output is void)
+    if (bad) atomicAdd(steps_total + 7, 1ull);
     __syncthreads();
     uint32_t lmin = NO_RANK;
     for (int i = tid; i < n; i += WG) {
@@ -350,7 +357,7 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
     for (int i = tid; i < n; i += WG) out[base + i] = tok[i];
     if (tid == 0) {
         out_len[text] = n;
-        if (steps_total && steps) atomicAdd(steps_total, (unsigned long long)steps);
+        if (steps) atomicAdd(steps_total, (unsigned long long)steps);
 #if BPE_ENC_TIMING
         for (int q = 0; q < 6; ++q) atomicAdd(steps_total + 1 + q, (unsigned long long)tk[q]);
 #endif
@@ -365,6 +372,37 @@ constexpr int SHAPE_K[N_SHAPES] = {3, 5, 9, 5, 9, 17, 9, 17};
 
 constexpr int shape_cap(int i) { return SHAPE_WG[i] * (SHAPE_K[i] - 1); }
 constexpr size_t shape_lds(int i) { return (size_t)shape_cap(i) * 6; }
+// The packed output of a call on the device: exclusive scan of the encoded lengths (one workgroup,
+// 1024 lengths per round) and a gather of every text from its input offset to its output offset
+// (one wave per text), so the host copies the result once, with no per-text loop.
+__global__ void __launch_bounds__(1024)
+k_scan_lens(const int32_t *__restrict__ len, int64_t n, int64_t *__restrict__ ooff) {
+    __shared__ int scn[16];
+    long long carry = 0;
+    for (int64_t b = 0; b < n; b += 1024) {
+        const int64_t i = b + threadIdx.x;
+        const int v = i < n ? len[i] : 0;
+        int total = 0;
+        const int before = block_scan<1024>(v, scn, total);
+        if (i < n) ooff[i] = carry + before;
+        carry += total;
+        __syncthreads();   // (scn is reused next round)
+    }
+    if (threadIdx.x == 0) ooff[n] = carry;
+}
+
+__global__ void __launch_bounds__(256)
+k_gather(const int32_t *__restrict__ src, const int64_t *__restrict__ in_off,
+         const int32_t *__restrict__ len, const int64_t *__restrict__ ooff, int64_t n,
+         int32_t *__restrict__ dst) {
+    const int64_t text = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (text >= n) return;
+    const int32_t *s = src + in_off[text];
+    int32_t *d = dst + ooff[text];
+    const int l = len[text];
+    for (int i = threadIdx.x & 63; i < l; i += 64) d[i] = s[i];
+}
+
 // shorter texts take the HBM table even in the few-texts form (the LDS copy costs more than its
 // faster probes save over their few steps)
 constexpr int LDS_TAB_MIN_TOKENS = 128;
@@ -686,24 +724,15 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         if (off[k + 1] < off[k]) return bpe_fail(BPE_ERR_ARG, "bpe native: text offsets must not decrease");
     const int64_t base = off[0], total = off[n_texts] - base;
     if (total && (!ids || !ids_out)) return bpe_fail(BPE_ERR_ARG, "bpe native: null id buffer");
-    for (int64_t i = 0; i < total; ++i)
-        if (ids[base + i] < 0 || ids[base + i] >= BPE_MAX_VOCAB)
-            return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
     ENC_TRY(hipSetDevice(E->device));
     E->st.calls++;
     E->st.tokens_in += total;
-    std::vector<int64_t> len((size_t)n_texts);
-    std::vector<int32_t> out((size_t)std::max<int64_t>(total, 1));
-    const int64_t m = (int64_t)E->c_of.size();
     // launch shape of every text (the smallest that holds it), or the apply-pass route
     std::vector<int32_t> lists[N_SHAPES];
     std::vector<int64_t> replay;
     for (int64_t k = 0; k < n_texts; ++k) {
         const int64_t l = off[k + 1] - off[k];
-        if (m == 0 || l < 2) {
-            std::memcpy(out.data() + (off[k] - base), ids + off[k], (size_t)l * 4);
-            len[k] = l;
-        } else if (!E->greedy_ok || l > CAP_MAX) {
+        if (!E->greedy_ok || l > CAP_MAX) {
             replay.push_back(k);
         } else {
             int i = 0;
@@ -714,68 +743,98 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     int64_t n_rank = 0;
     for (auto &L : lists) n_rank += (int64_t)L.size();
     int rc;
-    if (n_rank) {
-        if ((rc = upload_table(E))) return rc;
-        // staging: [ids | off (relative) | which lists] up, [out | len] down
-        const size_t b_ids = align16((size_t)total * 4), b_off = align16((size_t)(n_texts + 1) * 8);
-        const size_t b_which = align16((size_t)n_rank * 4), b_len = align16((size_t)n_texts * 4);
-        const size_t up = b_ids + b_off + b_which, bytes = up + b_ids + b_len;
-        if ((rc = grow_stage(E, bytes))) return rc;
-        char *h = E->h_buf, *d = E->d_buf;
-        std::memcpy(h, ids + base, (size_t)total * 4);
-        int64_t *h_off = reinterpret_cast<int64_t *>(h + b_ids);
-        for (int64_t k = 0; k <= n_texts; ++k) h_off[k] = off[k] - base;
-        int32_t *h_which = reinterpret_cast<int32_t *>(h + b_ids + b_off);
-        size_t at = 0;
-        for (auto &L : lists) {
-            std::memcpy(h_which + at, L.data(), L.size() * 4);
-            at += L.size();
-        }
-        ENC_TRY(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, E->stream));
-        const int32_t *d_ids = reinterpret_cast<const int32_t *>(d);
-        const int64_t *d_off = reinterpret_cast<const int64_t *>(d + b_ids);
-        const int32_t *d_which = reinterpret_cast<const int32_t *>(d + b_ids + b_off);
-        int32_t *d_out = reinterpret_cast<int32_t *>(d + up);
-        int32_t *d_len = reinterpret_cast<int32_t *>(d + up + b_ids);
-        // few texts: each has a CU to itself, and the table is read from LDS (when it fits)
-        const size_t tab = (size_t)E->lt.words * 4;
-        const bool few = (size_t)n_rank <= LATENCY_TEXTS;
-        ENC_TRY(hipEventRecord(E->ev0, E->stream));
-        at = 0;
-        for (int i = 0; i < N_SHAPES; ++i) {
-            if (lists[i].empty()) continue;
-            const bool tab_lds = few && shape_cap(i) > LDS_TAB_MIN_TOKENS && shape_lds(i) + tab <= LDS_BYTES;
-            launch_shape(i, E, (unsigned)lists[i].size(), tab_lds, d_ids, d_off, d_which + at, d_out, d_len);
-            at += lists[i].size();
-        }
+    if (!replay.empty()) {
+        // (only the replay's host route checks ids on the host; the kernels count bad ids)
+        for (int64_t k : replay)
+            for (int64_t i = off[k]; i < off[k + 1]; ++i)
+                if (ids[i] < 0 || ids[i] >= BPE_MAX_VOCAB)
+                    return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+    }
+    if ((rc = upload_table(E))) return rc;
+    // device: [ids (then the packed output) | off (relative) | which | out | len | out offsets];
+    // pinned: [off | which] up, the error count down
+    const size_t b_ids = align16((size_t)std::max<int64_t>(total, 1) * 4);
+    const size_t b_off = align16((size_t)(n_texts + 1) * 8);
+    const size_t b_which = align16((size_t)std::max<int64_t>(n_rank, 1) * 4);
+    const size_t b_len = align16((size_t)n_texts * 4);
+    const size_t bytes = b_ids + b_off + b_which + b_ids + b_len + b_off;
+    if ((rc = grow_stage(E, bytes))) return rc;
+    char *h = E->h_buf, *d = E->d_buf;
+    int32_t *d_ids = reinterpret_cast<int32_t *>(d);
+    int64_t *d_off = reinterpret_cast<int64_t *>(d + b_ids);
+    int32_t *d_which = reinterpret_cast<int32_t *>(d + b_ids + b_off);
+    int32_t *d_out = reinterpret_cast<int32_t *>(d + b_ids + b_off + b_which);
+    int32_t *d_len = reinterpret_cast<int32_t *>(d + 2 * b_ids + b_off + b_which);
+    int64_t *d_ooff = reinterpret_cast<int64_t *>(d + 2 * b_ids + b_off + b_which + b_len);
+    int64_t *h_off = reinterpret_cast<int64_t *>(h);
+    int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off);
+    for (int64_t k = 0; k <= n_texts; ++k) h_off[k] = off[k] - base;
+    size_t at = 0;
+    for (auto &L : lists) {
+        std::memcpy(h_which + at, L.data(), L.size() * 4);
+        at += L.size();
+    }
+    // the ids straight from the caller's buffer (no host staging copy)
+    if (total) ENC_TRY(hipMemcpyAsync(d_ids, ids + base, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
+    ENC_TRY(hipMemcpyAsync(d_off, h_off, (size_t)(n_texts + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    if (n_rank) ENC_TRY(hipMemcpyAsync(d_which, h_which, (size_t)n_rank * 4, hipMemcpyHostToDevice, E->stream));
+    // replay texts keep length 0 on the device; they are written on the host below
+    if (!replay.empty()) ENC_TRY(hipMemsetAsync(d_len, 0, (size_t)n_texts * 4, E->stream));
+    ENC_TRY(hipMemsetAsync(E->d_steps + 7, 0, 8, E->stream));
+    // few texts: each has a CU to itself, and the table is read from LDS (when it fits)
+    const size_t tab = (size_t)E->lt.words * 4;
+    const bool few = (size_t)n_rank <= LATENCY_TEXTS;
+    ENC_TRY(hipEventRecord(E->ev0, E->stream));
+    at = 0;
+    for (int i = 0; i < N_SHAPES; ++i) {
+        if (lists[i].empty()) continue;
+        const bool tab_lds = few && shape_cap(i) > LDS_TAB_MIN_TOKENS && shape_lds(i) + tab <= LDS_BYTES;
+        launch_shape(i, E, (unsigned)lists[i].size(), tab_lds, d_ids, d_off, d_which + at, d_out, d_len);
+        at += lists[i].size();
+    }
+    ENC_TRY(hipGetLastError());
+    ENC_TRY(hipEventRecord(E->ev1, E->stream));
+    if (replay.empty()) {
+        // packed on the device, into the ids buffer (read by the kernels above, free now)
+        k_scan_lens<<<1, 1024, 0, E->stream>>>(d_len, n_texts, d_ooff);
+        k_gather<<<(unsigned)((n_texts + 3) / 4), 256, 0, E->stream>>>(d_out, d_off, d_len, d_ooff,
+                                                                        n_texts, d_ids);
         ENC_TRY(hipGetLastError());
-        ENC_TRY(hipEventRecord(E->ev1, E->stream));
-        ENC_TRY(hipMemcpyAsync(h + up, d + up, b_ids + b_len, hipMemcpyDeviceToHost, E->stream));
-        // the long texts replay on the scratch engine's own stream meanwhile
-        if ((rc = encode_replay(E, ids, off, replay, out.data(), len.data()))) return rc;
+        ENC_TRY(hipMemcpyAsync(out_off, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
+        unsigned long long *h_err = reinterpret_cast<unsigned long long *>(h + b_off + b_which);
+        ENC_TRY(hipMemcpyAsync(h_err, E->d_steps + 7, 8, hipMemcpyDeviceToHost, E->stream));
+        // (the caller's buffer holds off[n] - off[0] ids: a text never grows)
+        if (total) ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
         ENC_TRY(hipStreamSynchronize(E->stream));
-        float ms = 0;
-        ENC_TRY(hipEventElapsedTime(&ms, E->ev0, E->ev1));
-        E->st.kernel_ms += ms;
-        E->st.texts_rank += n_rank;
-        const int32_t *h_out = reinterpret_cast<const int32_t *>(h + up);
-        const int32_t *h_len = reinterpret_cast<const int32_t *>(h + up + b_ids);
+        if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+    } else {
+        // host assembly: the kernels' texts come back at their input offsets, the replayed ones
+        // from the scratch engine (into the same host buffer: after the copies have landed)
+        std::vector<int64_t> len((size_t)n_texts, 0);
+        std::vector<int32_t> out((size_t)std::max<int64_t>(total, 1));
+        std::vector<int32_t> lens((size_t)n_texts);
+        unsigned long long err = 0;
+        ENC_TRY(hipMemcpyAsync(out.data(), d_out, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
+        ENC_TRY(hipMemcpyAsync(lens.data(), d_len, (size_t)n_texts * 4, hipMemcpyDeviceToHost, E->stream));
+        ENC_TRY(hipMemcpyAsync(&err, E->d_steps + 7, 8, hipMemcpyDeviceToHost, E->stream));
+        ENC_TRY(hipStreamSynchronize(E->stream));
+        if (err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+        if ((rc = encode_replay(E, ids, off, replay, out.data(), len.data()))) return rc;
         for (auto &L : lists)
-            for (int32_t k : L) {
-                len[k] = h_len[k];
-                std::memcpy(out.data() + (off[k] - base), h_out + (off[k] - base), (size_t)h_len[k] * 4);
-            }
-    } else if ((rc = encode_replay(E, ids, off, replay, out.data(), len.data()))) {
-        return rc;
+            for (int32_t k : L) len[k] = lens[k];
+        int64_t o = 0;
+        out_off[0] = 0;
+        for (int64_t k = 0; k < n_texts; ++k) {
+            if (len[k]) std::memcpy(ids_out + o, out.data() + (off[k] - base), (size_t)len[k] * 4);
+            o += len[k];
+            out_off[k + 1] = o;
+        }
     }
-    int64_t o = 0;
-    out_off[0] = 0;
-    for (int64_t k = 0; k < n_texts; ++k) {
-        if (len[k]) std::memcpy(ids_out + o, out.data() + (off[k] - base), (size_t)len[k] * 4);
-        o += len[k];
-        out_off[k + 1] = o;
-    }
-    E->st.tokens_out += o;
+    float ms = 0;
+    ENC_TRY(hipEventElapsedTime(&ms, E->ev0, E->ev1));
+    E->st.kernel_ms += ms;
+    E->st.texts_rank += n_rank;
+    E->st.tokens_out += out_off[n_texts];
     return BPE_OK;
 }
 

@@ -106,7 +106,7 @@ def test_random_texts_every_launch_shape(seed):
     st = enc.stats()
     long = sum(1 for t in texts if len(t) > cap)
     assert st['texts_replay'] == long
-    assert st['texts_rank'] == sum(1 for t in texts if 2 <= len(t) <= cap)
+    assert st['texts_rank'] == sum(1 for t in texts if len(t) <= cap)
     assert st['steps'] > 0
     enc.close()
 
@@ -195,6 +195,12 @@ def test_bad_ids_are_refused():
     enc = pkg.Encoder(0, [(0, 1, 2)])
     with pytest.raises(pkg.BpeError, match='out of range'):
         enc.encode([np.asarray([0, pkg.MAX_VOCAB], np.int32)])
+    with pytest.raises(pkg.BpeError, match='out of range'):   # (checked on the device)
+        enc.encode([np.asarray([0, 1, 0], np.int32), np.asarray([3, -1, 2, 0], np.int32)])
+    with pytest.raises(pkg.BpeError, match='out of range'):   # (the replay route: on the host)
+        enc.encode([np.asarray([0, 1] * 9000 + [-5], np.int32)])
+    # the encoder is still usable after a refused call
+    assert [t.tolist() for t in enc.encode([np.asarray([0, 1, 0, 1], np.int32)])] == [[2, 2]]
     with pytest.raises(pkg.BpeError, match='out of range'):
         enc.add_merges([(0, -1, 3)])
     enc.close()
