@@ -514,6 +514,9 @@ int upload_table(bpe_encoder *E) {
     return BPE_OK;
 }
 
+// calls of at most this many id bytes go through the pinned staging buffer both ways
+constexpr size_t SMALL_CALL_BYTES = 4u << 20;
+
 // texts per call up to which each gets a CU of its own, so the LDS copy of the table pays
 constexpr size_t LATENCY_TEXTS = 256;
 
@@ -757,8 +760,8 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     const size_t b_off = align16((size_t)(n_texts + 1) * 8);
     const size_t b_which = align16((size_t)std::max<int64_t>(n_rank, 1) * 4);
     const size_t b_len = align16((size_t)n_texts * 4);
-    const size_t bytes = b_ids + b_off + b_which + b_ids + b_len + b_off;
-    if ((rc = grow_stage(E, bytes))) return rc;
+    const size_t bytes = b_ids + b_off + b_which + b_ids + b_len + b_off;   // (the host side needs
+    if ((rc = grow_stage(E, bytes))) return rc;                              //  off, which, 16, ids, ooff)
     char *h = E->h_buf, *d = E->d_buf;
     int32_t *d_ids = reinterpret_cast<int32_t *>(d);
     int64_t *d_off = reinterpret_cast<int64_t *>(d + b_ids);
@@ -774,8 +777,17 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         std::memcpy(h_which + at, L.data(), L.size() * 4);
         at += L.size();
     }
-    // the ids straight from the caller's buffer (no host staging copy)
-    if (total) ENC_TRY(hipMemcpyAsync(d_ids, ids + base, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
+    // Large calls copy the ids straight from the caller's buffer (no host staging pass); small ones
+    // through the pinned buffer (a pageable copy costs tens of microseconds of fixed overhead)
+    const bool small = (size_t)total * 4 <= SMALL_CALL_BYTES;
+    int32_t *h_ids = reinterpret_cast<int32_t *>(h + b_off + b_which + 16);
+    int64_t *h_ooff = reinterpret_cast<int64_t *>(h + b_off + b_which + 16 + b_ids);
+    if (total && small) {
+        std::memcpy(h_ids, ids + base, (size_t)total * 4);
+        ENC_TRY(hipMemcpyAsync(d_ids, h_ids, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
+    } else if (total) {
+        ENC_TRY(hipMemcpyAsync(d_ids, ids + base, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
+    }
     ENC_TRY(hipMemcpyAsync(d_off, h_off, (size_t)(n_texts + 1) * 8, hipMemcpyHostToDevice, E->stream));
     if (n_rank) ENC_TRY(hipMemcpyAsync(d_which, h_which, (size_t)n_rank * 4, hipMemcpyHostToDevice, E->stream));
     // replay texts keep length 0 on the device; they are written on the host below
@@ -800,13 +812,22 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         k_gather<<<(unsigned)((n_texts + 3) / 4), 256, 0, E->stream>>>(d_out, d_off, d_len, d_ooff,
                                                                         n_texts, d_ids);
         ENC_TRY(hipGetLastError());
-        ENC_TRY(hipMemcpyAsync(out_off, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
         unsigned long long *h_err = reinterpret_cast<unsigned long long *>(h + b_off + b_which);
         ENC_TRY(hipMemcpyAsync(h_err, E->d_steps + 7, 8, hipMemcpyDeviceToHost, E->stream));
-        // (the caller's buffer holds off[n] - off[0] ids: a text never grows)
-        if (total) ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
-        ENC_TRY(hipStreamSynchronize(E->stream));
-        if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+        if (small) {
+            ENC_TRY(hipMemcpyAsync(h_ooff, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
+            if (total) ENC_TRY(hipMemcpyAsync(h_ids, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
+            ENC_TRY(hipStreamSynchronize(E->stream));
+            if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+            std::memcpy(out_off, h_ooff, (size_t)(n_texts + 1) * 8);
+            if (h_ooff[n_texts]) std::memcpy(ids_out, h_ids, (size_t)h_ooff[n_texts] * 4);
+        } else {
+            ENC_TRY(hipMemcpyAsync(out_off, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
+            // (the caller's buffer holds off[n] - off[0] ids: a text never grows)
+            if (total) ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
+            ENC_TRY(hipStreamSynchronize(E->stream));
+            if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+        }
     } else {
         // host assembly: the kernels' texts come back at their input offsets, the replayed ones
         // from the scratch engine (into the same host buffer: after the copies have landed)
