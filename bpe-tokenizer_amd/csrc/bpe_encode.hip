@@ -198,7 +198,8 @@ template <int WG, int KMAX, bool TAB_LDS>
 __global__ void __launch_bounds__(WG)
 k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
          const int32_t *__restrict__ which, int32_t *__restrict__ out, int32_t *__restrict__ out_len,
-         RankTab t, LdsTab lt, unsigned long long *__restrict__ steps_total) {
+         RankTab t, LdsTab lt, unsigned long long *__restrict__ steps_total,
+         unsigned long long *__restrict__ err) {
     static_assert(KMAX & 1, "odd segment lengths");
     constexpr int CAP = WG * (KMAX - 1);
     constexpr int H = KMAX + 2;   // segment + look-ahead
@@ -233,8 +234,8 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
         bad |= (uint32_t)v >= (uint32_t)BPE_MAX_VOCAB;
         tok[i] = (uint16_t)v;
     }
-    // (an id out of range: counted in steps_total[7], the call fails; the text's output is void)
-    if (bad) atomicAdd(steps_total + 7, 1ull);
+    // (an id out of range: counted in *err, the call fails; the text's output is void)
+    if (bad) atomicAdd(err, 1ull);
     __syncthreads();
     uint32_t lmin = NO_RANK;
     for (int i = tid; i < n; i += WG) {
@@ -375,8 +376,10 @@ constexpr size_t shape_lds(int i) { return (size_t)shape_cap(i) * 6; }
 // The packed output of a call on the device: exclusive scan of the encoded lengths (one workgroup,
 // 1024 lengths per round) and a gather of every text from its input offset to its output offset
 // (one wave per text), so the host copies the result once, with no per-text loop.
+// ooff[n + 1] receives the call's bad-id count (*err), so that one copy brings both back.
 __global__ void __launch_bounds__(1024)
-k_scan_lens(const int32_t *__restrict__ len, int64_t n, int64_t *__restrict__ ooff) {
+k_scan_lens(const int32_t *__restrict__ len, int64_t n, int64_t *__restrict__ ooff,
+            const unsigned long long *__restrict__ err) {
     __shared__ int scn[16];
     long long carry = 0;
     for (int64_t b = 0; b < n; b += 1024) {
@@ -388,7 +391,38 @@ k_scan_lens(const int32_t *__restrict__ len, int64_t n, int64_t *__restrict__ oo
         carry += total;
         __syncthreads();   // (scn is reused next round)
     }
-    if (threadIdx.x == 0) ooff[n] = carry;
+    if (threadIdx.x == 0) {
+        ooff[n] = carry;
+        ooff[n + 1] = (long long)*err;
+    }
+}
+
+// Both in one workgroup, for a call of at most 1024 texts (the one-text-per-call shape): the scan,
+// then one wave per text.
+__global__ void __launch_bounds__(1024)
+k_pack_small(const int32_t *__restrict__ src, const int64_t *__restrict__ in_off,
+             const int32_t *__restrict__ len, int n, int64_t *__restrict__ ooff,
+             const unsigned long long *__restrict__ err, int32_t *__restrict__ dst) {
+    __shared__ int scn[16];
+    __shared__ int start[1025];
+    const int v = (int)threadIdx.x < n ? len[threadIdx.x] : 0;
+    int total = 0;
+    const int before = block_scan<1024>(v, scn, total);
+    if ((int)threadIdx.x < n) {
+        start[threadIdx.x] = before;
+        ooff[threadIdx.x] = before;
+    }
+    if (threadIdx.x == 0) {
+        ooff[n] = total;
+        ooff[n + 1] = (long long)*err;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x >> 6; t < n; t += 16) {
+        const int32_t *s = src + in_off[t];
+        int32_t *d = dst + start[t];
+        const int l = len[t];
+        for (int i = threadIdx.x & 63; i < l; i += 64) d[i] = s[i];
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -539,22 +573,24 @@ hipError_t set_lds_attrs() {
 
 template <int I>
 void launch_one(bpe_encoder *E, unsigned n, bool tab_lds, const int32_t *ids, const int64_t *off,
-                const int32_t *which, int32_t *out, int32_t *len) {
+                const int32_t *which, int32_t *out, int32_t *len, unsigned long long *err) {
     constexpr int WG = SHAPE_WG[I], KM = SHAPE_K[I];
     const RankTab t{E->d_slots, (1u << E->bits) - 1, 32 - E->bits};
     if (tab_lds)
         k_encode<WG, KM, true><<<n, WG, shape_lds(I) + (size_t)E->lt.words * 4, E->stream>>>(
-            ids, off, which, out, len, t, E->lt, E->d_steps);
+            ids, off, which, out, len, t, E->lt, E->d_steps, err);
     else
         k_encode<WG, KM, false><<<n, WG, shape_lds(I), E->stream>>>(ids, off, which, out, len, t,
-                                                                    E->lt, E->d_steps);
+                                                                    E->lt, E->d_steps, err);
 }
 
 template <int I = 0>
 void launch_shape(int i, bpe_encoder *E, unsigned n, bool tab_lds, const int32_t *ids,
-                  const int64_t *off, const int32_t *which, int32_t *out, int32_t *len) {
-    if (i == I) return launch_one<I>(E, n, tab_lds, ids, off, which, out, len);
-    if constexpr (I + 1 < N_SHAPES) launch_shape<I + 1>(i, E, n, tab_lds, ids, off, which, out, len);
+                  const int64_t *off, const int32_t *which, int32_t *out, int32_t *len,
+                  unsigned long long *err) {
+    if (i == I) return launch_one<I>(E, n, tab_lds, ids, off, which, out, len, err);
+    if constexpr (I + 1 < N_SHAPES)
+        launch_shape<I + 1>(i, E, n, tab_lds, ids, off, which, out, len, err);
 }
 
 int grow_stage(bpe_encoder *E, size_t bytes) {
@@ -754,24 +790,30 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
                     return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
     }
     if ((rc = upload_table(E))) return rc;
-    // device: [ids (then the packed output) | off (relative) | which | out | len | out offsets];
-    // pinned: [off | which] up, the error count down
+    // device: [ooff (n+2) | ids, then the packed output | off (n+2) | which | out | len]; the pinned
+    // host buffer mirrors [ooff | ids | off | which], so a small call moves [ids | off | which] up in
+    // one copy and [ooff | packed ids] down in one.  off[n+1] = 0 is the bad-id counter (zeroed by
+    // the upload), which the pack kernel copies to ooff[n+1].
     const size_t b_ids = align16((size_t)std::max<int64_t>(total, 1) * 4);
-    const size_t b_off = align16((size_t)(n_texts + 1) * 8);
+    const size_t b_off = align16((size_t)(n_texts + 2) * 8);
     const size_t b_which = align16((size_t)std::max<int64_t>(n_rank, 1) * 4);
     const size_t b_len = align16((size_t)n_texts * 4);
-    const size_t bytes = b_ids + b_off + b_which + b_ids + b_len + b_off;   // (the host side needs
-    if ((rc = grow_stage(E, bytes))) return rc;                              //  off, which, 16, ids, ooff)
+    const size_t bytes = b_off + b_ids + b_off + b_which + b_ids + b_len;
+    if ((rc = grow_stage(E, bytes))) return rc;
     char *h = E->h_buf, *d = E->d_buf;
-    int32_t *d_ids = reinterpret_cast<int32_t *>(d);
-    int64_t *d_off = reinterpret_cast<int64_t *>(d + b_ids);
-    int32_t *d_which = reinterpret_cast<int32_t *>(d + b_ids + b_off);
-    int32_t *d_out = reinterpret_cast<int32_t *>(d + b_ids + b_off + b_which);
-    int32_t *d_len = reinterpret_cast<int32_t *>(d + 2 * b_ids + b_off + b_which);
-    int64_t *d_ooff = reinterpret_cast<int64_t *>(d + 2 * b_ids + b_off + b_which + b_len);
-    int64_t *h_off = reinterpret_cast<int64_t *>(h);
-    int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off);
+    int64_t *d_ooff = reinterpret_cast<int64_t *>(d);
+    int32_t *d_ids = reinterpret_cast<int32_t *>(d + b_off);
+    int64_t *d_off = reinterpret_cast<int64_t *>(d + b_off + b_ids);
+    int32_t *d_which = reinterpret_cast<int32_t *>(d + b_off + b_ids + b_off);
+    int32_t *d_out = reinterpret_cast<int32_t *>(d + b_off + b_ids + b_off + b_which);
+    int32_t *d_len = reinterpret_cast<int32_t *>(d + b_off + 2 * b_ids + b_off + b_which);
+    unsigned long long *d_err = reinterpret_cast<unsigned long long *>(d_off + n_texts + 1);
+    int64_t *h_ooff = reinterpret_cast<int64_t *>(h);
+    int32_t *h_ids = reinterpret_cast<int32_t *>(h + b_off);
+    int64_t *h_off = reinterpret_cast<int64_t *>(h + b_off + b_ids);
+    int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off + b_ids + b_off);
     for (int64_t k = 0; k <= n_texts; ++k) h_off[k] = off[k] - base;
+    h_off[n_texts + 1] = 0;
     size_t at = 0;
     for (auto &L : lists) {
         std::memcpy(h_which + at, L.data(), L.size() * 4);
@@ -780,19 +822,16 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     // Large calls copy the ids straight from the caller's buffer (no host staging pass); small ones
     // through the pinned buffer (a pageable copy costs tens of microseconds of fixed overhead)
     const bool small = (size_t)total * 4 <= SMALL_CALL_BYTES;
-    int32_t *h_ids = reinterpret_cast<int32_t *>(h + b_off + b_which + 16);
-    int64_t *h_ooff = reinterpret_cast<int64_t *>(h + b_off + b_which + 16 + b_ids);
-    if (total && small) {
-        std::memcpy(h_ids, ids + base, (size_t)total * 4);
-        ENC_TRY(hipMemcpyAsync(d_ids, h_ids, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
-    } else if (total) {
+    if (small) {
+        if (total) std::memcpy(h_ids, ids + base, (size_t)total * 4);
+        ENC_TRY(hipMemcpyAsync(d_ids, h_ids, b_ids + b_off + (size_t)n_rank * 4, hipMemcpyHostToDevice,
+                               E->stream));
+    } else {
         ENC_TRY(hipMemcpyAsync(d_ids, ids + base, (size_t)total * 4, hipMemcpyHostToDevice, E->stream));
+        ENC_TRY(hipMemcpyAsync(d_off, h_off, b_off + (size_t)n_rank * 4, hipMemcpyHostToDevice, E->stream));
     }
-    ENC_TRY(hipMemcpyAsync(d_off, h_off, (size_t)(n_texts + 1) * 8, hipMemcpyHostToDevice, E->stream));
-    if (n_rank) ENC_TRY(hipMemcpyAsync(d_which, h_which, (size_t)n_rank * 4, hipMemcpyHostToDevice, E->stream));
     // replay texts keep length 0 on the device; they are written on the host below
     if (!replay.empty()) ENC_TRY(hipMemsetAsync(d_len, 0, (size_t)n_texts * 4, E->stream));
-    ENC_TRY(hipMemsetAsync(E->d_steps + 7, 0, 8, E->stream));
     // few texts: each has a CU to itself, and the table is read from LDS (when it fits)
     const size_t tab = (size_t)E->lt.words * 4;
     const bool few = (size_t)n_rank <= LATENCY_TEXTS;
@@ -801,32 +840,36 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     for (int i = 0; i < N_SHAPES; ++i) {
         if (lists[i].empty()) continue;
         const bool tab_lds = few && shape_cap(i) > LDS_TAB_MIN_TOKENS && shape_lds(i) + tab <= LDS_BYTES;
-        launch_shape(i, E, (unsigned)lists[i].size(), tab_lds, d_ids, d_off, d_which + at, d_out, d_len);
+        launch_shape(i, E, (unsigned)lists[i].size(), tab_lds, d_ids, d_off, d_which + at, d_out, d_len,
+                     d_err);
         at += lists[i].size();
     }
     ENC_TRY(hipGetLastError());
     ENC_TRY(hipEventRecord(E->ev1, E->stream));
     if (replay.empty()) {
         // packed on the device, into the ids buffer (read by the kernels above, free now)
-        k_scan_lens<<<1, 1024, 0, E->stream>>>(d_len, n_texts, d_ooff);
-        k_gather<<<(unsigned)((n_texts + 3) / 4), 256, 0, E->stream>>>(d_out, d_off, d_len, d_ooff,
-                                                                        n_texts, d_ids);
+        if (n_texts <= 1024 && total <= (1 << 18)) {   // (one workgroup copies it all)
+            k_pack_small<<<1, 1024, 0, E->stream>>>(d_out, d_off, d_len, (int)n_texts, d_ooff, d_err, d_ids);
+        } else {
+            k_scan_lens<<<1, 1024, 0, E->stream>>>(d_len, n_texts, d_ooff, d_err);
+            k_gather<<<(unsigned)((n_texts + 3) / 4), 256, 0, E->stream>>>(d_out, d_off, d_len, d_ooff,
+                                                                            n_texts, d_ids);
+        }
         ENC_TRY(hipGetLastError());
-        unsigned long long *h_err = reinterpret_cast<unsigned long long *>(h + b_off + b_which);
-        ENC_TRY(hipMemcpyAsync(h_err, E->d_steps + 7, 8, hipMemcpyDeviceToHost, E->stream));
         if (small) {
-            ENC_TRY(hipMemcpyAsync(h_ooff, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
-            if (total) ENC_TRY(hipMemcpyAsync(h_ids, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
+            ENC_TRY(hipMemcpyAsync(h_ooff, d_ooff, b_off + (size_t)total * 4, hipMemcpyDeviceToHost,
+                                   E->stream));
             ENC_TRY(hipStreamSynchronize(E->stream));
-            if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+            if (h_ooff[n_texts + 1]) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
             std::memcpy(out_off, h_ooff, (size_t)(n_texts + 1) * 8);
             if (h_ooff[n_texts]) std::memcpy(ids_out, h_ids, (size_t)h_ooff[n_texts] * 4);
         } else {
-            ENC_TRY(hipMemcpyAsync(out_off, d_ooff, (size_t)(n_texts + 1) * 8, hipMemcpyDeviceToHost, E->stream));
+            ENC_TRY(hipMemcpyAsync(h_ooff, d_ooff, (size_t)(n_texts + 2) * 8, hipMemcpyDeviceToHost, E->stream));
             // (the caller's buffer holds off[n] - off[0] ids: a text never grows)
-            if (total) ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
+            ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
             ENC_TRY(hipStreamSynchronize(E->stream));
-            if (*h_err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+            if (h_ooff[n_texts + 1]) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+            std::memcpy(out_off, h_ooff, (size_t)(n_texts + 1) * 8);
         }
     } else {
         // host assembly: the kernels' texts come back at their input offsets, the replayed ones
@@ -837,7 +880,7 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         unsigned long long err = 0;
         ENC_TRY(hipMemcpyAsync(out.data(), d_out, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
         ENC_TRY(hipMemcpyAsync(lens.data(), d_len, (size_t)n_texts * 4, hipMemcpyDeviceToHost, E->stream));
-        ENC_TRY(hipMemcpyAsync(&err, E->d_steps + 7, 8, hipMemcpyDeviceToHost, E->stream));
+        ENC_TRY(hipMemcpyAsync(&err, d_err, 8, hipMemcpyDeviceToHost, E->stream));
         ENC_TRY(hipStreamSynchronize(E->stream));
         if (err) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
         if ((rc = encode_replay(E, ids, off, replay, out.data(), len.data()))) return rc;
