@@ -163,6 +163,48 @@ def incremental_mode(args, stream_merges):
             'handed_to_stream': st['pix_host']}
 
 
+def encode_line(args, merges, n_texts=100000, lo=16, hi=1024, reps=5):
+    """encodeToCode (core.ts:392-409) of a batch of short texts on the device encoder, with the
+    merge list the run made (the warmup merges + the timed ones): texts cut from a
+    later, disjoint stretch of the same synthetic stream.  Kernel time (HIP events) and end to
+    end time of bpe_encode_batch (its parity is the GPU tests' job: tests/test_encoder.py)."""
+    pkg = importlib.import_module('bpe-tokenizer_amd')
+    import numpy as np
+    import time
+    rng = np.random.default_rng(5)
+    lens = rng.integers(lo, hi + 1, size=n_texts)
+    need = int(lens.sum())
+    n = args.corpus_mib << 20
+    e = pkg.Engine(0)   # (the char map and the merges of the bench's own run: replayed here)
+    data = (pkg.synth_zipf(n + need, seed=12345) if args.corpus == 'zipf' else
+            pkg.synth_latin1(n + need, seed=12345, A=args.alphabet,
+                             base=0 if args.alphabet == 256 else 0x20))
+    cmap, n_tok, _ = e.add_latin1(data[:1 << 20], sample_bytes=1 << 20)
+    e.close()
+    ids = cmap[data[n:n + need]]
+    ids = ids[ids >= 0].astype(np.int32)
+    off = np.zeros(n_texts + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    off = np.minimum(off, ids.size)
+    abc = np.asarray([(a, b, n_tok + k) for k, (a, b, _w) in enumerate(merges)], np.int32)
+    enc = pkg.Encoder(0, abc)
+    enc.encode_flat(ids, off)
+    enc.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out, oo = enc.encode_flat(ids, off)
+    e2e = (time.perf_counter() - t0) / reps
+    st = enc.stats()
+    enc.close()
+    kern = st['kernel_ms'] / reps / 1e3
+    return {'what': 'encodeToCode of %d texts of %d-%d chars on the device encoder, the %d merges '
+                    'of the timed run' % (n_texts, lo, hi, len(merges)),
+            'tokens_in': int(off[-1]), 'tokens_out': int(oo[-1]),
+            'kernel_ms': kern * 1e3, 'e2e_ms': e2e * 1e3,
+            'kernel_tokens_per_s': off[-1] / kern, 'e2e_tokens_per_s': off[-1] / e2e,
+            'steps_per_text': st['steps'] / reps / n_texts}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -178,6 +220,10 @@ def main():
     ap.add_argument('--incremental', action='store_true',
                     help='also run the incremental mode on the same workload, printed as a second '
                          'JSON line after the bench line')
+    ap.add_argument('--encode', action='store_true',
+                    help='also run the device encoder (encodeToCode, bpe_encode_batch) with the '
+                         'merges of the timed run over 100 000 texts of 16-1024 chars of the same '
+                         'stream, printed as a further JSON line')
     args = ap.parse_args()
 
     import torch
@@ -310,6 +356,8 @@ def main():
             inc = incremental_mode(args, merges)
             inc['speedup_vs_stream_loop'] = (dt * 1e3 / args.steps) / inc['ms_per_step']
             print(json.dumps({'incremental_mode': inc}), flush=True)
+        if world == 1 and args.encode:
+            print(json.dumps({'encode': encode_line(args, trainer.merges)}), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -6,7 +6,8 @@
 #   tests      pytest -m gpu (PYTEST_PATHS: test paths, PYTEST_K: a -k expression; default all)
 #   smoke      __graft_entry__.smoke()
 #   driver     the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5), timed
-#   bench      full C3 bench line + the incremental mode's line (bench.py --incremental)
+#   bench      full C3 bench line + the incremental mode's and the encoder's lines
+#              (bench.py --incremental --encode)
 #   zipf       full zipf C3 bench line (bench.py --corpus zipf)
 #   prof       rocprofv3 --kernel-trace --stats of the full C3 bench (kernel stats CSV)
 #   profzipf   the same for zipf C3
@@ -55,7 +56,7 @@ for step in "$@"; do
     t1=$(date +%s.%N)
     cat "$OUT/driver.jsonl"; python3 -c "print('driver wall: %.1f s' % ($t1 - $t0))" | tee "$OUT/driver.wall" ;;
   bench)
-    timeout -k 10 700 python3 bench.py --incremental $BENCH_EXTRA > "$OUT/bench.jsonl" 2> "$OUT/bench.err" \
+    timeout -k 10 700 python3 bench.py --incremental --encode $BENCH_EXTRA > "$OUT/bench.jsonl" 2> "$OUT/bench.err" \
         || fail bench "$OUT/bench.err"
     cat "$OUT/bench.jsonl" ;;
   zipf)
