@@ -16,11 +16,14 @@ Prints ONE JSON line (rank 0), right after the timed region (the CPU baseline is
 any GPU work).  --incremental adds a second line: the same workload in the incremental mode.
 """
 import argparse
+import hashlib
 import importlib
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -340,6 +343,10 @@ def main():
                 'traffic_write_bytes': traffic.get('write_bytes_per_launch'),
                 'traffic_source': traffic.get('source'),
             },
+            # (identity of the run's merge list across builds and modes: sha256 of the (a, b, W)
+            # triples as int64, warmup merges included)
+            'merges_sha256': hashlib.sha256(
+                np.asarray(trainer.merges, dtype=np.int64).tobytes()).hexdigest(),
             'breakdown_ms_per_step': {
                 'stream_pass': k1_ms * st['step_launches'] / max(1, args.steps),
                 'select': st['select_ms'] / max(1e-9, timed_frac) / max(1, args.steps),

@@ -967,11 +967,12 @@ int bpe_rank_rccl_init(bpe_ctx *ctx, const void *id, int rank, int world) {
     if (!rc.rccl.init_rank) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    int dev = 0;
-    MHIP(hipGetDevice(&dev));
+    // (the communicator belongs to the context's device, whatever device the caller has current)
     void *s = nullptr;
     MTRY(bpe_get_stream(ctx, &s));
-    (void)s;
+    hipDevice_t dev = 0;
+    MHIP(hipStreamGetDevice((hipStream_t)s, &dev));
+    MHIP(hipSetDevice(dev));
     const ncclResult_t e = rc.rccl.init_rank(&rc.comm, world, u, rank);
     if (e != ncclSuccess)
         return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ncclCommInitRank: ") +
