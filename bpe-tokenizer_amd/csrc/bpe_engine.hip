@@ -128,7 +128,6 @@ struct bpe_ctx {
     // passes (a corpus whose winners are pairs of merged tokens, e.g. Zipf words)
     bool cold_exact = false;
     int exact_streak = 0;
-    bool force_exact = false;   // (BPE_MAINT_EARLY: the next host selection enters the maintained state)
     // with the cold table maintained, merge passes count incrementally (MODE_INCR: the hot bins are
     // maintained too, and a pass counts only the pairs the merge can change); BPE_FUSED=1 keeps
     // the full hot recount with the cold refresh riding along (MODE_FUSED) instead
@@ -188,13 +187,6 @@ struct bpe_ctx {
 };
 
 namespace {
-
-// (A/B knob: enter the maintained state at the first selection, and rebuild it at the next one
-// whenever it is left, instead of waiting for two heavy selections in a row)
-bool maint_early() {
-    static const bool e = getenv("BPE_MAINT_EARLY") != nullptr;
-    return e;
-}
 
 int set_device(bpe_ctx *c) {
     HIP_TRY(hipSetDevice(c->device));
@@ -714,7 +706,6 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
             c->cold_exact = false;
             c->counts_valid = false;
             c->exact_streak = 1;
-            c->force_exact = maint_early();
             return SELECT_RETRY;
         }
         if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3 ||
@@ -723,7 +714,6 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
             // them): this selection still reads it, the next one rebuilds it
             c->cold_exact = false;
             c->exact_streak = 1;
-            c->force_exact = maint_early();
         }
     } else if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
         // the reduce already left the best hot key in the Result: collect its pairs and the
@@ -743,13 +733,12 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
     HIP_TRY(hipStreamSynchronize(s));
     if ((rc = settle_with(c, c->h_res->replaced))) return rc;   // a pending apply's R came along
     if (local && !c->h_res->n_heavy && !c->cold_exact) c->exact_streak = 0;
-    if (local && (c->h_res->n_heavy || c->cold_exact || c->force_exact)) {
+    if (local && (c->h_res->n_heavy || c->cold_exact)) {
         // some cold pair may still reach W: count those exactly (or read the maintained table),
         // then recollect hot + cold
         if (!c->cold_exact) {
             // the second exact pass in a row counts every cold pair and keeps the table
-            const bool full = ++c->exact_streak >= 2 || c->force_exact;
-            c->force_exact = false;
+            const bool full = ++c->exact_streak >= 2;
             if (full) HIP_TRY(hipMemsetAsync(c->d_heavy, 0xFF, HEAVY_WORDS * sizeof(uint32_t), s));
             if ((rc = exact_pass(c))) return rc;
             c->cold_exact = full;
@@ -762,7 +751,6 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
                 // too full to probe well: this selection still reads it, the next one rebuilds it
                 c->cold_exact = false;
                 c->exact_streak = 1;
-                c->force_exact = maint_early();
             }
         }
         HIP_TRY(hipMemsetAsync(&c->d_res->n_cand, 0, sizeof(unsigned), s));
@@ -907,7 +895,6 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
         if (!fused) {
             c->cold_exact = false;
             c->exact_streak = 1;   // (the next exact pass rebuilds the whole table)
-            c->force_exact = maint_early();
         }
     }
     if (fused && !c->use_incr) k_cold_invalidate<<<COLD_GRID, 256, 0, c->stream>>>(c->cold, a, b);
@@ -2811,7 +2798,6 @@ static int merge_until_stream(bpe_ctx *c, int64_t max_length, int64_t min_weight
     // about twice the merges that one finished; after a batch that finished none, the device loop
     // rests for a few host iterations (backing off up to 16) before it is tried again.
     int64_t batch = LOOP_BATCH, rest = 0, backoff = 0;
-    if (maint_early() && !c->cold_exact) c->force_exact = true;
     while (!max_iterations || n < max_iterations) {                      // core.ts:374-378
         // (a maintained cold table: do_find settles the pending merge with its selection, and
         // do_apply compacts)
@@ -2827,7 +2813,6 @@ static int merge_until_stream(bpe_ctx *c, int64_t max_length, int64_t min_weight
             --rest;
             want = 0;
         }
-        if (c->force_exact) want = 0;
         if (want > 0) {
             int64_t nd = 0;
             int st = LOOP_DONE;
