@@ -864,11 +864,16 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
             std::memcpy(out_off, h_ooff, (size_t)(n_texts + 1) * 8);
             if (h_ooff[n_texts]) std::memcpy(ids_out, h_ids, (size_t)h_ooff[n_texts] * 4);
         } else {
+            // the offsets first, then only the packed ids (merges shrink a batch: 5x on zipf words)
             ENC_TRY(hipMemcpyAsync(h_ooff, d_ooff, (size_t)(n_texts + 2) * 8, hipMemcpyDeviceToHost, E->stream));
-            // (the caller's buffer holds off[n] - off[0] ids: a text never grows)
-            ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)total * 4, hipMemcpyDeviceToHost, E->stream));
             ENC_TRY(hipStreamSynchronize(E->stream));
             if (h_ooff[n_texts + 1]) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+            const int64_t n_out = h_ooff[n_texts];
+            if (n_out < 0 || n_out > total) return bpe_fail(BPE_ERR_STATE, "bpe native: bad packed length");
+            if (n_out) {
+                ENC_TRY(hipMemcpyAsync(ids_out, d_ids, (size_t)n_out * 4, hipMemcpyDeviceToHost, E->stream));
+                ENC_TRY(hipStreamSynchronize(E->stream));
+            }
             std::memcpy(out_off, h_ooff, (size_t)(n_texts + 1) * 8);
         }
     } else {
