@@ -447,6 +447,9 @@ struct bpe_encoder {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // large calls in groups (encode_groups): copies on cstream, kernels on stream, two slots
+    hipStream_t cstream = nullptr;
+    hipEvent_t g_in[2] = {nullptr, nullptr}, g_k0[2] = {nullptr, nullptr}, g_k1[2] = {nullptr, nullptr};
     std::vector<int32_t> abc;                 // the merges, in rank order
     bool greedy_ok = true;                    // the rank-greedy form equals the replay (above)
     std::vector<uint8_t> is_input;            // ids used as a or b by the merges so far
@@ -656,6 +659,129 @@ int encode_replay(bpe_encoder *E, const int32_t *ids, const int64_t *off, const 
     return BPE_OK;
 }
 
+// A large call (at least 2 x GROUP_TOKENS input tokens) whose texts all take the kernels, in a few
+// groups (BPE_ENCODE_GROUPS, default 3) through two slots: the copy stream takes group g's ids up (a pageable copy: the host waits for
+// it) while the kernel stream encodes group g - 1, and group g - 1's packed ids come down while
+// group g encodes.  Each group is packed on its own; its ids land after the previous groups'.
+constexpr int64_t GROUP_TOKENS = int64_t(1) << 23;
+
+int encode_groups_run(bpe_encoder *E, const int32_t *ids, const int64_t *off, int64_t n_texts,
+                      const std::vector<int32_t> &shape_of, int32_t *ids_out, int64_t *out_off) {
+    // contiguous text ranges [g0, g1) of >= GROUP_TOKENS tokens (the last one whatever is left)
+    // (few groups: each group's longest texts finish alone, so more groups cost kernel time)
+    static const int64_t n_groups = [] {
+        const char *v = getenv("BPE_ENCODE_GROUPS");
+        return v && atoi(v) >= 2 ? (int64_t)atoi(v) : (int64_t)3;
+    }();
+    const int64_t gt = std::max<int64_t>(GROUP_TOKENS / 2,
+                                          (off[n_texts] - off[0] + n_groups - 1) / n_groups);
+    std::vector<int64_t> cut{0};
+    for (int64_t k = 0; k < n_texts; ++k)
+        if (off[k + 1] - off[cut.back()] >= gt && k + 1 < n_texts) cut.push_back(k + 1);
+    cut.push_back(n_texts);
+    const int ng = (int)cut.size() - 1;
+    int64_t max_t = 0, max_n = 0;
+    for (int g = 0; g < ng; ++g) {
+        max_t = std::max(max_t, off[cut[g + 1]] - off[cut[g]]);
+        max_n = std::max(max_n, cut[g + 1] - cut[g]);
+    }
+    // per slot, device: [ooff (n+2) | ids | off (n+2) | which | out | len]; pinned: [ooff | off | which]
+    const size_t b_ids = align16((size_t)std::max<int64_t>(max_t, 1) * 4);
+    const size_t b_off = align16((size_t)(max_n + 2) * 8);
+    const size_t b_which = align16((size_t)max_n * 4);
+    const size_t slot_d = b_off + b_ids + b_off + b_which + b_ids + b_which;
+    const size_t slot_h = b_off + b_off + b_which;
+    int rc;
+    if ((rc = grow_stage(E, 2 * std::max(slot_d, slot_h)))) return rc;
+    hipStream_t ks = E->stream, cs = E->cstream;
+    int64_t base = 0;
+    out_off[0] = 0;
+    int64_t n_checked = 0;
+    // group g's texts come back: its offsets (small, pinned), then its packed ids
+    auto finish = [&](int g) -> int {
+        const int sl = g & 1;
+        const int64_t k0 = cut[g], n = cut[g + 1] - k0;
+        int64_t *h_ooff = reinterpret_cast<int64_t *>(E->h_buf + sl * slot_h);
+        char *d = E->d_buf + sl * slot_d;
+        ENC_TRY(hipStreamWaitEvent(cs, E->g_k1[sl], 0));
+        ENC_TRY(hipMemcpyAsync(h_ooff, d, (size_t)(n + 2) * 8, hipMemcpyDeviceToHost, cs));
+        ENC_TRY(hipStreamSynchronize(cs));
+        if (h_ooff[n + 1]) return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
+        const int64_t n_out = h_ooff[n];
+        if (n_out < 0 || n_out > off[cut[g + 1]] - off[k0])
+            return bpe_fail(BPE_ERR_STATE, "bpe native: bad packed length");
+        if (n_out) {
+            ENC_TRY(hipMemcpyAsync(ids_out + base, d + b_off, (size_t)n_out * 4, hipMemcpyDeviceToHost, cs));
+            ENC_TRY(hipStreamSynchronize(cs));
+        }
+        for (int64_t k = 1; k <= n; ++k) out_off[k0 + k] = base + h_ooff[k];
+        base += n_out;
+        float ms = 0;
+        ENC_TRY(hipEventElapsedTime(&ms, E->g_k0[sl], E->g_k1[sl]));
+        E->st.kernel_ms += ms;
+        n_checked = cut[g + 1];
+        return BPE_OK;
+    };
+    for (int g = 0; g < ng; ++g) {
+        const int sl = g & 1;
+        const int64_t k0 = cut[g], n = cut[g + 1] - k0, t0 = off[k0], tn = off[cut[g + 1]] - t0;
+        char *d = E->d_buf + sl * slot_d;
+        char *h = E->h_buf + sl * slot_h;
+        int64_t *d_ooff = reinterpret_cast<int64_t *>(d);
+        int32_t *d_ids = reinterpret_cast<int32_t *>(d + b_off);
+        int64_t *d_off = reinterpret_cast<int64_t *>(d + b_off + b_ids);
+        int32_t *d_which = reinterpret_cast<int32_t *>(d + b_off + b_ids + b_off);
+        int32_t *d_out = reinterpret_cast<int32_t *>(d + b_off + b_ids + b_off + b_which);
+        int32_t *d_len = reinterpret_cast<int32_t *>(d + b_off + 2 * b_ids + b_off + b_which);
+        unsigned long long *d_err = reinterpret_cast<unsigned long long *>(d_off + n + 1);
+        int64_t *h_off = reinterpret_cast<int64_t *>(h + b_off);
+        int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off + b_off);
+        // (slot sl's pinned staging was last read by group g - 2's upload, complete by now: its
+        // kernels, which waited for it, were waited for by finish(g - 2))
+        for (int64_t k = 0; k <= n; ++k) h_off[k] = off[k0 + k] - t0;
+        h_off[n + 1] = 0;
+        int64_t cnt[N_SHAPES] = {};
+        for (int64_t k = 0; k < n; ++k) ++cnt[shape_of[k0 + k]];
+        int64_t at[N_SHAPES];
+        for (int i = 0, a = 0; i < N_SHAPES; a += (int)cnt[i], ++i) at[i] = a;
+        int64_t fill[N_SHAPES];
+        std::memcpy(fill, at, sizeof fill);
+        for (int64_t k = 0; k < n; ++k) h_which[fill[shape_of[k0 + k]]++] = (int32_t)k;
+        ENC_TRY(hipMemcpyAsync(d_ids, ids + t0, (size_t)tn * 4, hipMemcpyHostToDevice, cs));
+        ENC_TRY(hipMemcpyAsync(d_off, h_off, b_off + (size_t)n * 4, hipMemcpyHostToDevice, cs));
+        ENC_TRY(hipEventRecord(E->g_in[sl], cs));
+        ENC_TRY(hipStreamWaitEvent(ks, E->g_in[sl], 0));
+        ENC_TRY(hipEventRecord(E->g_k0[sl], ks));
+        for (int i = 0; i < N_SHAPES; ++i)
+            if (cnt[i])
+                launch_shape(i, E, (unsigned)cnt[i], false, d_ids, d_off, d_which + at[i], d_out,
+                             d_len, d_err);
+        k_scan_lens<<<1, 1024, 0, ks>>>(d_len, n, d_ooff, d_err);
+        k_gather<<<(unsigned)((n + 3) / 4), 256, 0, ks>>>(d_out, d_off, d_len, d_ooff, n, d_ids);
+        ENC_TRY(hipGetLastError());
+        ENC_TRY(hipEventRecord(E->g_k1[sl], ks));
+        if (g > 0 && (rc = finish(g - 1))) return rc;
+    }
+    if ((rc = finish(ng - 1))) return rc;
+    if (n_checked != n_texts) return bpe_fail(BPE_ERR_STATE, "bpe native: encode groups incomplete");
+    E->st.texts_rank += n_texts;
+    E->st.tokens_out += out_off[n_texts];
+    return BPE_OK;
+}
+
+int encode_groups(bpe_encoder *E, const int32_t *ids, const int64_t *off, int64_t n_texts,
+                  const std::vector<int32_t> &shape_of, int32_t *ids_out, int64_t *out_off) {
+    // (nothing of an earlier call may still read the staging buffers; a refused call leaves
+    // nothing in flight either)
+    ENC_TRY(hipStreamSynchronize(E->stream));
+    const int rc = encode_groups_run(E, ids, off, n_texts, shape_of, ids_out, out_off);
+    if (rc) {
+        (void)hipStreamSynchronize(E->cstream);
+        (void)hipStreamSynchronize(E->stream);
+    }
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -675,8 +801,13 @@ int bpe_encoder_create(bpe_encoder **out, int device) {
     };
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&E->ev0) != hipSuccess || hipEventCreate(&E->ev1) != hipSuccess)
+        hipEventCreate(&E->ev0) != hipSuccess || hipEventCreate(&E->ev1) != hipSuccess ||
+        hipStreamCreateWithFlags(&E->cstream, hipStreamNonBlocking) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_HIP, "bpe native: encoder stream/events"));
+    for (int i = 0; i < 2; ++i)
+        if (hipEventCreateWithFlags(&E->g_in[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&E->g_k0[i]) != hipSuccess || hipEventCreate(&E->g_k1[i]) != hipSuccess)
+            return bail(bpe_fail(BPE_ERR_HIP, "bpe native: encoder stream/events"));
     if (hipMalloc((void **)&E->d_steps, 64) != hipSuccess ||
         hipMemset(E->d_steps, 0, 64) != hipSuccess)
         return bail(bpe_fail(BPE_ERR_OOM, "bpe native: encoder counters"));
@@ -691,6 +822,7 @@ int bpe_encoder_destroy(bpe_encoder *E) {
     if (!E) return BPE_OK;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
+    if (E->cstream) (void)hipStreamSynchronize(E->cstream);
     if (E->scratch) bpe_destroy(E->scratch);
     if (E->d_slots) (void)hipFree(E->d_slots);
     if (E->d_limg) (void)hipFree(E->d_limg);
@@ -699,6 +831,10 @@ int bpe_encoder_destroy(bpe_encoder *E) {
     if (E->h_buf) (void)hipHostFree(E->h_buf);
     if (E->ev0) (void)hipEventDestroy(E->ev0);
     if (E->ev1) (void)hipEventDestroy(E->ev1);
+    for (int i = 0; i < 2; ++i)
+        for (hipEvent_t ev : {E->g_in[i], E->g_k0[i], E->g_k1[i]})
+            if (ev) (void)hipEventDestroy(ev);
+    if (E->cstream) (void)hipStreamDestroy(E->cstream);
     if (E->stream) (void)hipStreamDestroy(E->stream);
     delete E;
     return BPE_OK;
@@ -790,6 +926,12 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
                     return bpe_fail(BPE_ERR_VOCAB, "bpe native: token id out of range in text");
     }
     if ((rc = upload_table(E))) return rc;
+    if (replay.empty() && total >= 2 * GROUP_TOKENS && !getenv("BPE_ENCODE_ONE_GROUP")) {
+        std::vector<int32_t> shape_of((size_t)n_texts);
+        for (int i = 0; i < N_SHAPES; ++i)
+            for (int32_t k : lists[i]) shape_of[k] = i;
+        return encode_groups(E, ids, off, n_texts, shape_of, ids_out, out_off);
+    }
     // device: [ooff (n+2) | ids, then the packed output | off (n+2) | which | out | len]; the pinned
     // host buffer mirrors [ooff | ids | off | which], so a small call moves [ids | off | which] up in
     // one copy and [ooff | packed ids] down in one.  off[n+1] = 0 is the bad-id counter (zeroed by

@@ -191,6 +191,44 @@ def test_list_the_greedy_cannot_take_is_replayed():
 
 
 @pytest.mark.gpu
+def test_large_call_in_groups(monkeypatch):
+    """A call of more than 2 x 2^23 input tokens goes through the pipelined groups
+    (encode_groups): the same ids and offsets as the one-group form, the reference replay on texts
+    around every group boundary, and a bad id in a late group refused."""
+    rng = np.random.default_rng(21)
+    merges = trained_merges(rng, 30, 200, 400)
+    lengths = rng.integers(0, 1500, size=24000)
+    lengths[100] = pkg.ENCODE_LDS_TOKENS                      # (every launch shape)
+    flat = np.concatenate([np.full(5, 7, np.int32),           # (off[0] > 0)
+                           rng.integers(0, 30, size=int(lengths.sum())).astype(np.int32)])
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64) + 5
+    assert off[-1] - off[0] >= 2 * (1 << 23)
+    enc = pkg.Encoder(0, merges)
+    got, got_off = enc.encode_flat(flat, off)
+    monkeypatch.setenv('BPE_ENCODE_ONE_GROUP', '1')
+    one, one_off = enc.encode_flat(flat, off)
+    monkeypatch.delenv('BPE_ENCODE_ONE_GROUP')
+    assert np.array_equal(got_off, one_off) and np.array_equal(got, one)
+    # texts around each group's first text (three groups by default; BPE_ENCODE_GROUPS) and a
+    # spread of others
+    T = int(off[-1] - off[0])
+    starts = np.searchsorted(off - off[0], [T // 3, 2 * T // 3, T // 2, 1 << 23, 1 << 24])
+    pick = sorted({int(k) for s in starts for k in range(max(0, s - 3), min(len(lengths), s + 3))} |
+                  set(range(0, 24000, 997)) | {100, 23999})
+    texts = [flat[off[k]:off[k + 1]] for k in pick]
+    want = oracle.encode(texts, merges)
+    for k, w in zip(pick, want):
+        assert got[got_off[k]:got_off[k + 1]].tolist() == w.tolist(), k
+    bad = flat.copy()
+    bad[off[23000] + 1] = -3
+    with pytest.raises(pkg.BpeError, match='out of range'):
+        enc.encode_flat(bad, off)
+    again, again_off = enc.encode_flat(flat, off)
+    assert np.array_equal(again_off, got_off) and np.array_equal(again, got)
+    enc.close()
+
+
+@pytest.mark.gpu
 def test_bad_ids_are_refused():
     enc = pkg.Encoder(0, [(0, 1, 2)])
     with pytest.raises(pkg.BpeError, match='out of range'):
