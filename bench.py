@@ -166,6 +166,36 @@ def incremental_mode(args, stream_merges):
             'handed_to_stream': st['pix_host']}
 
 
+def encode_cpu_baseline(ids, off, abc, dev_out=None, dev_off=None, sample_texts=10000):
+    """The device encoder's CPU baseline: the same rank-greedy algorithm on the host
+    (oracle/bpe_cpu_encode.cc: a heap of (rank, position) per text, OpenMP over texts) over the
+    same texts, on the host cores this process may use (cpu_share) and on one thread (a sample of
+    the first texts).  With the device's output given, the CPU's must equal it on every text."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle
+    share = cpu_share()
+    T = share['threads']
+    oracle.cpu_encode_flat(ids, off[:2], abc, threads=1)   # (library load, rank table)
+    t0 = time.perf_counter()
+    got, oo, used = oracle.cpu_encode_flat(ids, off, abc, threads=T)
+    t_mt = time.perf_counter() - t0
+    k = min(sample_texts, len(off) - 1)
+    t0 = time.perf_counter()
+    oracle.cpu_encode_flat(ids, off[:k + 1], abc, threads=1)
+    t_1 = time.perf_counter() - t0
+    res = {'kind': 'port', 'cores': used, 'unit': 'tokens/s',
+           'value': float(off[-1] - off[0]) / t_mt, 'seconds': t_mt,
+           'value_1_thread': float(off[k] - off[0]) / t_1,
+           'sample_1_thread': '%d texts, %d tokens, %.2f s' % (k, int(off[k] - off[0]), t_1),
+           'what': 'oracle/bpe_cpu_encode.cc: the device encoder\'s rank-greedy algorithm on the '
+                   'host (heap per text), all texts of the batch',
+           'host': dict(share, cpu_model=cpu_model())}
+    if dev_out is not None:
+        res['identical_to_device'] = bool(np.array_equal(np.asarray(dev_off), oo) and
+                                          np.array_equal(np.asarray(dev_out)[:oo[-1]], got))
+    return res
+
+
 def encode_line(args, merges, n_texts=100000, lo=16, hi=1024, reps=5):
     """encodeToCode (core.ts:392-409) of a batch of short texts on the device encoder, with the
     merge list the run made (the warmup merges + the timed ones): texts cut from a
@@ -205,7 +235,8 @@ def encode_line(args, merges, n_texts=100000, lo=16, hi=1024, reps=5):
             'tokens_in': int(off[-1]), 'tokens_out': int(oo[-1]),
             'kernel_ms': kern * 1e3, 'e2e_ms': e2e * 1e3,
             'kernel_tokens_per_s': off[-1] / kern, 'e2e_tokens_per_s': off[-1] / e2e,
-            'steps_per_text': st['steps'] / reps / n_texts}
+            'steps_per_text': st['steps'] / reps / n_texts,
+            'cpu_baseline': encode_cpu_baseline(ids, off, abc, out, oo)}
 
 
 def main():

@@ -71,7 +71,8 @@ class Stats(ctypes.Structure):
         ('fused_passes', ctypes.c_int64), ('pix_builds', ctypes.c_int64),
         ('pix_merges', ctypes.c_int64), ('pix_host', ctypes.c_int64),
         ('pix_build_ms', ctypes.c_double), ('cold_used', ctypes.c_int64),
-        ('sel_blocks', ctypes.c_int64),
+        ('sel_blocks', ctypes.c_int64), ('xchg_bytes', ctypes.c_int64),
+        ('xchg_iters', ctypes.c_int64), ('pix_fallbacks', ctypes.c_int64),
     ]
 
     def as_dict(self):

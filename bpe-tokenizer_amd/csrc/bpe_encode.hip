@@ -246,25 +246,9 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
     uint32_t r = block_min<WG>(lmin, red);
     __syncthreads();
     int steps = 0;
-#if BPE_ENC_TIMING
-    // (timing probe: shader cycles per phase of a step, thread 0, summed into steps_total[1..6])
-    long long tk[6] = {0, 0, 0, 0, 0, 0};
-    long long tprev = clock64();
-#define ENC_TICK(q)                                  \
-    do {                                             \
-        const long long now_ = clock64();            \
-        tk[q] += now_ - tprev;                       \
-        tprev = now_;                                \
-    } while (0)
-#else
-#define ENC_TICK(q) \
-    do {            \
-    } while (0)
-#endif
 
     while (r != NO_RANK) {   // (uniform: every thread holds the same r)
         ++steps;
-        ENC_TICK(0);
         const uint32_t c = r & 0xFFFFu;
         // segment length: odd, so that lane t's j-th word (t * k + j) falls in a bank of its own
         // (an even stride would put 2..16 lanes on one bank)
@@ -296,10 +280,8 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
             cnt += (f && j < len) ? 1 : 0;
             d = m ? d + 1 : 0;
         }
-        ENC_TICK(1);
         int total = 0;
         const int before = block_scan<WG>(cnt, scn, total);   // (barrier: all reads done)
-        ENC_TICK(2);
         const int p0 = s - before + (fprev ? 1 : 0);
         // live positions of the segment: j is dead when j - 1 is counted
         const uint32_t live = ~((F << 1) | (fprev ? 1u : 0u)) & ((1u << len) - 1u);
@@ -348,20 +330,15 @@ k_encode(const int32_t *__restrict__ in, const int64_t *__restrict__ off,
                 req &= req - 1;
             }
         }
-        ENC_TICK(4);
         n -= total;
         r = block_min<WG>(lmin, red);   // (barrier: the rewritten text visible)
         __syncthreads();
-        ENC_TICK(5);
     }
 
     for (int i = tid; i < n; i += WG) out[base + i] = tok[i];
     if (tid == 0) {
         out_len[text] = n;
         if (steps) atomicAdd(steps_total, (unsigned long long)steps);
-#if BPE_ENC_TIMING
-        for (int q = 0; q < 6; ++q) atomicAdd(steps_total + 1 + q, (unsigned long long)tk[q]);
-#endif
     }
 }
 
@@ -596,15 +573,23 @@ void launch_shape(int i, bpe_encoder *E, unsigned n, bool tab_lds, const int32_t
         launch_shape<I + 1>(i, E, n, tab_lds, ids, off, which, out, len, err);
 }
 
-int grow_stage(bpe_encoder *E, size_t bytes) {
-    if (E->h_cap < bytes) {
+// Staging buffers of a call: h_bytes of pinned host memory and d_bytes of device memory.  The
+// pinned buffer holds only what a call stages through the host (a large call's ids go straight
+// from and to the caller's buffers), and one larger than PINNED_KEEP is released at the end of
+// the call that needed it (release_stage), so a rare huge call does not pin host memory for the
+// encoder's lifetime.
+constexpr size_t PINNED_KEEP = size_t(64) << 20;
+
+int grow_stage(bpe_encoder *E, size_t h_bytes, size_t d_bytes) {
+    if (E->h_cap < h_bytes) {
         if (E->h_buf) (void)hipHostFree(E->h_buf);
         E->h_buf = nullptr;
         E->h_cap = 0;
-        const size_t n = bytes * 3 / 2 + 4096;
+        const size_t n = h_bytes * 3 / 2 + 4096;
         ENC_TRY(hipHostMalloc((void **)&E->h_buf, n, hipHostMallocDefault));
         E->h_cap = n;
     }
+    const size_t bytes = d_bytes;
     if (E->d_cap < bytes) {
         if (E->d_buf) (void)hipFree(E->d_buf);
         E->d_buf = nullptr;
@@ -614,6 +599,17 @@ int grow_stage(bpe_encoder *E, size_t bytes) {
         E->d_cap = n;
     }
     return BPE_OK;
+}
+
+void release_stage(bpe_encoder *E) {
+    if (E->h_cap > PINNED_KEEP) {
+        // (an early error return may leave a copy from it in flight)
+        (void)hipStreamSynchronize(E->stream);
+        (void)hipStreamSynchronize(E->cstream);
+        (void)hipHostFree(E->h_buf);
+        E->h_buf = nullptr;
+        E->h_cap = 0;
+    }
 }
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -692,7 +688,7 @@ int encode_groups_run(bpe_encoder *E, const int32_t *ids, const int64_t *off, in
     const size_t slot_d = b_off + b_ids + b_off + b_which + b_ids + b_which;
     const size_t slot_h = b_off + b_off + b_which;
     int rc;
-    if ((rc = grow_stage(E, 2 * std::max(slot_d, slot_h)))) return rc;
+    if ((rc = grow_stage(E, 2 * slot_h, 2 * slot_d))) return rc;
     hipStream_t ks = E->stream, cs = E->cstream;
     int64_t base = 0;
     out_off[0] = 0;
@@ -775,10 +771,10 @@ int encode_groups(bpe_encoder *E, const int32_t *ids, const int64_t *off, int64_
     // nothing in flight either)
     ENC_TRY(hipStreamSynchronize(E->stream));
     const int rc = encode_groups_run(E, ids, off, n_texts, shape_of, ids_out, out_off);
-    if (rc) {
-        (void)hipStreamSynchronize(E->cstream);
-        (void)hipStreamSynchronize(E->stream);
-    }
+    // (every copy of the call is complete on success; a failed call drains both streams)
+    (void)hipStreamSynchronize(E->cstream);
+    (void)hipStreamSynchronize(E->stream);
+    release_stage(E);
     return rc;
 }
 
@@ -932,16 +928,25 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
             for (int32_t k : lists[i]) shape_of[k] = i;
         return encode_groups(E, ids, off, n_texts, shape_of, ids_out, out_off);
     }
-    // device: [ooff (n+2) | ids, then the packed output | off (n+2) | which | out | len]; the pinned
-    // host buffer mirrors [ooff | ids | off | which], so a small call moves [ids | off | which] up in
-    // one copy and [ooff | packed ids] down in one.  off[n+1] = 0 is the bad-id counter (zeroed by
-    // the upload), which the pack kernel copies to ooff[n+1].
+    // device: [ooff (n+2) | ids, then the packed output | off (n+2) | which | out | len].  A small
+    // call's pinned host buffer mirrors [ooff | ids | off | which], so it moves [ids | off | which]
+    // up in one copy and [ooff | packed ids] down in one; a large call copies its ids straight from
+    // and to the caller's buffers and pins only [ooff | off | which].  off[n+1] = 0 is the bad-id
+    // counter (zeroed by the upload), which the pack kernel copies to ooff[n+1].
     const size_t b_ids = align16((size_t)std::max<int64_t>(total, 1) * 4);
     const size_t b_off = align16((size_t)(n_texts + 2) * 8);
     const size_t b_which = align16((size_t)std::max<int64_t>(n_rank, 1) * 4);
     const size_t b_len = align16((size_t)n_texts * 4);
     const size_t bytes = b_off + b_ids + b_off + b_which + b_ids + b_len;
-    if ((rc = grow_stage(E, bytes))) return rc;
+    // Large calls copy the ids straight from the caller's buffer (no host staging pass); small ones
+    // through the pinned buffer (a pageable copy costs tens of microseconds of fixed overhead)
+    const bool small = (size_t)total * 4 <= SMALL_CALL_BYTES;
+    const size_t h_ids_bytes = small ? b_ids : 0;
+    if ((rc = grow_stage(E, b_off + h_ids_bytes + b_off + b_which, bytes))) return rc;
+    struct Release {
+        bpe_encoder *e;
+        ~Release() { release_stage(e); }
+    } release{E};
     char *h = E->h_buf, *d = E->d_buf;
     int64_t *d_ooff = reinterpret_cast<int64_t *>(d);
     int32_t *d_ids = reinterpret_cast<int32_t *>(d + b_off);
@@ -951,9 +956,9 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
     int32_t *d_len = reinterpret_cast<int32_t *>(d + b_off + 2 * b_ids + b_off + b_which);
     unsigned long long *d_err = reinterpret_cast<unsigned long long *>(d_off + n_texts + 1);
     int64_t *h_ooff = reinterpret_cast<int64_t *>(h);
-    int32_t *h_ids = reinterpret_cast<int32_t *>(h + b_off);
-    int64_t *h_off = reinterpret_cast<int64_t *>(h + b_off + b_ids);
-    int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off + b_ids + b_off);
+    int32_t *h_ids = reinterpret_cast<int32_t *>(h + b_off);   // (small calls only)
+    int64_t *h_off = reinterpret_cast<int64_t *>(h + b_off + h_ids_bytes);
+    int32_t *h_which = reinterpret_cast<int32_t *>(h + b_off + h_ids_bytes + b_off);
     for (int64_t k = 0; k <= n_texts; ++k) h_off[k] = off[k] - base;
     h_off[n_texts + 1] = 0;
     size_t at = 0;
@@ -961,9 +966,6 @@ int bpe_encode_batch(bpe_encoder *E, const int32_t *ids, const int64_t *off, int
         std::memcpy(h_which + at, L.data(), L.size() * 4);
         at += L.size();
     }
-    // Large calls copy the ids straight from the caller's buffer (no host staging pass); small ones
-    // through the pinned buffer (a pageable copy costs tens of microseconds of fixed overhead)
-    const bool small = (size_t)total * 4 <= SMALL_CALL_BYTES;
     if (small) {
         if (total) std::memcpy(h_ids, ids + base, (size_t)total * 4);
         ENC_TRY(hipMemcpyAsync(d_ids, h_ids, b_ids + b_off + (size_t)n_rank * 4, hipMemcpyHostToDevice,
@@ -1055,12 +1057,6 @@ int bpe_encoder_get_stats(bpe_encoder *E, bpe_encoder_stats *out) {
     unsigned long long steps[8] = {};
     ENC_TRY(hipMemcpy(steps, E->d_steps, 64, hipMemcpyDeviceToHost));
     E->st.steps = (int64_t)steps[0];
-#if BPE_ENC_TIMING
-    fprintf(stderr, "[enc timing] cycles per step: read+flags %.0f scan %.0f write %.0f lookups %.0f min %.0f (pre %.0f)\n",
-            (double)steps[2] / std::max(1ull, steps[0]), (double)steps[3] / std::max(1ull, steps[0]),
-            (double)steps[4] / std::max(1ull, steps[0]), (double)steps[5] / std::max(1ull, steps[0]),
-            (double)steps[6] / std::max(1ull, steps[0]), (double)steps[1] / std::max(1ull, steps[0]));
-#endif
     *out = E->st;
     return BPE_OK;
 }

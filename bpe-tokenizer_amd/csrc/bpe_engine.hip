@@ -167,6 +167,7 @@ struct bpe_ctx {
     unsigned long long *rl_table = nullptr, *rl_tie = nullptr;
     int rl_rank = 0, rl_world = 1;
     int64_t rl_base = 0, rl_enqueued = 0, rl_max_length = 0;
+    int64_t rl_words = 0;   // words of the exchange all-reduced per iteration (this batch)
     bool rl_open = false;
     // d_hot and the cold table hold the GLOBAL counts of a sharded corpus, replicated on every
     // rank (bpe_set_global_counts): the rank loop keeps them merge by merge from the all-reduced
@@ -1235,10 +1236,18 @@ int rank_loop_select(bpe_ctx *c) {
     hipEvent_t e_sel = span_begin(c);
     if (c->rl_global) {
         k_apply_delta<<<COLD_GRID, 256, 0, s>>>(c->rl_table, c->d_hot, c->cold, c->d_ctl);
-        k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(c->d_hot, c->d_len16, ml, c->d_res, c->d_ctl);
-        k_argmax_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_len16, ml, c->d_res, c->d_ctl);
-        k_collect<<<COLD_GRID, 256, 0, s>>>(c->d_hot, c->cold, c->d_len16, ml, c->d_res, c->d_cand,
-                                            c->d_ctl);
+        // the block maxima of the cold table, as in the single-corpus device loop (round 5: was
+        // k_argmax_hot + k_argmax_cold + k_collect, two scans of every claimed cold pair per merge,
+        // which grew with the vocabulary).  The summed delta rows re-add the pairs of a and b that
+        // k_incr_invalidate zeroed (to at most their old count: their blocks were flagged when the
+        // zeroed entry may have been the max) and claim the pairs of c (new claims at the end of
+        // the dense view), exactly the changes the incremental form recomputes.  A full scan on the
+        // first selection of a batch and every SEL_FULL_EVERY-th (its dead claims).
+        static const bool sel_full = getenv("BPE_SEL_FULL") != nullptr;
+        const bool full = sel_full || c->rl_enqueued % SEL_FULL_EVERY == 0;
+        k_select_maint<<<full ? COLD_GRID : HOT_BINS / 256, 256, 0, s>>>(
+            c->d_hot, c->cold, c->d_len16, ml, c->d_res, c->d_cand, c->d_brec, c->d_ticket,
+            c->d_ctl, full ? 1 : 0);
     } else {
         const unsigned long long *table = c->rl_table + XCHG_HDR;
         k_argmax_hot<<<HOT_BINS / 256, 256, 0, s>>>(table, c->d_len16, ml, c->d_res, c->d_ctl);
@@ -1282,7 +1291,8 @@ int rank_loop_count(bpe_ctx *c) {
     unsigned long long *x = c->rl_table;
     hipEvent_t e_step = span_begin(c);
     if (c->rl_global) {
-        k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl);
+        k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl, c->d_len16,
+                                                    c->rl_max_length);
         k_step_loop<MODE_INCR><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
                                                    c->d_ctl, c->d_partials, c->d_spill, c->cold,
                                                    c->d_sums, &c->d_res->replaced, c->d_hot, x);
@@ -2727,8 +2737,10 @@ int bpe_rank_loop_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, uint
         return fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
     int rc = set_device(c);
     if (rc) return rc;
-    return rank_loop_begin(c, max_length, min_weight, (unsigned long long *)xchg,
-                           (unsigned long long *)tie, rank, world, xchg_words);
+    rc = rank_loop_begin(c, max_length, min_weight, (unsigned long long *)xchg,
+                         (unsigned long long *)tie, rank, world, xchg_words);
+    if (rc == BPE_OK) c->rl_words = *xchg_words;
+    return rc;
 }
 
 int bpe_cold_counts(bpe_ctx *c, uint32_t *keys, uint64_t *counts, int64_t cap, int64_t *n) {
@@ -2753,8 +2765,27 @@ int bpe_rank_loop_select(bpe_ctx *c) {
     NOT_MULTI;
     if (!c) return fail(BPE_ERR_ARG, "bpe native: null context");
     int rc = set_device(c);
+    if (rc == BPE_OK && c->stats_on && c->rl_open) {
+        // (every iteration's exchange: one all-reduce(SUM) of rl_words words before this call)
+        c->stats.xchg_bytes += c->rl_words * 8;
+        c->stats.xchg_iters += 1;
+    }
     return rc ? rc : rank_loop_select(c);
 }
+
+}  // extern "C"
+
+// (internal, bpe_multi.cpp bpe_rank_loop_rccl) the buffers and size of the open batch: the
+// all-reduces a caller issues must be over exactly these
+int rank_loop_buffers(bpe_ctx *c, unsigned long long **xchg, unsigned long long **tie, int64_t *words) {
+    if (!c || !c->rl_open) return fail(BPE_ERR_STATE, "bpe native: rank loop not begun");
+    *xchg = c->rl_table;
+    *tie = c->rl_tie;
+    *words = c->rl_words;
+    return BPE_OK;
+}
+
+extern "C" {
 
 int bpe_rank_loop_decide(bpe_ctx *c) {
     NOT_MULTI;

@@ -55,13 +55,7 @@ constexpr int RING = BPE_RING;
 static_assert(RING >= 5, "ring depth");
 // (the overflow screen runs once per ring round: 16 waves x RING chunks x 256 adds must stay
 // below the 49152 adds of headroom above 0x4000, see lds_sweep)
-// BPE_SCREEN_LAG: a round's LDS returns are screened at the end of the NEXT round (two banks, the
-// loop unrolled by two rounds), so the screen waits only on adds a round old (round-4 A/B, not
-// taken: 1.3 % slower, profiles/r04_ab_step_asm_lag.txt)
-#ifndef BPE_SCREEN_LAG
-#define BPE_SCREEN_LAG 0
-#endif
-static_assert(WAVES_PER_WG * RING * (BPE_SCREEN_LAG ? 2 : 1) * 256 < 49152,
+static_assert(WAVES_PER_WG * RING * 256 < 49152,
               "ring depth vs the LDS overflow screen");
 // How far ahead k_step loads: chunk c + LEAD at stage c, into the slot of chunk c + LEAD - RING.
 // At stage c the wave holds chunks c - 1 (count), c (apply) and c + 1 (its first token), so every
@@ -77,12 +71,6 @@ static_assert(LEAD >= 2 && LEAD <= RING - 2, "load lead");
 #ifndef BPE_LOAD_AUX
 #define BPE_LOAD_AUX 2
 #endif
-// Merge detection of the streaming pass: 0 packed (slot, neighbour) words (v_perm + compare per
-// plane), 1 compares into wave masks (slot == a, slot == b) combined on the scalar unit
-#ifndef BPE_APPLY_MASKS
-#define BPE_APPLY_MASKS 0
-#endif
-
 // f(integral_constant<I>) for I = 0 .. N-1, unrolled in the source (the ring's slot indices must be
 // compile-time constants, or the ring is moved to scratch memory)
 template <int I, int N, typename F>
@@ -456,25 +444,11 @@ __device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | (
 
 // The same from the pair, as two instructions (the compiler otherwise re-associates the mask and
 // the shift into three, for lack of a second literal operand)
-// BPE_ASM_ONE (round-4 A/B, not taken): the three VALU in one asm block, without the s_nop the
-// hazard recognizer pads after each inline-asm result; 1.2 % slower on k_step_loop
-// (profiles/r04_ab_step_asm_lag.txt)
-#ifndef BPE_ASM_ONE
-#define BPE_ASM_ONE 0
-#endif
 __device__ __forceinline__ uint32_t cold_addr_of(int32_t x, int32_t y) {
-#if !BPE_ASM_ONE
     uint32_t b, a;
     asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
     asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(a) : "v"(b), "s"(HOT_BYTES));
     return a;
-#else
-    uint32_t a;
-    asm("v_mad_u32_u24 %0, %1, %2, %3\n\tv_bfe_u32 %0, %0, 0, 13\n\tv_lshl_or_b32 %0, %0, 2, %4"
-        : "=&v"(a)
-        : "v"(x), "s"(SKETCH_K), "v"(y), "s"(HOT_BYTES));
-    return a;
-#endif
 }
 
 __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
@@ -959,20 +933,7 @@ __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, 
         addr = hot & (HOT_BYTES - 4);
         inc = (uint32_t)(u >= 0xFFFFFF00u) << (((uint32_t)x << 4) & 31u);   // both ids < 256
     } else {
-#if !BPE_ASM_ONE
         addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of(x, y));   // both ids < 256
-#else
-        // the class compare, the sketch address (three VALU) and the select in one block: the
-        // compare's VCC is read three instructions later, so no wait state is padded in
-        asm("v_cmp_lt_u32 vcc, %5, %6\n\t"
-            "v_mad_u32_u24 %0, %1, %2, %3\n\t"
-            "v_bfe_u32 %0, %0, 0, 13\n\t"
-            "v_lshl_or_b32 %0, %0, 2, %4\n\t"
-            "v_cndmask_b32 %0, %0, %7, vcc"
-            : "=&v"(addr)
-            : "v"(x), "s"(SKETCH_K), "v"(y), "s"(HOT_BYTES), "s"(0xFFFFFEFFu), "v"(u), "v"(hot)
-            : "vcc");
-#endif
         inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
     }
 }
@@ -1231,27 +1192,6 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
         return;
     }
 #endif
-#if BPE_APPLY_MASKS
-    // The common case, no (a, b) in the chunk: eight compares into wave masks (slot == a, slot ==
-    // b), the matches M[e] = A[e] & B[e + 1] on the scalar unit (dead slots and tail tags are
-    // negative: never a or b), the last live slot's pair (last, nxt) as a scalar test.
-    const unsigned long long A0 = __ballot(w.t[0] == ma), A1 = __ballot(w.t[1] == ma),
-                             A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
-    const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
-                             B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
-    {
-        const unsigned long long H = (A0 & B1) | (A1 & B2) | (A2 & B3) | (A3 & (B0 >> 1));
-        const uint32_t m_l = ((uint32_t)(w.last ^ ma) | (uint32_t)(nxt ^ mb)) == 0u;
-        unsigned long long T = H | (unsigned long long)(m_l | (uint32_t)ap.match);
-        if (MERGE == MERGE_XX) T |= (unsigned long long)(uint32_t)(w.last == ma);
-        if (T == 0ull) {
-            ap.prev = w.last;
-            ap.par = 0;
-            ap.match = 0;
-            return;
-        }
-    }
-#else
     // The common case, no (a, b) in the chunk: four packed (slot, right neighbour) compares.  In a
     // partial chunk lane 63's slot 3 (dead) stands in for the last live slot, paired with nxt.
     // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)
@@ -1277,7 +1217,6 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
                              A2 = __ballot(w.t[2] == ma), A3 = __ballot(w.t[3] == ma);
     const unsigned long long B0 = __ballot(w.t[0] == mb), B1 = __ballot(w.t[1] == mb),
                              B2 = __ballot(w.t[2] == mb), B3 = __ballot(w.t[3] == mb);
-#endif
     unsigned long long M0 = A0 & B1, M1 = A1 & B2, M2 = A2 & B3, M3 = A3 & (B0 >> 1);
     // the last live slot's neighbour is nxt
     int m_last = ((uint32_t)(w.last ^ ma) | (uint32_t)(nxt ^ mb)) == 0u;
@@ -1451,25 +1390,19 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         // c+RING-3 into the slot of chunk c-3 (fre), which the previous stage freed, so the load
         // can issue at once without its registers overlapping a chunk still in use.  Stage i of a
         // round keeps its count's LDS returns in D[i] until the round's overflow screen.
-        Defer D[RING], D2[BPE_SCREEN_LAG ? RING : 1];
+        Defer D[RING];
         static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
             D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
-            if (BPE_SCREEN_LAG) D2[i].o[0] = D2[i].o[1] = D2[i].o[2] = D2[i].o[3] = 0u;
         });
         // The overflow screen of a round (MODE_TABLE / MODE_FUSED): every word the wave's adds
         // returned since the last screen, then a sweep if some half stood at >= 0x4000 (lds_sweep)
-        auto screen_bank = [&](Defer(&B)[BPE_SCREEN_LAG ? RING : 1], bool lagged) __attribute__((always_inline)) {
+        auto screen_round = [&]() __attribute__((always_inline)) {
             if (MODE != MODE_TABLE && MODE != MODE_FUSED && MODE != MODE_INCR) return;
             uint32_t acc = s.seen;
             s.seen = 0;
             static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
-                if (lagged) {
-                    acc |= B[i].o[0] | B[i].o[1] | B[i].o[2] | B[i].o[3];
-                    B[i].o[0] = B[i].o[1] = B[i].o[2] = B[i].o[3] = 0u;
-                } else {
-                    acc |= D[i].o[0] | D[i].o[1] | D[i].o[2] | D[i].o[3];
-                    D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
-                }
+                acc |= D[i].o[0] | D[i].o[1] | D[i].o[2] | D[i].o[3];
+                D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
             });
             if (__ballot((acc & SWEEP_BITS) != 0u) != 0ull) {
                 if (MODE == MODE_INCR) {
@@ -1482,7 +1415,6 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 }
             }
         };
-        auto screen_round = [&]() __attribute__((always_inline)) { screen_bank(D2, false); };
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
                          Defer &df) __attribute__((always_inline)) {
             load(fre, c + LEAD);
@@ -1517,28 +1449,6 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             }
             // whole rounds of RING stages; stages past the region see empty chunks, so the
             // pending chunk always ends in the last slot
-#if BPE_SCREEN_LAG
-            // two rounds per trip: round A's adds return into D, round B's into D2; each screen
-            // takes the bank of the round before (its adds a round old)
-            for (int c = 0; c < nc; c += 2 * RING) {
-                static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
-                    constexpr int i = decltype(I)::value;
-                    stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
-                          S[(i + LEAD) % RING], c + i, D[i]);
-                });
-                screen_bank(D2, true);
-                static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
-                    constexpr int i = decltype(I)::value;
-                    stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
-                          S[(i + LEAD) % RING], c + RING + i, D2[i]);
-                });
-                screen_bank(D2, false);   // (bank D)
-            }
-            Defer dt;   // (the region's last chunk takes the exact path: s.seen)
-            if (S[RING - 1].len) count_chunk<MODE, true>(S[RING - 1], NONE, lane, s, k, dt);
-            screen_bank(D2, true);
-            screen_round();
-#else
             for (int c = 0; c < nc; c += RING) {
                 static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
                     constexpr int i = decltype(I)::value;
@@ -1550,7 +1460,6 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             Defer dt;   // (the region's last chunk takes the exact path: s.seen)
             if (S[RING - 1].len) count_chunk<MODE, true>(S[RING - 1], NONE, lane, s, k, dt);
             screen_round();
-#endif
         }
         if (lane == 0) {
             RegionSum o;

@@ -75,7 +75,8 @@ struct bpe_multi {
     // index, entered at the first batch; entries counts them (one index build each), and a run
     // whose batches keep handing over goes on in the streaming mode (pix_off)
     bool pix = false, pix_off = false;
-    int64_t pix_entries = 0;
+    // (since the last bpe_set_mode: index entries, merges made; fallbacks: times pix_off was set)
+    int64_t pix_entries = 0, pix_merged = 0, pix_fallbacks = 0;
     std::vector<ncclComm_t> comms;
     Rccl rccl;
     // shards sharing one device (the one-GPU test box, BPE_REDUCE_HOST): the exchange is a device
@@ -342,6 +343,7 @@ int multi_set_mode(bpe_multi *m, int mode) {
     for (auto s : m->sh) MTRY(bpe_set_mode(s, mode));
     m->pix = mode == BPE_MODE_INCREMENTAL;
     m->pix_off = false;
+    m->pix_entries = m->pix_merged = 0;
     m->maintained = false;   // (the next batch enters the mode's own global state)
     m->heavy_streak = 0;
     for (auto s : m->sh) MTRY(bpe_leave_global(s));
@@ -791,8 +793,11 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
             // once; the streaming mode when the cold pairs outgrow the sketch)
             const bool pix = m->pix && !m->pix_off;
             if (!m->maintained && (m->heavy_streak >= 2 || pix)) {
-                if (pix && ++m->pix_entries > 64 && m->pix_entries > n / 16) {
-                    m->pix_off = true;   // (the index keeps handing over here: the stream goes on)
+                // (more than 64 entries since the mode was set, at least one per 16 merges made:
+                // the index keeps handing over here, and the stream goes on)
+                if (pix && ++m->pix_entries > 64 && m->pix_entries > (m->pix_merged + n) / 16) {
+                    m->pix_off = true;
+                    ++m->pix_fallbacks;
                     for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
                 }
                 MTRY(enter_maintained(m));
@@ -862,6 +867,7 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
         if (rep != w) return bpe_fail(BPE_ERR_STATE, "bpe native: replacement count != W");
         put(a, b, w);
     }
+    if (m->pix) m->pix_merged += n;
     *n_merges = n;
     return BPE_OK;
 }
@@ -898,7 +904,10 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.pix_merges += x.pix_merges;
         acc.pix_host = std::max(acc.pix_host, x.pix_host);
         acc.pix_build_ms = std::max(acc.pix_build_ms, x.pix_build_ms);
+        acc.xchg_bytes += x.xchg_bytes;
+        acc.xchg_iters = std::max(acc.xchg_iters, x.xchg_iters);
     }
+    acc.pix_fallbacks = m->pix_fallbacks;
     *out = acc;
     return BPE_OK;
 }
@@ -915,18 +924,20 @@ int multi_get_stream(bpe_multi *m, void **stream) { return bpe_get_stream(m->sh[
 // context's own stream between the rank loop's kernels, so a batch of iterations is enqueued by
 // one call with no host round trip and no cross-stream event per collective.
 namespace {
+// (one RCCL library for every rank communicator and for ncclGetUniqueId: loaded once, kept for
+// the process's lifetime, so no communicator outlives the library it came from)
+Rccl &id_rccl() {
+    static Rccl r;
+    return r;
+}
 struct RankComm {
-    Rccl rccl;
+    const Rccl *rccl = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
 };
 std::map<bpe_ctx *, RankComm> &rank_comms() {
     static std::map<bpe_ctx *, RankComm> m;
     return m;
-}
-Rccl &id_rccl() {   // (the library ncclGetUniqueId comes from: loaded once, kept)
-    static Rccl r;
-    return r;
 }
 }  // namespace
 
@@ -935,7 +946,8 @@ void rank_rccl_forget(bpe_ctx *ctx) {
     auto &m = rank_comms();
     auto it = m.find(ctx);
     if (it == m.end()) return;
-    if (it->second.comm && it->second.rccl.destroy) it->second.rccl.destroy(it->second.comm);
+    if (it->second.comm && it->second.rccl && it->second.rccl->destroy)
+        it->second.rccl->destroy(it->second.comm);
     m.erase(it);
 }
 
@@ -962,9 +974,11 @@ int bpe_rank_rccl_init(bpe_ctx *ctx, const void *id, int rank, int world) {
     MTRY(bpe_shard_count(ctx, &n_shards));
     if (n_shards != 1) return bpe_fail(BPE_ERR_STATE, "bpe native: a rank communicator needs a single-device context");
     rank_rccl_forget(ctx);
+    Rccl &lib = id_rccl();
+    if (!lib.so) MTRY(load_rccl(lib));
     RankComm rc;
-    MTRY(load_rccl(rc.rccl));
-    if (!rc.rccl.init_rank) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
+    rc.rccl = &lib;
+    if (!lib.init_rank) return bpe_fail(BPE_ERR_HIP, "bpe native: RCCL symbols missing");
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     // (the communicator belongs to the context's device, whatever device the caller has current)
@@ -973,10 +987,10 @@ int bpe_rank_rccl_init(bpe_ctx *ctx, const void *id, int rank, int world) {
     hipDevice_t dev = 0;
     MHIP(hipStreamGetDevice((hipStream_t)s, &dev));
     MHIP(hipSetDevice(dev));
-    const ncclResult_t e = rc.rccl.init_rank(&rc.comm, world, u, rank);
+    const ncclResult_t e = lib.init_rank(&rc.comm, world, u, rank);
     if (e != ncclSuccess)
         return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ncclCommInitRank: ") +
-                                      (rc.rccl.error_string ? rc.rccl.error_string(e) : "RCCL error")).c_str());
+                                      (lib.error_string ? lib.error_string(e) : "RCCL error")).c_str());
     rc.rank = rank;
     rc.world = world;
     rank_comms()[ctx] = rc;
@@ -989,15 +1003,22 @@ int bpe_rank_loop_rccl(bpe_ctx *ctx, uint64_t *xchg, int64_t xchg_words, uint64_
         return bpe_fail(BPE_ERR_STATE, "bpe native: no rank communicator (bpe_rank_rccl_init)");
     if (!xchg || !tie || xchg_words < 1 || iterations < 0)
         return bpe_fail(BPE_ERR_ARG, "bpe native: bad rank loop arguments");
+    // the all-reduces must cover exactly the buffers the batch's kernels use (bpe_rank_loop_begin)
+    unsigned long long *bx = nullptr, *bt = nullptr;
+    int64_t bw = 0;
+    MTRY(rank_loop_buffers(ctx, &bx, &bt, &bw));
+    if ((void *)bx != (void *)xchg || (void *)bt != (void *)tie || xchg_words != bw)
+        return bpe_fail(BPE_ERR_ARG, "bpe native: the exchange / tie buffers or the word count differ "
+                                     "from the batch's (bpe_rank_loop_begin)");
     RankComm &rc = it->second;
     void *sp = nullptr;
     MTRY(bpe_get_stream(ctx, &sp));
     hipStream_t st = (hipStream_t)sp;
     auto ar = [&](uint64_t *buf, size_t count, ncclRedOp_t op, const char *what) -> int {
-        const ncclResult_t e = rc.rccl.all_reduce(buf, buf, count, ncclUint64, op, rc.comm, st);
+        const ncclResult_t e = rc.rccl->all_reduce(buf, buf, count, ncclUint64, op, rc.comm, st);
         if (e == ncclSuccess) return BPE_OK;
         return bpe_fail(BPE_ERR_HIP, (std::string("bpe native: ") + what + ": " +
-                                      (rc.rccl.error_string ? rc.rccl.error_string(e) : "RCCL error")).c_str());
+                                      (rc.rccl->error_string ? rc.rccl->error_string(e) : "RCCL error")).c_str());
     };
     for (int i = 0; i < iterations; ++i) {
         MTRY(ar(xchg, (size_t)xchg_words, ncclSum, "ncclAllReduce(exchange)"));

@@ -45,5 +45,9 @@ extern "C" int bpe_sum_shards(unsigned long long *const *bufs, int n, size_t cou
 // (bpe_multi.cpp) a context going away frees its rank communicator (bpe_rank_rccl_init)
 void rank_rccl_forget(bpe_ctx *ctx);
 
+// (bpe_engine.hip) the exchange and tie buffers and the exchange's word count of the context's
+// open rank-loop batch (bpe_rank_loop_begin); BPE_ERR_STATE when no batch is open
+int rank_loop_buffers(bpe_ctx *c, unsigned long long **xchg, unsigned long long **tie, int64_t *words);
+
 // error reporting shared with bpe_engine.hip
 int bpe_fail(int code, const char *msg);

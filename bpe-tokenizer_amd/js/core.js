@@ -20,8 +20,7 @@ const {
   loadNative,
   maxLengthArg,
   minWeightArg,
-  encodeOnDevice,
-  encodeIdsOnDevice,
+  encodeIdsMaybeOnDevice,
   idsToCode,
 } = require('./native')
 
@@ -411,10 +410,8 @@ class BPETokenizer {
       content_in_code += token.code
     }
 
-    if (encodeOnDevice(ids.length, this.merge_tokens.length)) {
-      let out = encodeIdsOnDevice(this, this.merge_tokens, tokenTriple, ids)
-      return idsToCode(out, 0, out.length)
-    }
+    let out = encodeIdsMaybeOnDevice(this, this.merge_tokens, tokenTriple, ids)
+    if (out) return idsToCode(out, 0, out.length)
 
     for (let [from_code, to_code] of this.merge_codes) {
       content_in_code = replaceAll(content_in_code, from_code, to_code)

@@ -32,8 +32,7 @@ const {
   loadNative,
   maxLengthArg,
   minWeightArg,
-  encodeOnDevice,
-  encodeIdsOnDevice,
+  encodeIdsMaybeOnDevice,
   idsToCode,
 } = require('./native')
 const { EOF } = require('./core')
@@ -607,10 +606,8 @@ class BPETokenizerDB {
       ids.push(token.id - 1)
       content_in_code += token.code
     }
-    if (encodeOnDevice(ids.length, this.merge_codes.length)) {
-      let out = encodeIdsOnDevice(this, this.merge_codes, codeTriple, ids)
-      return idsToCode(out, 0, out.length)
-    }
+    let out = encodeIdsMaybeOnDevice(this, this.merge_codes, codeTriple, ids)
+    if (out) return idsToCode(out, 0, out.length)
     for (let [from_code, to_code] of this.merge_codes) {
       content_in_code = content_in_code.split(from_code).join(to_code)
     }

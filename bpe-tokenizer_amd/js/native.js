@@ -21,8 +21,11 @@ function loadNative() {
  *                   + 0.05 us per char (id and code conversions, copies)
  *   device (long) ~ 10 us per merge (one replay pass each) + 0.05 us per char
  * In practice: long merge lists with short texts, and long texts.  BPE_ENCODE_DEVICE=0 keeps every
- * call on the JS replay (host-only runs without a device), =1 sends every call with a merge to the
- * device (tests).
+ * call on the JS replay, =1 sends every call with a merge to the device and lets its errors through
+ * (tests).  By default a call the device cannot take falls back to the JS replay
+ * (encodeIdsMaybeOnDevice): no addon or no HIP device (remembered for the owner's lifetime), or a
+ * merge list with a token id the device encoder does not hold (>= BPE_MAX_VOCAB: remembered while
+ * the owner keeps that list), so the drop-in encodes wherever the reference does.
  */
 const ENCODE_LDS_TOKENS = 16384
 const ENCODE_DEVICE = process.env.BPE_ENCODE_DEVICE
@@ -82,6 +85,27 @@ function encodeIdsOnDevice(owner, list, tripleOf, ids) {
   return res[0]
 }
 
+/**
+ * encodeIdsOnDevice when the cost model sends the call to the device and the device can take it,
+ * else null (the caller then runs the reference's replay).  A device failure is cached on the owner
+ * (non-enumerable `_enc_failed`): `true` when the encoder itself cannot be made, the list when its
+ * merges cannot be loaded.
+ */
+function encodeIdsMaybeOnDevice(owner, list, tripleOf, ids) {
+  if (!encodeOnDevice(ids.length, list.length)) return null
+  if (ENCODE_DEVICE !== '1' && (owner._enc_failed === true || owner._enc_failed === list))
+    return null
+  try {
+    return encodeIdsOnDevice(owner, list, tripleOf, ids)
+  } catch (e) {
+    if (ENCODE_DEVICE === '1') throw e
+    if (!Object.prototype.hasOwnProperty.call(owner, '_enc_failed'))
+      Object.defineProperty(owner, '_enc_failed', { value: null, writable: true, enumerable: false })
+    owner._enc_failed = owner._encoder ? list : true
+    return null
+  }
+}
+
 /** engine ids -> code point string (code = index + 1, core.ts:149) */
 function idsToCode(ids, begin, end) {
   let parts = []
@@ -119,5 +143,6 @@ module.exports = {
   minWeightArg,
   encodeOnDevice,
   encodeIdsOnDevice,
+  encodeIdsMaybeOnDevice,
   idsToCode,
 }

@@ -209,8 +209,13 @@ class ShardedTrainer:
         self._maintained = False
         self._heavy_streak = 0
         # the incremental mode: the global state lives in every rank's position index (entered at
-        # once, the tables' counts exchanged as signed delta rows: bpe_pix.hip.h)
+        # once, the tables' counts exchanged as signed delta rows: bpe_pix.hip.h).  As in
+        # bpe_multi.cpp: every re-entry builds the index again, so a run whose batches keep handing
+        # over (more than 64 entries since set_mode, at least one per 16 merges) goes on in the
+        # streaming mode (_pix_off), on every rank alike (the entries and merges are global facts)
         self.pix = False
+        self._pix_off = False
+        self._pix_entries = self._pix_merged = 0
         # RCCL backend: the rank loop's two all-reduces per iteration are issued from C++ on the
         # engine's stream (bpe_rank_loop_rccl, one call per batch); BPE_RANK_LOOP=python keeps them
         # as torch.distributed calls (A/B)
@@ -220,6 +225,8 @@ class ShardedTrainer:
         """'stream' or 'incremental' (bpe_set_mode) for this rank's engine; every rank alike."""
         self.engine.set_mode(mode)
         self.pix = mode == 'incremental'
+        self._pix_off = False
+        self._pix_entries = self._pix_merged = 0
         self._maintained = False
 
     @classmethod
@@ -382,7 +389,13 @@ class ShardedTrainer:
         batch = LOOP_BATCH      # (as bpe_merge_until: about twice what an early-ended batch did)
         while len(ms) < n:
             k = min(batch, n - len(ms))
-            if not self._maintained and (self._heavy_streak >= 2 or self.pix):
+            pix = self.pix and not self._pix_off
+            if not self._maintained and (self._heavy_streak >= 2 or pix):
+                if pix:
+                    self._pix_entries += 1
+                    if self._pix_entries > 64 and self._pix_entries > (self._pix_merged + len(ms)) // 16:
+                        self._pix_off = True
+                        self.engine.set_mode('stream')
                 self.enter_maintained()
             batch_maintained = self._maintained
             with torch.cuda.stream(stream):
@@ -426,6 +439,8 @@ class ShardedTrainer:
                 if m is None:
                     break
                 ms.append(m)
+        if self.pix:
+            self._pix_merged += len(ms)
         return ms
 
     def step(self, max_length=0, min_weight=0, info=None):

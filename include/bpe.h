@@ -301,6 +301,12 @@ typedef struct {
     int64_t cold_used;        /* maintained state: claimed entries of the cold-pair table (largest seen) */
     int64_t sel_blocks;       /* maintained state: block maxima recomputed by incremental selections
                                  (cumulative since the context was made) */
+    int64_t xchg_bytes;       /* rank loop: bytes of the per-iteration exchange all-reduced (SUM leg;
+                                 the table, or the maintained state's delta rows), summed over the
+                                 iterations (a multi-device context: over its shards) */
+    int64_t xchg_iters;       /* rank loop: iterations those bytes cover */
+    int64_t pix_fallbacks;    /* multi-device context, incremental mode: times the shards' index kept
+                                 handing over and the run went on in the streaming mode */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -312,3 +312,43 @@ class CpuMT:
     def samples(self):
         ids, off = self.read()
         return [ids[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+
+
+# ---- the rank-greedy batch encoder on the host's cores (oracle/bpe_cpu_encode.cc): the device
+# encoder's CPU baseline, checked against encode() (the in-order replay) by the tests ----------
+LIB_ENC_PATH = os.environ.get('ORACLE_ENC_LIB') or os.path.join(HERE, 'liboracle_enc.so')
+_lib_enc = None
+
+
+def lib_enc():
+    global _lib_enc
+    if _lib_enc is None:
+        if not os.path.exists(LIB_ENC_PATH):
+            build()
+        L = ctypes.CDLL(LIB_ENC_PATH)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.cpu_encode_batch.argtypes = [i32p, i64p, ctypes.c_int64, i32p, ctypes.c_int64, i32p, i64p,
+                                       ctypes.c_int]
+        L.cpu_encode_batch.restype = ctypes.c_int
+        _lib_enc = L
+    return _lib_enc
+
+
+def cpu_encode_flat(ids, off, abc, threads=0):
+    """encodeToCode of the texts ids[off[k]:off[k+1]] through the (a, b, c) merges, rank-greedy on
+    `threads` host threads (0: all).  Returns (packed ids, offsets, threads used)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    abc = np.ascontiguousarray(np.asarray(abc, dtype=np.int32).reshape(-1))
+    n = len(off) - 1
+    out = np.zeros(max(1, int(off[-1] - off[0])), np.int32)
+    oo = np.zeros(n + 1, np.int64)
+    buf = ids if ids.size else np.zeros(1, np.int32)
+    m = abc.size // 3
+    if abc.size == 0:
+        abc = np.zeros(3, np.int32)
+    used = lib_enc().cpu_encode_batch(_p(buf, ctypes.c_int32), _p(off, ctypes.c_int64), n,
+                                      _p(abc, ctypes.c_int32), m, _p(out, ctypes.c_int32),
+                                      _p(oo, ctypes.c_int64), threads)
+    return out[:oo[-1]], oo, used

@@ -1,0 +1,90 @@
+// encodeToCode's default routing in the drop-ins (js/native.js encodeIdsMaybeOnDevice): a call the
+// cost model sends to the device encoder falls back to the reference's replay (core.ts:404-406)
+// when the device cannot take it, with the same result.
+//   node encode_routing.js host   no HIP device: every routed call replays; the owner remembers
+//                                 that the encoder cannot be made (_enc_failed === true)
+//   node encode_routing.js gpu    a device: a list with ids < BPE_MAX_VOCAB encodes on it; a list
+//                                 holding ids >= 55296 (valid in the reference, past the device
+//                                 encoder's table) replays, remembered for that list
+// Run without BPE_ENCODE_DEVICE (the default routing).
+'use strict'
+const assert = require('assert')
+const path = require('path')
+const { BPETokenizer } = require(path.join(__dirname, '..', '..', 'bpe-tokenizer_amd', 'js', 'core.js'))
+
+const mode = process.argv.slice(2).find(a => a === 'host' || a === 'gpu') || 'host'
+assert(!process.env.BPE_ENCODE_DEVICE, 'run with the default routing')
+
+let seed = 12345
+function rnd(n) {
+  seed ^= seed << 13; seed >>>= 0
+  seed ^= seed >>> 17
+  seed ^= seed << 5; seed >>>= 0
+  return seed % n
+}
+
+// a BPETokenizerJSON v2 with n_merges merges over ten chars: every pair of base chars first, then
+// a recent token with a base char (so merges keep firing on a text)
+function makeJSON(n_merges) {
+  const base = 'abcdefghij'
+  const chars = base.split('')
+  const table = chars.map(ch => [ch, 1, 1])
+  const codes = []
+  for (let k = 0; k < n_merges; k++) {
+    const v = chars.length
+    let a, b
+    if (k < 100) { a = Math.floor(k / 10); b = k % 10 } else {
+      a = v - 1 - rnd(Math.min(v, 400))
+      b = rnd(10)
+    }
+    chars.push(chars[a] + chars[b])
+    table.push([chars[a] + chars[b], 1, 1])
+    codes.push([String.fromCodePoint(a + 1), String.fromCodePoint(b + 1), String.fromCodePoint(v + 1)])
+  }
+  return { version: 2, char_count: 10, token_table: table, merge_codes: codes }
+}
+
+function replay(json, text) {
+  let s = ''
+  for (const ch of text) s += String.fromCodePoint('abcdefghij'.indexOf(ch) + 1)
+  for (const [a, b, c] of json.merge_codes) s = s.split(a + b).join(c)
+  return s
+}
+
+function text(n) {
+  let s = ''
+  for (let i = 0; i < n; i++) s += 'abcdefghij'[rnd(10)]
+  return s
+}
+
+// 1) a long list, short texts: the cost model picks the device
+const j1 = makeJSON(2000)
+const t1 = new BPETokenizer()
+t1.fromJSON(j1)
+for (const n of [16, 64, 300]) {
+  const s = text(n)
+  assert.strictEqual(t1.encodeToCode(s), replay(j1, s), 'list 1, ' + n + ' chars')
+}
+if (mode === 'host') {
+  assert.strictEqual(t1._enc_failed, true, 'no device: remembered for the owner')
+} else {
+  assert(!t1._enc_failed, 'device: the list encodes on it')
+  assert(t1._encoder, 'device encoder made')
+}
+
+// 2) a list past the device encoder's ids (55296 = BPE_MAX_VOCAB): replayed, remembered per list
+const j2 = makeJSON(55300 - 10)
+const t2 = new BPETokenizer()
+t2.fromJSON(j2)
+for (const n of [16, 200]) {
+  const s = text(n)
+  assert.strictEqual(t2.encodeToCode(s), replay(j2, s), 'list 2, ' + n + ' chars')
+}
+if (mode === 'host') assert.strictEqual(t2._enc_failed, true)
+else assert.strictEqual(t2._enc_failed, t2.merge_tokens, 'the list is remembered')
+// the same owner with a list the device can take again (fromJSON replaces the list)
+t2.fromJSON(j1)
+const s = text(40)
+assert.strictEqual(t2.encodeToCode(s), replay(j1, s))
+if (mode !== 'host') assert.notStrictEqual(t2._enc_failed, t2.merge_tokens)
+console.log('encode_routing ok', mode)

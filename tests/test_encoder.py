@@ -286,3 +286,23 @@ def test_greedy_equals_replay_cpu(seed):
     want = oracle.encode(texts, merges)
     for t, w in zip(texts, want):
         assert greedy_encode(t.tolist(), merges) == w.tolist()
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_cpu_rank_greedy_equals_replay(seed):
+    """The device encoder's CPU baseline (oracle/bpe_cpu_encode.cc: rank-greedy with a heap of
+    (rank, position), OpenMP over texts) against the replay, on several thread counts."""
+    rng = np.random.default_rng(300 + seed)
+    alphabet = [2, 3, 5, 8, 16, 30][seed]
+    merges = trained_merges(rng, alphabet, 20, 150)
+    texts = random_texts(rng, alphabet, rng.integers(0, 300, size=200)) + \
+        skewed_texts(rng, alphabet, [1, 2, 50, 150, 700])
+    want = oracle.encode(texts, merges)
+    off = np.zeros(len(texts) + 1, np.int64)
+    np.cumsum([len(t) for t in texts], out=off[1:])
+    ids = np.concatenate(texts).astype(np.int32)
+    for threads in (1, 3):
+        got, oo, used = oracle.cpu_encode_flat(ids, off, merges, threads=threads)
+        assert used == threads
+        for k, w in enumerate(want):
+            assert got[oo[k]:oo[k + 1]].tolist() == w.tolist(), (threads, k)

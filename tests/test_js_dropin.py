@@ -18,8 +18,8 @@ def build_addon():
     subprocess.check_call(['make', '-s', '-C', ADDON_DIR])
 
 
-def run_node(script, *flags, timeout=600, env=None):
-    out = subprocess.run([NODE, *flags, os.path.join(ROOT, 'tests', 'js', script)],
+def run_node(script, *flags, timeout=600, env=None, args=()):
+    out = subprocess.run([NODE, *flags, os.path.join(ROOT, 'tests', 'js', script), *args],
                          capture_output=True, text=True, timeout=timeout,
                          env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
@@ -37,14 +37,31 @@ def test_addon_builds_and_exports():
                            'readSamples,sampleLengths,setTokenLen16')
 
 
-# (no device here: encodeToCode keeps the reference's JS replay for every merge-list length;
-# the GPU tests run the same golden vectors through the device encoder)
-HOST_ONLY = {'BPE_ENCODE_DEVICE': '0'}
+# (the default routing: with no device here, every encodeToCode the cost model sends to the
+# device encoder falls back to the reference's JS replay; the GPU tests run the same golden vectors
+# through the device encoder)
+DEFAULT_ROUTING = {'BPE_ENCODE_DEVICE': ''}
 
 
 def test_host_logic_against_golden():
     build_addon()
-    assert 'host_only ok' in run_node('host_only.js', env=HOST_ONLY)
+    assert 'host_only ok' in run_node('host_only.js', env=DEFAULT_ROUTING)
+
+
+def test_encode_routing_falls_back_without_a_device():
+    """encodeToCode with a 2000-merge list on short texts (the cost model picks the device) and with
+    a list past the device encoder's ids (>= 55296): no HIP device here, so each call replays as the
+    reference does, and the owner remembers that the encoder cannot be made."""
+    build_addon()
+    assert 'encode_routing ok host' in run_node('encode_routing.js', env=DEFAULT_ROUTING, args=['host'])
+
+
+@pytest.mark.gpu
+def test_encode_routing_on_the_device():
+    """The same lists with a device: the 2000-merge list encodes on the device encoder, the list
+    with ids >= 55296 falls back to the replay (remembered for that list, not for the owner)."""
+    build_addon()
+    assert 'encode_routing ok gpu' in run_node('encode_routing.js', env=DEFAULT_ROUTING, args=['gpu'])
 
 
 def test_db_twin_host_logic_over_sqlite():
@@ -52,7 +69,7 @@ def test_db_twin_host_logic_over_sqlite():
     tests/js/sqlite_bridge.js): schema, JSON round trips and golden encode/decode vectors, token
     rows and weights, the proxy views, error messages.  No device needed."""
     build_addon()
-    assert 'db_host_only ok' in run_node('db_host_only.js', env=HOST_ONLY)
+    assert 'db_host_only ok' in run_node('db_host_only.js', env=DEFAULT_ROUTING)
 
 
 @pytest.mark.gpu

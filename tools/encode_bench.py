@@ -6,9 +6,11 @@ The merges: mergeUntil({min_weight: 2, max_iterations: M}) on MiB of a synthetic
 incremental mode, identical merges to the streaming one).  The texts: a later, disjoint stretch of
 the same stream cut into texts of random length in [min, max] chars.  Prints one JSON line:
 kernel time (HIP events around the launches), end-to-end time of the call (host packing, copies,
-kernels, unpacking), input tokens/s for both, the greedy steps taken, and the CPU replay
-(oracle_encode: every merge in order over each text, the reference's algorithm) on a bounded sample
-of the same batch, whose outputs must equal the device's.
+kernels, unpacking), input tokens/s for both, the greedy steps taken, and two CPU legs:
+  - cpu_baseline: the same rank-greedy algorithm on the host's cores (oracle/bpe_cpu_encode.cc,
+    bench.encode_cpu_baseline) over every text of the batch, whose outputs must equal the device's;
+  - cpu_replay: the reference's own algorithm (oracle_encode: every merge in order over each text,
+    core.ts:404-406) on a bounded sample, one thread, also checked against the device.
 
 Usage: tools/encode_bench.py [--corpus uniform|zipf] [--mib 256] [--merges 8000] [--texts 100000]
                              [--min 16] [--max 1024] [--reps 5]
@@ -26,6 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'oracle'))
 pkg = importlib.import_module('bpe-tokenizer_amd')
+from bench import encode_cpu_baseline   # noqa: E402
 
 
 def main():
@@ -96,6 +99,7 @@ def main():
                        'tokens_per_s': tok_sample / t_cpu,
                        'what': 'oracle_encode (oracle/bpe_oracle.c): every merge in order, core.ts:404-406'},
         'identical_on_cpu_sample': bool(same),
+        'cpu_baseline': encode_cpu_baseline(ids, off, merges, out, oo),
     }
     enc.close()
     print(json.dumps(res), flush=True)
