@@ -239,6 +239,24 @@ def encode_line(args, merges, n_texts=100000, lo=16, hi=1024, reps=5):
             'cpu_baseline': encode_cpu_baseline(ids, off, abc, out, oo)}
 
 
+def fixture_check(args, merges):
+    """The run's merge list against the threaded CPU restatement's run of the same workload
+    (tests/golden/config3_cpu_mt_8000.json for C3, zipf_cpu_mt_2000.json for the skewed variant;
+    oracle/gen_cpu_mt_fixtures.py): the first min(len) merges must be equal.  None when no
+    fixture covers this workload (another corpus size or alphabet)."""
+    if args.corpus_mib != 1024 or (args.corpus == 'uniform' and args.alphabet != 256):
+        return None
+    name = 'config3_cpu_mt_8000.json' if args.corpus == 'uniform' else 'zipf_cpu_mt_2000.json'
+    path = os.path.join(ROOT, 'tests', 'golden', name)
+    if not os.path.exists(path):
+        return None
+    want = json.load(open(path))['merges']
+    n = min(len(want), len(merges))
+    got = [list(map(int, m)) for m in merges[:n]]
+    return {'fixture': 'tests/golden/' + name, 'merges_compared': n,
+            'merges_match_fixture': got == want[:n]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -378,6 +396,8 @@ def main():
             # triples as int64, warmup merges included)
             'merges_sha256': hashlib.sha256(
                 np.asarray(trainer.merges, dtype=np.int64).tobytes()).hexdigest(),
+            # (the merges of the whole run, warmup included, against the CPU restatement's run)
+            'fixture_check': fixture_check(args, trainer.merges) if world == 1 else None,
             'breakdown_ms_per_step': {
                 'stream_pass': k1_ms * st['step_launches'] / max(1, args.steps),
                 'select': st['select_ms'] / max(1e-9, timed_frac) / max(1, args.steps),

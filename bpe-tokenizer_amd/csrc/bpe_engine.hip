@@ -185,6 +185,9 @@ struct bpe_ctx {
     // between rank loop batches, and the corpus is in the index's slot layout until it is dropped
     bool rl_pix = false;
     uint64_t pix_min_cap = 0;    // (the next index build's least table size)
+    // sharded incremental mode, compact exchange: entries of L and of R the next batch's exchange
+    // holds (0: not known yet, every token id; sized from the largest need of the batches before)
+    int64_t pix_lr_cap = 0;
 };
 
 namespace {
@@ -2245,13 +2248,31 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
         k_pix_sbmax<<<1024, 256, 0, s>>>(P->T, P->B, P->d_ctl, 1);
     }
     P->T.delta = xchg;
-    const int64_t nw = XCHG_HDR + DELTA_ROWS * std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
+    // the exchange: the compact layout (L and R of each merge, k_pix_lr), sized for this batch,
+    // or (BPE_XCHG_DENSE=1, A/B and checks) six dense rows per token id
+    const bool dense = getenv("BPE_XCHG_DENSE") != nullptr;   // (read per batch: tests switch it)
+    const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
+    int64_t nw, lr_cap = 0;
+    if (dense) {
+        P->T.lr_bits = P->T.lr_pre = nullptr;
+        nw = XCHG_HDR + DELTA_ROWS * ids;
+    } else {
+        if (!P->T.lr_bits) {
+            if ((rc = pix_alloc(P, &P->T.lr_bits, 2 * PIX_LR_WORDS))) return rc;
+            if ((rc = pix_alloc(P, &P->T.lr_pre, 2 * (PIX_LR_WORDS + 1)))) return rc;
+            HIP_TRY(hipMemsetAsync(P->T.lr_bits, 0, 2 * PIX_LR_WORDS * sizeof(uint32_t), s));
+            c->rl_delta_pending = false;   // (a fresh index: no merge of the old layout pending)
+        }
+        lr_cap = c->pix_lr_cap > 0 ? std::min(c->pix_lr_cap, ids) : ids;
+        nw = XCHG_HDR + PIX_XCHG_SPECIAL + 4 * lr_cap;
+    }
     // (delta pending: the last batch's last merge's rows are in xchg, for this batch's first
     // all-reduce; else all of it zero: the rows past this batch's words are read by later ones)
     if (!c->rl_delta_pending)
         HIP_TRY(hipMemsetAsync(xchg, 0, XCHG_WORDS * sizeof(unsigned long long), s));
     k_pix_rank_begin<<<1, 1, 0, s>>>(P->d_ctl, LOOP_BATCH, (int32_t)base,
-                                     min_weight == 0 ? 2 : min_weight);   // core.ts:256
+                                     min_weight == 0 ? 2 : min_weight,   // core.ts:256
+                                     (uint32_t)lr_cap);
     HIP_TRY(hipGetLastError());
     c->opt_max_length = max_length;
     c->rl_table = xchg;
@@ -2273,6 +2294,11 @@ int pix_rank_select(bpe_ctx *c) {
     k_pix_apply_delta<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->rl_table);
     k_pix_dirty<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
     k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
+    if (P->T.lr_bits) {
+        // (one thread per token id of the batch's vocabulary)
+        const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, c->rl_base + LOOP_BATCH + 1);
+        k_pix_lr<<<(unsigned)((ids + 255) / 256), 256, 0, s>>>(P->T, P->d_ctl);
+    }
     k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
     k_pix_export<<<1, 64, 0, s>>>(P->d_ctl, c->rl_table, c->rl_tie, c->rl_rank);
     HIP_TRY(hipGetLastError());
@@ -2348,6 +2374,14 @@ int pix_rank_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *st
     }
     c->len16_lo = base + nd;   // (pix_commit wrote the new lengths on the device)
     const int st = h->status == PIX_DONE ? LOOP_DONE : h->status == PIX_HOST ? LOOP_HOST : LOOP_RUN;
+    if (P->T.lr_bits) {
+        // the next batch's capacity: twice the largest need seen in this one (every shard alike:
+        // the sets come from the global counts), shrinking by at most a quarter per batch, so a
+        // merge past it (a hand-off, err 40) stays rare
+        const int64_t need = (int64_t)h->lr_need;
+        const int64_t prev = c->pix_lr_cap > 0 ? c->pix_lr_cap : 2 * need;
+        c->pix_lr_cap = std::max<int64_t>({256, 2 * need, prev * 3 / 4});
+    }
     if (st != LOOP_RUN) {
         static const bool dbg = getenv("BPE_DEBUG_PIX") != nullptr;
         if (dbg)

@@ -65,6 +65,10 @@ static_assert(WAVES_PER_WG * RING * 256 < 49152,
 #endif
 constexpr int LEAD = BPE_LEAD;
 static_assert(LEAD >= 2 && LEAD <= RING - 2, "load lead");
+// (round-5 A/B) MODE_INCR: skip the row adds of a plane with no touched pair
+#ifndef BPE_INCR_PLANE_SKIP
+#define BPE_INCR_PLANE_SKIP 0
+#endif
 // Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
 // pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
 // this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
@@ -1072,6 +1076,9 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 unsigned long long hsh = 0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
+#if BPE_INCR_PLANE_SKIP
+                    if (Wm[e] == 0ull) continue;   // (no touched pair in this plane: df.o[e] stays 0)
+#endif
                     const int32_t xx = x[e], yy = y[e];
                     const bool act = lane_in(Wm[e]);
                     const bool xa = xx == ma, xb = xx == mb, ya = yy == ma, yb = yy == mb;

@@ -25,11 +25,13 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 extern "C" int bpe_leave_global(bpe_ctx *c);
@@ -77,6 +79,8 @@ struct bpe_multi {
     bool pix = false, pix_off = false;
     // (since the last bpe_set_mode: index entries, merges made; fallbacks: times pix_off was set)
     int64_t pix_entries = 0, pix_merged = 0, pix_fallbacks = 0;
+    // the streaming mode went on in the incremental mode past AUTO_PIX_VOCAB token ids (round 5)
+    bool pix_auto = false;
     std::vector<ncclComm_t> comms;
     Rccl rccl;
     // shards sharing one device (the one-GPU test box, BPE_REDUCE_HOST): the exchange is a device
@@ -197,6 +201,102 @@ int all_reduce(bpe_multi *m, std::vector<unsigned long long *> &buf, size_t coun
         MHIP(hipMemcpyAsync(buf[r], m->h_sum, count * 8, hipMemcpyHostToDevice, m->st[r]));
         MHIP(hipStreamSynchronize(m->st[r]));   // (h_sum is reused by the next reduction)
     }
+    return BPE_OK;
+}
+
+// ---- the batch enqueued by one host thread per shard ---------------------------------------------
+// (round 5) Each iteration of the rank loop enqueues about eight launches per shard plus the two
+// exchanges; from one host thread, eight shards' enqueues bounded the one-process driver.  Each
+// shard's thread enqueues its own kernels on its own stream.  The RCCL exchange needs no host
+// coordination (one communicator per thread, as NCCL's one-thread-per-GPU use); the device-kernel
+// exchange of shards sharing a device meets at a spin barrier twice per all-reduce (every shard's
+// event recorded, then shard 0's sum kernel enqueued behind them and its event recorded).
+struct SpinBarrier {
+    explicit SpinBarrier(int n) : n(n) {}
+    int n;
+    std::atomic<int> count{0}, gen{0};
+    std::atomic<bool> abort{false};
+    bool wait() {
+        const int g = gen.load(std::memory_order_acquire);
+        if (count.fetch_add(1, std::memory_order_acq_rel) == n - 1) {
+            count.store(0, std::memory_order_relaxed);
+            gen.fetch_add(1, std::memory_order_release);
+            return !abort.load(std::memory_order_relaxed);
+        }
+        for (int spin = 0; gen.load(std::memory_order_acquire) == g; ++spin) {
+            if (abort.load(std::memory_order_relaxed)) return false;
+            if (spin > 4096) std::this_thread::yield();
+        }
+        return !abort.load(std::memory_order_relaxed);
+    }
+};
+
+constexpr int ABORTED = -1000;   // (another shard's thread failed: this one stops, no message)
+constexpr int32_t AUTO_PIX_VOCAB = 18432;   // (INCR_RLIM, bpe_kernels.hip.h)
+
+int shard_all_reduce(bpe_multi *m, int r, SpinBarrier &bar, std::vector<unsigned long long *> &buf,
+                     size_t count, bool max) {
+    if (m->reduce == BPE_REDUCE_RCCL) {
+        const ncclResult_t e = m->rccl.all_reduce(buf[r], buf[r], count, ncclUint64,
+                                                  max ? ncclMax : ncclSum, m->comms[r], m->st[r]);
+        return nccl_check(m, e, "ncclAllReduce");
+    }
+    // one device: every shard's part, then the sum on shard 0's stream, then every shard after it
+    MHIP(hipEventRecord(m->ev[r], m->st[r]));
+    if (!bar.wait()) return ABORTED;
+    if (r == 0) {
+        for (int q = 0; q < m->n; ++q) MHIP(hipStreamWaitEvent(m->st[0], m->ev[q], 0));
+        MTRY(bpe_sum_shards(buf.data(), m->n, count, max ? 1 : 0, m->st[0]));
+        MHIP(hipEventRecord(m->ev_done, m->st[0]));
+    }
+    if (!bar.wait()) return ABORTED;
+    if (r != 0) MHIP(hipStreamWaitEvent(m->st[r], m->ev_done, 0));
+    return BPE_OK;
+}
+
+// `want` iterations of every shard's rank loop (bpe_rank_loop_begin done on every shard), nw words
+// of exchange per iteration.
+int enqueue_batch(bpe_multi *m, int64_t want, size_t nw) {
+    static const bool one_thread = getenv("BPE_MULTI_ONE_THREAD") != nullptr;   // (A/B knob)
+    if (m->n == 1 || one_thread || (m->reduce != BPE_REDUCE_RCCL && !m->one_device)) {
+        for (int64_t i = 0; i < want; ++i) {
+            MTRY(all_reduce(m, m->d_xchg, nw, false));
+            for (auto s : m->sh) MTRY(bpe_rank_loop_select(s));
+            MTRY(all_reduce(m, m->d_tie, BPE_TIE_WORDS, true));
+            for (auto s : m->sh) MTRY(bpe_rank_loop_decide(s));
+            for (auto s : m->sh) MTRY(bpe_rank_loop_count(s));
+        }
+        return BPE_OK;
+    }
+    SpinBarrier bar(m->n);
+    std::vector<int> rcs(m->n, BPE_OK);
+    std::vector<std::string> msgs(m->n);
+    auto work = [&](int r) {
+        auto run = [&]() -> int {
+            MHIP(hipSetDevice(m->dev[r]));
+            for (int64_t i = 0; i < want; ++i) {
+                MTRY(shard_all_reduce(m, r, bar, m->d_xchg, nw, false));
+                MTRY(bpe_rank_loop_select(m->sh[r]));
+                MTRY(shard_all_reduce(m, r, bar, m->d_tie, BPE_TIE_WORDS, true));
+                MTRY(bpe_rank_loop_decide(m->sh[r]));
+                MTRY(bpe_rank_loop_count(m->sh[r]));
+            }
+            return BPE_OK;
+        };
+        rcs[r] = run();
+        if (rcs[r] < 0 && rcs[r] != ABORTED) {
+            char buf[512];
+            bpe_last_error(buf, sizeof buf);   // (this thread's message: republished by the caller)
+            msgs[r] = buf;
+            bar.abort.store(true);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < m->n; ++r) th.emplace_back(work, r);
+    work(0);
+    for (auto &t : th) t.join();
+    for (int r = 0; r < m->n; ++r)
+        if (rcs[r] < 0 && rcs[r] != ABORTED) return bpe_fail(rcs[r], msgs[r].c_str());
     return BPE_OK;
 }
 
@@ -342,6 +442,7 @@ int multi_shard_count(bpe_multi *m, int *n) {
 int multi_set_mode(bpe_multi *m, int mode) {
     for (auto s : m->sh) MTRY(bpe_set_mode(s, mode));
     m->pix = mode == BPE_MODE_INCREMENTAL;
+    m->pix_auto = false;
     m->pix_off = false;
     m->pix_entries = m->pix_merged = 0;
     m->maintained = false;   // (the next batch enters the mode's own global state)
@@ -784,6 +885,18 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
     while (!max_iterations || n < max_iterations) {
         int32_t nt = 0;
         MTRY(check_vocab(m, &nt));
+        // Past AUTO_PIX_VOCAB token ids the streaming mode's maintained state outgrows its design:
+        // the merge pass's LDS rows index the other token of a pair below 18432 (INCR_RLIM), and
+        // every merge scans all the claimed cold pairs (their invalidation; the selection's block
+        // maxima fall back to full scans past 2^16 blocks), whose number grows with the vocabulary
+        // (8 shards of 512 MiB: 1.0 ms/merge at 4k merges, 5.1 ms/merge at 32k; profiles/
+        // r05_kernel_stats_multi8_32k_stream.csv).  So the shards go on in the incremental mode,
+        // whose merges and counts are the same.  BPE_STREAM_ONLY=1 keeps the stream.
+        static const bool stream_only = getenv("BPE_STREAM_ONLY") != nullptr;
+        if (!m->pix && !stream_only && nt >= AUTO_PIX_VOCAB) {
+            MTRY(multi_set_mode(m, BPE_MODE_INCREMENTAL));
+            m->pix_auto = true;
+        }
         int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)nt);
         if (max_iterations) want = std::min<int64_t>(want, max_iterations - n);
         int status = 2;
@@ -811,13 +924,7 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                 if (nw >= 0 && w_r != nw) return bpe_fail(BPE_ERR_STATE, "bpe native: shards disagree on the exchange");
                 nw = w_r;
             }
-            for (int64_t i = 0; i < want; ++i) {
-                MTRY(all_reduce(m, m->d_xchg, (size_t)nw, false));
-                for (auto s : m->sh) MTRY(bpe_rank_loop_select(s));
-                MTRY(all_reduce(m, m->d_tie, BPE_TIE_WORDS, true));
-                for (auto s : m->sh) MTRY(bpe_rank_loop_decide(s));
-                for (auto s : m->sh) MTRY(bpe_rank_loop_count(s));
-            }
+            MTRY(enqueue_batch(m, want, (size_t)nw));
             int64_t nd = -1;
             for (int r = 0; r < m->n; ++r) {
                 int64_t k = 0;

@@ -56,6 +56,11 @@ struct PixTable {
     // from the summed delta rows (include/bpe.h BPE_XCHG_*); this shard's count changes go to its
     // delta rows (delta != nullptr) instead of cnt.  The lists stay this shard's own.
     unsigned long long *delta;
+    // ... in the compact layout (round 5, lr_bits != nullptr): the merge's left set L (every x
+    // with a pair (x, a)) and right set R (every y with a pair (b, y)) as bitmaps over the token
+    // ids, [L | R] x PIX_LR_WORDS, and their exclusive word prefixes of set bits,
+    // [L | R] x (PIX_LR_WORDS + 1): every shard numbers the same sets alike (k_pix_lr)
+    uint32_t *lr_bits, *lr_pre;
     int32_t *len16;          // UTF-16 lengths (max_length filter)
     long long ml;            // max_length of this index's selections
     uint32_t *keys;
@@ -94,6 +99,10 @@ struct PixCtl {
     // sharded (delta rows): the last merge's rows are still to be added (k_pix_apply_delta); this
     // shard's sites of the merge being made (the header word the shards' sum must equal W in)
     uint32_t merged, pad1;
+    // sharded, compact layout: |L| and |R| of the last merge made; the batch's capacity (entries
+    // of L and of R the exchange holds); the largest max(|L|, |R|) of the batch (the host sizes
+    // the next batch from it); k_pix_lr's last-block ticket
+    uint32_t lr_n[2], lr_cap, lr_need, lr_ticket, pad2;
 };
 
 __device__ __forceinline__ uint32_t pix_key(int32_t u, int32_t v) {
@@ -179,11 +188,48 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
 // A shard of a sharded corpus: the change goes to this shard's delta row of the pair (every pair a
 // merge (a, b) -> c changes has a side in {a, b, c}: delta_slot), summed over the shards and added
 // to every shard's global counts by k_pix_apply_delta.
-__device__ __forceinline__ void pix_delta(const PixTable &t, const PixCtl *ctl, uint32_t key,
-                                          long long d) {
-    if (d) atomicAdd(&t.delta[delta_slot((int32_t)(key >> 16), (int32_t)(key & 0xFFFFu), ctl->a,
-                                         ctl->b, ctl->c)],
-                     (unsigned long long)d);
+// The compact layout of the exchange (round 5): HDR, then PIX_XCHG_SPECIAL words for the pairs of
+// two of {a, b, c}, then four words per entry j: (L_j, a), (L_j, c), (b, R_j), (c, R_j), where L_j
+// / R_j is the j-th id of L / R in increasing order.  Every pair a merge (a, b) -> c changes is
+// one of these: a site's left neighbour l loses (l, a) and gains (l, c), and l is
+// in L since (l, a) occurs; its right neighbour r loses (b, r) and gains (c, r) (a == b: (a, r));
+// chains, runs and the new (c, c) pair only ids of {a, b, c}.  So the exchange carries
+// 4 max(|L|, |R|) words instead of six dense rows per token id.
+constexpr uint32_t PIX_LR_WORDS = (55296 + 31) / 32;   // (BPE_MAX_VOCAB ids)
+constexpr uint32_t PIX_XCHG_SPECIAL = 16;
+
+__device__ __forceinline__ uint32_t lr_index(const uint32_t *bits, const uint32_t *pre, uint32_t x) {
+    const uint32_t w = x >> 5, bit = 1u << (x & 31u), word = bits[w];
+    return (word & bit) ? pre[w] + (uint32_t)__popc(word & (bit - 1u)) : PIX_NONE;
+}
+
+// exchange word of pair (x, y) in the compact layout (PIX_NONE: not a pair of this merge)
+__device__ __forceinline__ uint32_t lr_slot(const PixTable &t, int32_t a, int32_t b, int32_t c,
+                                            int32_t x, int32_t y) {
+    const int sx = x == a ? 0 : x == b ? 1 : x == c ? 2 : 3;
+    const int sy = y == a ? 0 : y == b ? 1 : y == c ? 2 : 3;
+    if (sx < 3 && sy < 3) return XCHG_HDR + 3 * sx + sy;
+    uint32_t j = PIX_NONE, r = 0;
+    if (sx == 3 && (sy == 0 || sy == 2)) {            // (x, a), (x, c)
+        j = lr_index(t.lr_bits, t.lr_pre, (uint32_t)x);
+        r = sy == 0 ? 0u : 1u;
+    } else if (sy == 3 && (x == b || sx == 2)) {       // (b, y), (c, y)
+        j = lr_index(t.lr_bits + PIX_LR_WORDS, t.lr_pre + PIX_LR_WORDS + 1, (uint32_t)y);
+        r = sx == 2 ? 3u : 2u;
+    }
+    return j == PIX_NONE ? PIX_NONE : XCHG_HDR + PIX_XCHG_SPECIAL + 4 * j + r;
+}
+
+__device__ __forceinline__ void pix_delta(const PixTable &t, PixCtl *ctl, uint32_t key, long long d) {
+    if (!d) return;
+    const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
+    const uint32_t slot = t.lr_bits ? lr_slot(t, ctl->a, ctl->b, ctl->c, x, y)
+                                    : delta_slot(x, y, ctl->a, ctl->b, ctl->c);
+    if (slot == PIX_NONE) {
+        pix_fail(ctl, 41);   // (cannot happen: every changed pair has its word)
+        return;
+    }
+    atomicAdd(&t.delta[slot], (unsigned long long)d);
 }
 
 __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
@@ -1594,13 +1640,115 @@ __global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restr
 //   rank_loop_count    k_pix_alloc, k_pix_apply (this shard's corpus and lists)
 constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
 
-// the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on
-__global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight) {
+// the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on; lr_cap
+// entries of L and of R in the compact exchange (0: the dense rows)
+__global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight,
+                                 uint32_t lr_cap) {
     if (ctl->status == PIX_PAUSE) ctl->status = PIX_RUN;
     ctl->n_done = 0;
     ctl->n_want = n;
     ctl->next_id = next_id;
     ctl->min_weight = min_weight;
+    ctl->lr_cap = lr_cap;
+    ctl->lr_need = 0;
+}
+
+// The compact exchange's sets of the merge (a, b) -> c just decided (k_pix_select), from the
+// GLOBAL counts every shard holds alike: L = {x : (x, a) occurs}, R = {y : (b, y) occurs}, ids of
+// {a, b, c} aside, as bitmaps; the last block writes their word prefixes and sizes, and hands the
+// iteration to the host when either set exceeds the batch's capacity (every shard alike: before
+// any shard applies the merge).  Runs between k_pix_select and k_pix_sites.
+__global__ void __launch_bounds__(256) k_pix_lr(PixTable t, PixCtl *ctl) {
+    __shared__ uint32_t s_go, s_last;
+    __shared__ uint32_t s_sum[2][4];
+    if (threadIdx.x == 0) s_go = ctl->status == PIX_RUN && ctl->tie == PIX_TIE_NONE;
+    __syncthreads();
+    if (!s_go) return;
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    const uint32_t nid = (uint32_t)c + 1u, nw = (nid + 31u) / 32u;
+    const int lane = threadIdx.x & 63;
+    // (one id per thread; a wave's ballots are two whole words: 64-aligned ids per wave)
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nw * 32u; x += gridDim.x * blockDim.x) {
+        bool in_l = false, in_r = false;
+        if (x < nid && (int32_t)x != a && (int32_t)x != b && (int32_t)x != c) {
+            const PixProbe pl = pix_probe(t, pix_key((int32_t)x, a));
+            const PixProbe pr = pix_probe(t, pix_key(b, (int32_t)x));
+            const uint32_t sl = pix_slot(t, ctl, pix_key((int32_t)x, a), false, false, pl);
+            const uint32_t sr = pix_slot(t, ctl, pix_key(b, (int32_t)x), false, false, pr);
+            in_l = sl != PIX_NONE && t.cnt[sl] != 0;
+            in_r = sr != PIX_NONE && t.cnt[sr] != 0;
+        }
+        const unsigned long long ml = __ballot(in_l), mr = __ballot(in_r);
+        if ((lane & 31) == 0 && (x >> 5) < nw) {
+            t.lr_bits[x >> 5] = (uint32_t)(ml >> lane);
+            t.lr_bits[PIX_LR_WORDS + (x >> 5)] = (uint32_t)(mr >> lane);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(&ctl->lr_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    // exclusive prefixes of the words' set bits: each thread a contiguous range of words
+    const uint32_t per = (nw + blockDim.x - 1) / blockDim.x;
+    const uint32_t w0 = min(nw, threadIdx.x * per), w1 = min(nw, w0 + per);
+    uint32_t cl = 0, cr = 0;
+    for (uint32_t w = w0; w < w1; ++w) {
+        cl += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        cr += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[PIX_LR_WORDS + w], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+    }
+    const int wv = threadIdx.x >> 6;
+    uint32_t il = wave_incl_sum((int)cl, lane), ir = wave_incl_sum((int)cr, lane);
+    if (lane == 63) {
+        s_sum[0][wv] = il;
+        s_sum[1][wv] = ir;
+    }
+    __syncthreads();
+    uint32_t bl = 0, br = 0, tl = 0, tr = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (q < wv) {
+            bl += s_sum[0][q];
+            br += s_sum[1][q];
+        }
+        tl += s_sum[0][q];
+        tr += s_sum[1][q];
+    }
+    uint32_t el = bl + il - cl, er = br + ir - cr;   // (exclusive, this thread's first word)
+    for (uint32_t w = w0; w < w1; ++w) {
+        t.lr_pre[w] = el;
+        t.lr_pre[PIX_LR_WORDS + 1 + w] = er;
+        el += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        er += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[PIX_LR_WORDS + w], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+    }
+    if (threadIdx.x == 0) {
+        t.lr_pre[nw] = tl;
+        t.lr_pre[PIX_LR_WORDS + 1 + nw] = tr;
+        ctl->lr_n[0] = tl;
+        ctl->lr_n[1] = tr;
+        const uint32_t need = max(tl, tr);
+        ctl->lr_need = max(ctl->lr_need, need);
+        if (need > ctl->lr_cap) pix_fail(ctl, 40);   // (the next batch holds it: bpe_engine.hip)
+        ctl->lr_ticket = 0;
+    }
+}
+
+// the j-th id of a set (bits, pre over nw words)
+__device__ __forceinline__ int32_t lr_select(const uint32_t *bits, const uint32_t *pre, uint32_t nw,
+                                             uint32_t j) {
+    uint32_t lo = 0, hi = nw;   // the word w with pre[w] <= j < pre[w + 1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    uint32_t word = bits[lo];
+    for (uint32_t k = j - pre[lo]; k; --k) word &= word - 1u;
+    return (int32_t)(32u * lo + (uint32_t)__ffs(word) - 1u);
 }
 
 // The summed delta rows of the last merge (a, b) -> c into this shard's global counts: a fall marks
@@ -1624,16 +1772,38 @@ __global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, 
         }
     }
     unsigned long long *d = xchg + XCHG_HDR;
-    const uint32_t n = (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);   // other tokens <= c
+    // (compact: the sets of the last merge are still those k_pix_lr made for it)
+    const bool lr = t.lr_bits != nullptr;
+    const uint32_t nw = ((uint32_t)c + 32u) / 32u;
+    const uint32_t n = lr ? PIX_XCHG_SPECIAL + 4u * max(ctl->lr_n[0], ctl->lr_n[1])
+                          : (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);   // other tokens <= c
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const unsigned long long v = d[i];
         if (!v) continue;
         d[i] = 0;
-        const uint32_t row = i % DELTA_ROWS;
-        const int32_t o = (int32_t)(i / DELTA_ROWS);
-        const int32_t m = row == 0 || row == 2 ? a : row == 1 || row == 3 ? b : c;
-        const bool left = row == 0 || row == 1 || row == 4;   // (m, o), else (o, m)
-        const uint32_t key = pix_key(left ? m : o, left ? o : m);
+        uint32_t key;
+        if (lr) {
+            if (i < PIX_XCHG_SPECIAL) {
+                if (i >= 9) continue;   // (never written)
+                const int32_t abc[3] = {a, b, c};
+                key = pix_key(abc[i / 3], abc[i % 3]);
+            } else {
+                const uint32_t j = (i - PIX_XCHG_SPECIAL) >> 2, r = (i - PIX_XCHG_SPECIAL) & 3u;
+                if (r < 2) {
+                    const int32_t o = lr_select(t.lr_bits, t.lr_pre, nw, j);
+                    key = pix_key(o, r ? c : a);
+                } else {
+                    const int32_t o = lr_select(t.lr_bits + PIX_LR_WORDS, t.lr_pre + PIX_LR_WORDS + 1, nw, j);
+                    key = pix_key(r == 2 ? b : c, o);
+                }
+            }
+        } else {
+            const uint32_t row = i % DELTA_ROWS;
+            const int32_t o = (int32_t)(i / DELTA_ROWS);
+            const int32_t m = row == 0 || row == 2 ? a : row == 1 || row == 3 ? b : c;
+            const bool left = row == 0 || row == 1 || row == 4;   // (m, o), else (o, m)
+            key = pix_key(left ? m : o, left ? o : m);
+        }
         const bool rise = (long long)v > 0;
         const uint32_t s = pix_slot(t, ctl, key, rise, true);
         if (s == PIX_NONE) {   // (a fall of a pair no shard holds: the tables disagree)

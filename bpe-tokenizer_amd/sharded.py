@@ -41,6 +41,7 @@ HOT_BINS = 256 * 256
 TABLE_BINS = HOT_BINS + 16384
 MAX_CAND = 16            # BPE_MAX_CAND: tie positions all-reduced per iteration
 LOOP_BATCH = 64          # BPE_LOOP_BATCH: iterations per host round trip of the rank loop
+AUTO_PIX_VOCAB = 18432   # the streaming mode goes on in the incremental mode here (bpe_multi.cpp)
 RANK_SHIFT = 40          # global position = rank << 40 | shard-local position
 
 
@@ -389,6 +390,12 @@ class ShardedTrainer:
         batch = LOOP_BATCH      # (as bpe_merge_until: about twice what an early-ended batch did)
         while len(ms) < n:
             k = min(batch, n - len(ms))
+            # (as bpe_multi.cpp: past AUTO_PIX_VOCAB token ids the streaming mode's maintained state
+            # outgrows its LDS rows and its scans of the claimed cold pairs; the ranks go on in the
+            # incremental mode, same merges.  BPE_STREAM_ONLY=1 keeps the stream)
+            if (not self.pix and self.n_tokens >= AUTO_PIX_VOCAB
+                    and not os.environ.get('BPE_STREAM_ONLY')):
+                self.set_mode('incremental')
             pix = self.pix and not self._pix_off
             if not self._maintained and (self._heavy_streak >= 2 or pix):
                 if pix:

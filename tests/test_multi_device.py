@@ -1,7 +1,8 @@
 """One corpus sharded over several shards behind ONE context (bpe_create_multi, include/bpe.h):
 the drop-in's BPE_NUM_GPUS path.  On the one-GPU test box the shards share device 0 and exchange
-their tables through host copies (BPE_REDUCE_HOST); the RCCL exchange (one shard per device) runs
-only where several devices exist.  Every result must equal the oracle's on the whole corpus."""
+their tables through a device kernel (BPE_REDUCE_HOST: bpe_sum_shards, ordered by events), or a
+1-rank RCCL communicator; the RCCL exchange over several devices runs only where they exist.
+Every result must equal the oracle's on the whole corpus."""
 import os
 import random
 
@@ -295,12 +296,47 @@ def test_incremental_mode_over_shards(shards, corpus, n, max_length):
     multi.close()
 
 
+def test_incremental_exchange_compact_vs_dense_rows(monkeypatch):
+    """The sharded incremental mode's exchange in its compact layout (round 5: per merge, L = the
+    ids x with a pair (x, a) and R = the ids y with a pair (b, y), numbered alike on every shard
+    from the global counts; 4 words per entry) against the dense delta rows (6 per token id,
+    BPE_XCHG_DENSE=1): the same merges and corpus as one context, and fewer bytes per merge."""
+    data = pkg.synth_latin1(16 << 20, seed=4242, A=96, base=32)
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    want = one.merge_until(0, 2, 1500)
+    ids1, _ = one.read_corpus()
+    one.close()
+    per_merge = {}
+    for layout in ('dense', 'compact'):
+        if layout == 'dense':
+            monkeypatch.setenv('BPE_XCHG_DENSE', '1')
+        else:
+            monkeypatch.delenv('BPE_XCHG_DENSE', raising=False)
+        multi = pkg.Engine(devices=[0] * 4, reduce='host')
+        multi.add_latin1(data, sample_bytes=1 << 20)
+        multi.set_mode('incremental')
+        multi.stats_enable(True)
+        got = multi.merge_until(0, 2, 1500)
+        st = multi.stats()
+        assert got == want, layout
+        ids, _ = multi.read_corpus()
+        assert np.array_equal(ids, ids1), layout
+        assert st['pix_merges'] >= 4 * 1400 and st['xchg_iters'] >= 1400, st
+        # (xchg_bytes is summed over the 4 shards)
+        per_merge[layout] = st['xchg_bytes'] / 4 / st['xchg_iters']
+        multi.close()
+    # (a small vocabulary: the dense rows are short too; the 32k-vocabulary test reports the gap)
+    assert per_merge['compact'] < per_merge['dense'], per_merge
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize('mode', ['stream', 'pix'])
 def test_eight_shards_to_the_32k_vocabulary(mode):
-    """8 shards of the C5 stream on one device (host-copy exchange, the same rank loop as RCCL
-    over 8 GPUs) taken to the 32k-token vocabulary: past the sketch's reach the shards keep the
-    global tables themselves (maintained state), so the iterations stay in the device loop
+    """8 shards of the C5 stream on one device (exchanged by a device kernel, the same rank loop
+    as RCCL over 8 GPUs; one enqueue thread per shard) taken to the 32k-token vocabulary: past the
+    sketch's reach the shards keep the global tables themselves (maintained state; past 18432 ids
+    the streaming mode goes on in the incremental mode), so the iterations stay in the device loop
     (few host hand-offs); merges and final corpus equal one context's."""
     n = 512 << 20
     data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
@@ -324,6 +360,11 @@ def test_eight_shards_to_the_32k_vocabulary(mode):
     assert st['loop_host'] <= 24, st
     if mode == 'pix':   # (summed over the 8 shards)
         assert st['pix_merges'] > 8 * 30000, st
+        # the compact exchange: bytes per merge over the run (was 6 dense rows per token id:
+        # 1.57 MB per merge at the 32k vocabulary)
+        print('exchange bytes per merge: %.0f' % (st['xchg_bytes'] / 8 / max(1, st['xchg_iters'])))
     else:
-        assert st['fused_passes'] > 8 * 10000, st
+        # the streaming mode's maintained state up to AUTO_PIX_VOCAB (18432) token ids, then the
+        # incremental mode (bpe_multi.cpp: the maintained state outgrows its LDS rows there)
+        assert st['fused_passes'] > 8 * 9000 and st['pix_merges'] > 8 * 14000, st
     multi.close()

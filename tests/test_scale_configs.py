@@ -1,12 +1,14 @@
 """BASELINE configs 3, 4 and 5 at their full sizes on one MI355X (core.ts:365-383, mergeUntil).
 
-  C3 — 1 GiB, the device loop (and the incremental mode) for 1000 merges against the threaded CPU
-       restatement's run (tests/golden/config3_cpu_mt_1000.json: merges, live tokens and the
-       SHA-256 of the final corpus).  The restatement is pinned to the reference's own first C3
-       merges (config3_prefix.json) and to every golden case (tests/test_oracle_mt.py).
+  C3 — 1 GiB, the device loop (and the incremental mode) for 1000 merges, and for the whole run of
+       8000, against the threaded CPU restatement's run (tests/golden/config3_cpu_mt_1000.json,
+       config3_cpu_mt_8000.json: merges, live tokens and the SHA-256 of the final corpus); the
+       skewed variant (Zipf words) for 2000 merges (zipf_cpu_mt_2000.json).  The restatement is
+       pinned to the reference's own first C3 merges (config3_prefix.json) and to every golden
+       case (tests/test_oracle_mt.py).
   C4 — 4 GiB sharded 4 ways behind one context (bpe_create_multi): on the one-GPU box the four
-       shards share device 0 and exchange through host copies, the same rank loop and protocol
-       as the RCCL exchange over 4 GPUs.  200 merges against config4_cpu_mt_200.json and against
+       shards share device 0 and exchange through a device kernel (bpe_sum_shards), the same rank
+       loop and protocol as the RCCL exchange over 4 GPUs.  200 merges against config4_cpu_mt_200.json and against
        one context over the whole corpus.
   C5 — 16 GiB sharded 8 ways the same way (64 GiB of int32 slots per corpus copy), 200 merges
        against one context and the restatement's first merges on the host; and one GPU's C5
@@ -67,6 +69,58 @@ def test_config3_1000_merges_vs_cpu_restatement(mode):
     else:
         assert st['pix_merges'] == len(g['merges']), st
     e.close()
+
+
+def run_against_fixture(g, data, mode):
+    """mergeUntil({min_weight}) for the fixture's merges on one context, in the device loop or the
+    incremental mode: the merge list, the live tokens and the final corpus's SHA-256 must equal
+    the threaded CPU restatement's run."""
+    e, _, nt = engine(data)
+    del data
+    assert nt == g['char_count']
+    if mode == 'pix':
+        e.set_mode('incremental')
+    got = e.merge_until(0, g['min_weight'], len(g['merges']))
+    assert [list(m) for m in got] == g['merges']
+    assert hashlib.sha256(np.asarray(got, dtype=np.int64).tobytes()).hexdigest() == g['merges_sha256']
+    assert e.corpus_size()[1] == g['live_tokens_after']
+    ids, off = e.read_corpus()
+    assert hashlib.sha256(np.ascontiguousarray(ids, '<i4').tobytes()).hexdigest() == g['sha256_ids_after']
+    assert hashlib.sha256(np.ascontiguousarray(off, '<i8').tobytes()).hexdigest() == g['sha256_offsets_after']
+    st = e.stats()
+    e.close()
+    return st
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(GOLDEN, 'config3_cpu_mt_8000.json')),
+                    reason='fixture not generated (oracle/gen_cpu_mt_fixtures.py c3_8000)')
+@pytest.mark.parametrize('mode', ['loop', 'pix'])
+def test_config3_all_8000_merges_vs_cpu_restatement(mode):
+    """The whole headline run (BASELINE config 3: 1 GiB, 8000 merges, the bench's workload) against
+    the threaded CPU restatement's: every merge, including the ~370 R3 tie decisions and the 12
+    compactions of the streaming mode, and the final corpus."""
+    g = fixture('config3_cpu_mt_8000.json')
+    st = run_against_fixture(g, pkg.synth_latin1(g['bytes'], seed=g['seed'], A=g['alphabet'], base=0),
+                             mode)
+    if mode == 'loop':
+        assert st['loop_host'] <= 4 and st['compactions'] >= 10 and st['tie_passes'] >= 100, st
+    else:
+        assert st['pix_merges'] == len(g['merges']), st
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(GOLDEN, 'zipf_cpu_mt_2000.json')),
+                    reason='fixture not generated (oracle/gen_cpu_mt_fixtures.py zipf_2000)')
+@pytest.mark.parametrize('mode', ['loop', 'pix'])
+def test_zipf_2000_merges_vs_cpu_restatement(mode):
+    """The skewed variant of config 3 (1 GiB of Zipf(1.1) words, bench.py --corpus zipf) for 2000
+    merges against the CPU restatement: the streaming mode's maintained state (hot and cold tables
+    kept merge by merge, MODE_INCR passes) and the incremental mode with its heavy-merge prefix."""
+    g = fixture('zipf_cpu_mt_2000.json')
+    st = run_against_fixture(g, pkg.synth_zipf(g['bytes'], seed=g['seed']), mode)
+    if mode == 'loop':
+        assert st['fused_passes'] > 1000, st
+    else:
+        assert st['pix_merges'] > 0, st
 
 
 def test_config4_four_shards_vs_one_context_and_cpu_restatement():

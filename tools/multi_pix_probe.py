@@ -35,7 +35,10 @@ def main():
         print(json.dumps({'merges': done, 'chunk_s': round(dt, 3), 'ms_per_merge': dt * 1e3 / max(1, len(got)),
                           'last_w': got[-1][2] if got else None, 'pix_merges': st['pix_merges'],
                           'pix_builds': st['pix_builds'], 'pix_host': st['pix_host'],
-                          'loop_host': st['loop_host']}), flush=True)
+                          'loop_host': st['loop_host'],
+                          # (the exchange each shard all-reduces per iteration, over the run so far)
+                          'xchg_bytes_per_iter': st['xchg_bytes'] / shards / max(1, st['xchg_iters'])}),
+              flush=True)
         if len(got) < k:
             break
     print(json.dumps({'total_s': time.perf_counter() - t_all, 'merges': done, 'mode': mode,

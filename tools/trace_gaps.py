@@ -58,13 +58,25 @@ def main():
                              'avg_gap_before_us': (sum(g) / len(g) / 1e3) if g else None,
                              'total_gap_ms': sum(g) / 1e6}
     out['busy_ms'] = sum(v['total_ms'] for v in out['kernels'].values())
+    # the time some kernel runs (the union of the intervals: kernels of several queues overlap)
+    u, cur_s, cur_e = 0, None, None
+    for s, e, _n, _q in rows:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                u += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        u += cur_e - cur_s
+    out['union_busy_ms'] = u / 1e6
     out['gaps_ms'] = sum(v['total_gap_ms'] for v in out['kernels'].values())
     txt = json.dumps(out, indent=1)
     if len(args) > 1:
         with open(args[1], 'w') as f:
             f.write(txt)
-    print('launches %d  span %.1f ms  busy %.1f ms  gaps %.1f ms' % (len(rows), out['span_ms'], out['busy_ms'],
-                                                                   out['gaps_ms']))
+    print('launches %d  span %.1f ms  busy %.1f ms (union %.1f ms)  gaps %.1f ms'
+          % (len(rows), out['span_ms'], out['busy_ms'], out['union_busy_ms'], out['gaps_ms']))
     for n, v in list(out['kernels'].items())[:14]:
         print('%-60s %6d  %9.2f us  gap %s' % (n[:60], v['calls'], v['avg_us'],
                                                '%.2f us' % v['avg_gap_before_us'] if v['avg_gap_before_us'] is not None else '-'))
