@@ -2248,8 +2248,8 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
         k_pix_sbmax<<<1024, 256, 0, s>>>(P->T, P->B, P->d_ctl, 1);
     }
     P->T.delta = xchg;
-    // the exchange: the compact layout (L and R of each merge, k_pix_lr), sized for this batch,
-    // or (BPE_XCHG_DENSE=1, A/B and checks) six dense rows per token id
+    // the exchange: the compact layout (a count per member of L and of R of each merge, k_pix_lr),
+    // sized for this batch, or (BPE_XCHG_DENSE=1, A/B and checks) six dense rows per token id
     const bool dense = getenv("BPE_XCHG_DENSE") != nullptr;   // (read per batch: tests switch it)
     const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
     int64_t nw, lr_cap = 0;
@@ -2258,13 +2258,14 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
         nw = XCHG_HDR + DELTA_ROWS * ids;
     } else {
         if (!P->T.lr_bits) {
-            if ((rc = pix_alloc(P, &P->T.lr_bits, 2 * PIX_LR_WORDS))) return rc;
-            if ((rc = pix_alloc(P, &P->T.lr_pre, 2 * (PIX_LR_WORDS + 1)))) return rc;
-            HIP_TRY(hipMemsetAsync(P->T.lr_bits, 0, 2 * PIX_LR_WORDS * sizeof(uint32_t), s));
+            if ((rc = pix_alloc(P, &P->T.lr_bits, 4 * PIX_LR_WORDS))) return rc;
+            if ((rc = pix_alloc(P, &P->T.lr_pre, 4 * (PIX_LR_WORDS + 1)))) return rc;
+            HIP_TRY(hipMemsetAsync(P->T.lr_bits, 0, 4 * PIX_LR_WORDS * sizeof(uint32_t), s));
             c->rl_delta_pending = false;   // (a fresh index: no merge of the old layout pending)
         }
-        lr_cap = c->pix_lr_cap > 0 ? std::min(c->pix_lr_cap, ids) : ids;
-        nw = XCHG_HDR + PIX_XCHG_SPECIAL + 4 * lr_cap;
+        // (words after the specials: at most one per member of L and of R, each at most ids)
+        lr_cap = c->pix_lr_cap > 0 ? std::min(c->pix_lr_cap, 2 * ids) : 2 * ids;
+        nw = XCHG_HDR + PIX_XCHG_SPECIAL + lr_cap;
     }
     // (delta pending: the last batch's last merge's rows are in xchg, for this batch's first
     // all-reduce; else all of it zero: the rows past this batch's words are read by later ones)
@@ -2375,12 +2376,20 @@ int pix_rank_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *st
     c->len16_lo = base + nd;   // (pix_commit wrote the new lengths on the device)
     const int st = h->status == PIX_DONE ? LOOP_DONE : h->status == PIX_HOST ? LOOP_HOST : LOOP_RUN;
     if (P->T.lr_bits) {
-        // the next batch's capacity: twice the largest need seen in this one (every shard alike:
-        // the sets come from the global counts), shrinking by at most a quarter per batch, so a
-        // merge past it (a hand-off, err 40) stays rare
+        // the next batch's capacity: 1.25 times the most words a merge of this one took (every
+        // shard alike: the sets come from the global counts), shrinking by at most a quarter per
+        // batch, and no more than every id in both sets with narrow lanes takes unless a merge
+        // needed more (wide members); a merge past it pauses the batch (k_pix_lr) and is made in
+        // the next one
         const int64_t need = (int64_t)h->lr_need;
         const int64_t prev = c->pix_lr_cap > 0 ? c->pix_lr_cap : 2 * need;
-        c->pix_lr_cap = std::max<int64_t>({256, 2 * need, prev * 3 / 4});
+        const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, (int64_t)c->h_len16.size() + LOOP_BATCH + 1);
+        const int64_t narrow_all = 2 * ((ids + 3) / 4);
+        c->pix_lr_cap = std::max<int64_t>({64, need + need / 4 + 16, prev * 3 / 4});
+        if (need <= narrow_all) c->pix_lr_cap = std::min(c->pix_lr_cap, narrow_all);
+        // (BPE_XCHG_TIGHT=1, tests: exactly the largest need, so that merges pause often)
+        if (getenv("BPE_XCHG_TIGHT") != nullptr) c->pix_lr_cap = std::max<int64_t>(1, need);
+        if (c->stats_on) c->stats.xchg_pauses += h->lr_pauses;
     }
     if (st != LOOP_RUN) {
         static const bool dbg = getenv("BPE_DEBUG_PIX") != nullptr;

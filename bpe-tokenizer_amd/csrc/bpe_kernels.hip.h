@@ -65,10 +65,6 @@ static_assert(WAVES_PER_WG * RING * 256 < 49152,
 #endif
 constexpr int LEAD = BPE_LEAD;
 static_assert(LEAD >= 2 && LEAD <= RING - 2, "load lead");
-// (round-5 A/B) MODE_INCR: skip the row adds of a plane with no touched pair
-#ifndef BPE_INCR_PLANE_SKIP
-#define BPE_INCR_PLANE_SKIP 0
-#endif
 // Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
 // pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
 // this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
@@ -1076,9 +1072,9 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                 unsigned long long hsh = 0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-#if BPE_INCR_PLANE_SKIP
-                    if (Wm[e] == 0ull) continue;   // (no touched pair in this plane: df.o[e] stays 0)
-#endif
+                    // a plane with no touched pair adds nothing (its df.o[e] stays 0): 3 % of
+                    // the skewed corpus's pass (profiles/r05_ab_zipf_plane_skip.txt)
+                    if (Wm[e] == 0ull) continue;
                     const int32_t xx = x[e], yy = y[e];
                     const bool act = lane_in(Wm[e]);
                     const bool xa = xx == ma, xb = xx == mb, ya = yy == ma, yb = yy == mb;
@@ -1185,10 +1181,10 @@ __device__ __forceinline__ void tag_tail(int32_t (&y)[4], int total, int32_t las
 
 // Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
 // in place: nxt = the first pre-merge live token after it (the next region's first for the last
-// chunk).  A touched chunk is re-packed and written back.  key = pack_pair_s(ma, mb).
+// chunk).  A touched chunk is re-packed and written back.
 template <int MERGE>
 __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, int32_t mb,
-                                            int32_t mc, uint32_t key,
+                                            int32_t mc,
                                             const __amdgpu_buffer_rsrc_t rs, int c, int lane,
                                             Apply &ap) {
 #ifdef BPE_PROBE_NOAPPLY
@@ -1202,10 +1198,13 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
     // The common case, no (a, b) in the chunk: four packed (slot, right neighbour) compares.  In a
     // partial chunk lane 63's slot 3 (dead) stands in for the last live slot, paired with nxt.
     // (A tail tag can alias a token in its low half; such a false hit only takes the exact path.)
+    // (Testing for `a` alone, four compares instead of eight VALU, timed 2 % slower on C3 and zipf
+    // C3: a chunk holding `a` without (a, b) then pays the full test; profiles/r05_ab_acheck.txt.)
     {
         const int32_t r3 = from_next(w.t[0], nxt);
         const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
         const int32_t x3 = sel(lane_in(P63), w.last, w.t[3]);
+        const uint32_t key = pack_pair_s(ma, mb);
         const unsigned long long H =
             __ballot(pack_pair(w.t[0], w.t[1]) == key) | __ballot(pack_pair(w.t[1], w.t[2]) == key) |
             __ballot(pack_pair(w.t[2], w.t[3]) == key) | __ballot(pack_pair(x3, r3) == key);
@@ -1392,7 +1391,6 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             }
             return v;
         };
-        const uint32_t key = pack_pair_s(ma, mb);
         // Ring of RING slots: stage c applies chunk c (cur), counts chunk c-1 (prv) and loads chunk
         // c+RING-3 into the slot of chunk c-3 (fre), which the previous stage freed, so the load
         // can issue at once without its registers overlapping a chunk still in use.  Stage i of a
@@ -1435,8 +1433,8 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 cur.last = NONE;
             }
             if (MERGE && cur.len)
-                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, key,
-                                   rs, c, lane, ap);
+                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs, c,
+                                   lane, ap);
             if (cur.len) {
                 if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, df);
             } else {

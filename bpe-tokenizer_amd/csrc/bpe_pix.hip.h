@@ -57,9 +57,11 @@ struct PixTable {
     // delta rows (delta != nullptr) instead of cnt.  The lists stay this shard's own.
     unsigned long long *delta;
     // ... in the compact layout (round 5, lr_bits != nullptr): the merge's left set L (every x
-    // with a pair (x, a)) and right set R (every y with a pair (b, y)) as bitmaps over the token
-    // ids, [L | R] x PIX_LR_WORDS, and their exclusive word prefixes of set bits,
-    // [L | R] x (PIX_LR_WORDS + 1): every shard numbers the same sets alike (k_pix_lr)
+    // with a pair (x, a)) and right set R (every y with a pair (b, y)), and their wide members
+    // (global count of the pair > 0xFFFF), as bitmaps over the token ids,
+    // [L | Lwide | R | Rwide] x PIX_LR_WORDS, and their exclusive word prefixes of set bits,
+    // [L | Lwide | R | Rwide] x (PIX_LR_WORDS + 1): every shard numbers the same sets alike
+    // (k_pix_lr)
     uint32_t *lr_bits, *lr_pre;
     int32_t *len16;          // UTF-16 lengths (max_length filter)
     long long ml;            // max_length of this index's selections
@@ -99,10 +101,11 @@ struct PixCtl {
     // sharded (delta rows): the last merge's rows are still to be added (k_pix_apply_delta); this
     // shard's sites of the merge being made (the header word the shards' sum must equal W in)
     uint32_t merged, pad1;
-    // sharded, compact layout: |L| and |R| of the last merge made; the batch's capacity (entries
-    // of L and of R the exchange holds); the largest max(|L|, |R|) of the batch (the host sizes
-    // the next batch from it); k_pix_lr's last-block ticket
-    uint32_t lr_n[2], lr_cap, lr_need, lr_ticket, pad2;
+    // sharded, compact layout: the narrow and wide members of L and of R of the last merge made,
+    // the exchange words they take; the batch's capacity (words after the special ones); the
+    // largest lr_words of the batch (the host sizes the next batch from it); merges paused for
+    // capacity; k_pix_lr's last-block ticket
+    uint32_t lr_n[4], lr_words, lr_cap, lr_need, lr_pauses, lr_ticket, pad2;
 };
 
 __device__ __forceinline__ uint32_t pix_key(int32_t u, int32_t v) {
@@ -189,47 +192,96 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
 // merge (a, b) -> c changes has a side in {a, b, c}: delta_slot), summed over the shards and added
 // to every shard's global counts by k_pix_apply_delta.
 // The compact layout of the exchange (round 5): HDR, then PIX_XCHG_SPECIAL words for the pairs of
-// two of {a, b, c}, then four words per entry j: (L_j, a), (L_j, c), (b, R_j), (c, R_j), where L_j
-// / R_j is the j-th id of L / R in increasing order.  Every pair a merge (a, b) -> c changes is
-// one of these: a site's left neighbour l loses (l, a) and gains (l, c), and l is
-// in L since (l, a) occurs; its right neighbour r loses (b, r) and gains (c, r) (a == b: (a, r));
-// chains, runs and the new (c, c) pair only ids of {a, b, c}.  So the exchange carries
-// 4 max(|L|, |R|) words instead of six dense rows per token id.
+// two of {a, b, c}, then one count per member of L and of R.  Every pair a merge (a, b) -> c
+// changes is one of these: a site's left neighbour l loses (l, a) and gains
+// (l, c), and l is in L since (l, a) occurs; its right neighbour r loses (b, r) and gains (c, r)
+// (a == b: (a, r)); chains, runs and the new (c, c) pair only ids of {a, b, c}.  So one number
+// per member carries both changes: n_l, the sites with left neighbour l (the loss of (l, a), the
+// gain of (l, c)), and n_r likewise.  n_l <= the global count of (l, a) (each such site is one of
+// its occurrences), so a member whose pair counts at most 0xFFFF (narrow) takes a 16-bit lane, four
+// to a word, the u64 all-reduce(SUM) adding the lanes without carries (the counts are never
+// negative); a wide member takes a word.  Words after the specials: [L narrow | L wide |
+// R narrow | R wide], each part in increasing id order.  At the 32k vocabulary that is ~1/16 of
+// the four u64 words per member of the first compact layout.
 constexpr uint32_t PIX_LR_WORDS = (55296 + 31) / 32;   // (BPE_MAX_VOCAB ids)
 constexpr uint32_t PIX_XCHG_SPECIAL = 16;
+constexpr unsigned long long PIX_LANE_MAX = 0xFFFFull;
 
-__device__ __forceinline__ uint32_t lr_index(const uint32_t *bits, const uint32_t *pre, uint32_t x) {
-    const uint32_t w = x >> 5, bit = 1u << (x & 31u), word = bits[w];
-    return (word & bit) ? pre[w] + (uint32_t)__popc(word & (bit - 1u)) : PIX_NONE;
+// first word (after the specials) of part q = 2 side + wide
+__device__ __forceinline__ uint32_t lr_part_base(const PixCtl *ctl, int q) {
+    const uint32_t wln = (ctl->lr_n[0] + 3u) / 4u, wrn = (ctl->lr_n[2] + 3u) / 4u;
+    const uint32_t base[4] = {0u, wln, wln + ctl->lr_n[1], wln + ctl->lr_n[1] + wrn};
+    return base[q];
 }
 
-// exchange word of pair (x, y) in the compact layout (PIX_NONE: not a pair of this merge)
-__device__ __forceinline__ uint32_t lr_slot(const PixTable &t, int32_t a, int32_t b, int32_t c,
-                                            int32_t x, int32_t y) {
-    const int sx = x == a ? 0 : x == b ? 1 : x == c ? 2 : 3;
-    const int sy = y == a ? 0 : y == b ? 1 : y == c ? 2 : 3;
-    if (sx < 3 && sy < 3) return XCHG_HDR + 3 * sx + sy;
-    uint32_t j = PIX_NONE, r = 0;
-    if (sx == 3 && (sy == 0 || sy == 2)) {            // (x, a), (x, c)
-        j = lr_index(t.lr_bits, t.lr_pre, (uint32_t)x);
-        r = sy == 0 ? 0u : 1u;
-    } else if (sy == 3 && (x == b || sx == 2)) {       // (b, y), (c, y)
-        j = lr_index(t.lr_bits + PIX_LR_WORDS, t.lr_pre + PIX_LR_WORDS + 1, (uint32_t)y);
-        r = sx == 2 ? 3u : 2u;
+// exchange word (after the specials) and lane shift of member o of side (0: L, 1: R), wide: a
+// word of its own; PIX_NONE when o is not a member
+__device__ __forceinline__ uint32_t lr_lane(const PixTable &t, const PixCtl *ctl, int side,
+                                            uint32_t o, uint32_t &shift, bool &wide) {
+    const uint32_t *bm = t.lr_bits + 2 * side * PIX_LR_WORDS, *bw = bm + PIX_LR_WORDS;
+    const uint32_t *pm = t.lr_pre + 2 * side * (PIX_LR_WORDS + 1), *pw = pm + PIX_LR_WORDS + 1;
+    const uint32_t w = o >> 5, bit = 1u << (o & 31u), below = bit - 1u;
+    const uint32_t m = bm[w], wd = bw[w];
+    if (!(m & bit)) return PIX_NONE;
+    wide = (wd & bit) != 0u;
+    if (wide) {
+        shift = 0;
+        return lr_part_base(ctl, 2 * side + 1) + pw[w] + (uint32_t)__popc(wd & below);
     }
-    return j == PIX_NONE ? PIX_NONE : XCHG_HDR + PIX_XCHG_SPECIAL + 4 * j + r;
+    const uint32_t j = pm[w] - pw[w] + (uint32_t)__popc(m & ~wd & below);
+    shift = 16u * (j & 3u);
+    return lr_part_base(ctl, 2 * side) + j / 4u;
 }
 
 __device__ __forceinline__ void pix_delta(const PixTable &t, PixCtl *ctl, uint32_t key, long long d) {
     if (!d) return;
     const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-    const uint32_t slot = t.lr_bits ? lr_slot(t, ctl->a, ctl->b, ctl->c, x, y)
-                                    : delta_slot(x, y, ctl->a, ctl->b, ctl->c);
-    if (slot == PIX_NONE) {
-        pix_fail(ctl, 41);   // (cannot happen: every changed pair has its word)
+    if (!t.lr_bits) {
+        const uint32_t slot = delta_slot(x, y, ctl->a, ctl->b, ctl->c);
+        if (slot == PIX_NONE) {
+            pix_fail(ctl, 41);   // (cannot happen: every changed pair has its word)
+            return;
+        }
+        atomicAdd(&t.delta[slot], (unsigned long long)d);
         return;
     }
-    atomicAdd(&t.delta[slot], (unsigned long long)d);
+    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
+    const int sx = x == a ? 0 : x == b ? 1 : x == c ? 2 : 3;
+    const int sy = y == a ? 0 : y == b ? 1 : y == c ? 2 : 3;
+    if (sx < 3 && sy < 3) {
+        atomicAdd(&t.delta[XCHG_HDR + 3 * sx + sy], (unsigned long long)d);
+        return;
+    }
+    int side;
+    bool gain;
+    uint32_t o;
+    if (sx == 3 && (sy == 0 || sy == 2)) {             // (x, a) lost, (x, c) gained
+        side = 0;
+        gain = sy == 2;
+        o = (uint32_t)x;
+    } else if (sy == 3 && (x == b || sx == 2)) {        // (b, y) lost, (c, y) gained
+        side = 1;
+        gain = sx == 2;
+        o = (uint32_t)y;
+    } else {
+        pix_fail(ctl, 41);   // (cannot happen: every changed pair is one of these)
+        return;
+    }
+    // a gain mirrors the loss at the same site (k_pix_apply_delta makes both from the count); a
+    // loss that rises or a gain that falls would break that: never, checked
+    if (gain != (d > 0)) {
+        pix_fail(ctl, 42);
+        return;
+    }
+    if (gain) return;
+    uint32_t shift;
+    bool wide;
+    const uint32_t w = lr_lane(t, ctl, side, o, shift, wide);
+    if (w == PIX_NONE) {
+        pix_fail(ctl, 41);
+        return;
+    }
+    atomicAdd(&t.delta[XCHG_HDR + PIX_XCHG_SPECIAL + w], (unsigned long long)(-d) << shift);
 }
 
 __device__ __forceinline__ uint32_t pix_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
@@ -1641,7 +1693,7 @@ __global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restr
 constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
 
 // the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on; lr_cap
-// entries of L and of R in the compact exchange (0: the dense rows)
+// words after the specials in the compact exchange (0: the dense rows)
 __global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight,
                                  uint32_t lr_cap) {
     if (ctl->status == PIX_PAUSE) ctl->status = PIX_RUN;
@@ -1651,16 +1703,19 @@ __global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long
     ctl->min_weight = min_weight;
     ctl->lr_cap = lr_cap;
     ctl->lr_need = 0;
+    ctl->lr_pauses = 0;
 }
 
 // The compact exchange's sets of the merge (a, b) -> c just decided (k_pix_select), from the
 // GLOBAL counts every shard holds alike: L = {x : (x, a) occurs}, R = {y : (b, y) occurs}, ids of
-// {a, b, c} aside, as bitmaps; the last block writes their word prefixes and sizes, and hands the
-// iteration to the host when either set exceeds the batch's capacity (every shard alike: before
-// any shard applies the merge).  Runs between k_pix_select and k_pix_sites.
+// {a, b, c} aside, and their wide members (count > PIX_LANE_MAX), as bitmaps; the last block
+// writes their word prefixes and sizes.  When the words exceed the batch's capacity the batch
+// pauses before this merge (every shard alike, before any shard counts its sites): the next batch,
+// sized from lr_need, selects it again from the same counts.  Runs between k_pix_select and
+// k_pix_sites.
 __global__ void __launch_bounds__(256) k_pix_lr(PixTable t, PixCtl *ctl) {
     __shared__ uint32_t s_go, s_last;
-    __shared__ uint32_t s_sum[2][4];
+    __shared__ uint32_t s_sum[4][4];
     if (threadIdx.x == 0) s_go = ctl->status == PIX_RUN && ctl->tie == PIX_TIE_NONE;
     __syncthreads();
     if (!s_go) return;
@@ -1669,20 +1724,20 @@ __global__ void __launch_bounds__(256) k_pix_lr(PixTable t, PixCtl *ctl) {
     const int lane = threadIdx.x & 63;
     // (one id per thread; a wave's ballots are two whole words: 64-aligned ids per wave)
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nw * 32u; x += gridDim.x * blockDim.x) {
-        bool in_l = false, in_r = false;
+        unsigned long long nl = 0, nr = 0;
         if (x < nid && (int32_t)x != a && (int32_t)x != b && (int32_t)x != c) {
             const PixProbe pl = pix_probe(t, pix_key((int32_t)x, a));
             const PixProbe pr = pix_probe(t, pix_key(b, (int32_t)x));
             const uint32_t sl = pix_slot(t, ctl, pix_key((int32_t)x, a), false, false, pl);
             const uint32_t sr = pix_slot(t, ctl, pix_key(b, (int32_t)x), false, false, pr);
-            in_l = sl != PIX_NONE && t.cnt[sl] != 0;
-            in_r = sr != PIX_NONE && t.cnt[sr] != 0;
+            nl = sl != PIX_NONE ? t.cnt[sl] : 0ull;
+            nr = sr != PIX_NONE ? t.cnt[sr] : 0ull;
         }
-        const unsigned long long ml = __ballot(in_l), mr = __ballot(in_r);
-        if ((lane & 31) == 0 && (x >> 5) < nw) {
-            t.lr_bits[x >> 5] = (uint32_t)(ml >> lane);
-            t.lr_bits[PIX_LR_WORDS + (x >> 5)] = (uint32_t)(mr >> lane);
-        }
+        const unsigned long long m[4] = {__ballot(nl != 0), __ballot(nl > PIX_LANE_MAX),
+                                         __ballot(nr != 0), __ballot(nr > PIX_LANE_MAX)};
+        if ((lane & 31) == 0 && (x >> 5) < nw)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t.lr_bits[q * PIX_LR_WORDS + (x >> 5)] = (uint32_t)(m[q] >> lane);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1695,67 +1750,87 @@ __global__ void __launch_bounds__(256) k_pix_lr(PixTable t, PixCtl *ctl) {
     // exclusive prefixes of the words' set bits: each thread a contiguous range of words
     const uint32_t per = (nw + blockDim.x - 1) / blockDim.x;
     const uint32_t w0 = min(nw, threadIdx.x * per), w1 = min(nw, w0 + per);
-    uint32_t cl = 0, cr = 0;
-    for (uint32_t w = w0; w < w1; ++w) {
-        cl += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        cr += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[PIX_LR_WORDS + w], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT));
-    }
+    auto bits = [&](int q, uint32_t w) {
+        return (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[q * PIX_LR_WORDS + w], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT));
+    };
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    for (uint32_t w = w0; w < w1; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cnt[q] += bits(q, w);
     const int wv = threadIdx.x >> 6;
-    uint32_t il = wave_incl_sum((int)cl, lane), ir = wave_incl_sum((int)cr, lane);
-    if (lane == 63) {
-        s_sum[0][wv] = il;
-        s_sum[1][wv] = ir;
+    uint32_t incl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        incl[q] = wave_incl_sum((int)cnt[q], lane);
+        if (lane == 63) s_sum[q][wv] = incl[q];
     }
     __syncthreads();
-    uint32_t bl = 0, br = 0, tl = 0, tr = 0;
+    uint32_t tot[4];
+#pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (q < wv) {
-            bl += s_sum[0][q];
-            br += s_sum[1][q];
+        uint32_t before = 0, all = 0;
+        for (int v = 0; v < 4; ++v) {
+            if (v < wv) before += s_sum[q][v];
+            all += s_sum[q][v];
         }
-        tl += s_sum[0][q];
-        tr += s_sum[1][q];
-    }
-    uint32_t el = bl + il - cl, er = br + ir - cr;   // (exclusive, this thread's first word)
-    for (uint32_t w = w0; w < w1; ++w) {
-        t.lr_pre[w] = el;
-        t.lr_pre[PIX_LR_WORDS + 1 + w] = er;
-        el += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        er += (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[PIX_LR_WORDS + w], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT));
+        tot[q] = all;
+        uint32_t e = before + incl[q] - cnt[q];   // (exclusive, this thread's first word)
+        for (uint32_t w = w0; w < w1; ++w) {
+            t.lr_pre[q * (PIX_LR_WORDS + 1) + w] = e;
+            e += bits(q, w);
+        }
+        if (threadIdx.x == 0) t.lr_pre[q * (PIX_LR_WORDS + 1) + nw] = all;
     }
     if (threadIdx.x == 0) {
-        t.lr_pre[nw] = tl;
-        t.lr_pre[PIX_LR_WORDS + 1 + nw] = tr;
-        ctl->lr_n[0] = tl;
-        ctl->lr_n[1] = tr;
-        const uint32_t need = max(tl, tr);
-        ctl->lr_need = max(ctl->lr_need, need);
-        if (need > ctl->lr_cap) pix_fail(ctl, 40);   // (the next batch holds it: bpe_engine.hip)
+        // (narrow = members - wide)
+        const uint32_t n[4] = {tot[0] - tot[1], tot[1], tot[2] - tot[3], tot[3]};
+        const uint32_t words = (n[0] + 3u) / 4u + n[1] + (n[2] + 3u) / 4u + n[3];
+        ctl->lr_need = max(ctl->lr_need, words);
+        if (words > ctl->lr_cap) {
+            // (merge not made: k_pix_select's next run, in the next batch, selects it again; err
+            // stays clear, other checks read it)
+            ctl->status = PIX_PAUSE;
+            ctl->lr_pauses += 1;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ctl->lr_n[q] = n[q];
+            ctl->lr_words = words;
+        }
         ctl->lr_ticket = 0;
     }
 }
 
-// the j-th id of a set (bits, pre over nw words)
-__device__ __forceinline__ int32_t lr_select(const uint32_t *bits, const uint32_t *pre, uint32_t nw,
-                                             uint32_t j) {
-    uint32_t lo = 0, hi = nw;   // the word w with pre[w] <= j < pre[w + 1]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= j) lo = mid;
-        else hi = mid;
+// One summed count change into this shard's global counts: a fall marks the block when the entry
+// was its max, a rise (only pairs with c rise) lifts the block and superblock maxima; a pair new to
+// this shard gets a slot (no list here).
+__device__ __forceinline__ void pix_global_add(const PixTable &t, const PixBufs &B, PixCtl *ctl,
+                                               uint32_t key, unsigned long long v) {
+    const bool rise = (long long)v > 0;
+    const uint32_t s = pix_slot(t, ctl, key, rise, true);
+    if (s == PIX_NONE) {   // (a fall of a pair no shard holds: the tables disagree)
+        if (rise) pix_fail(ctl, 1);
+        else if (atomicCAS(&ctl->status, PIX_RUN, PIX_ERROR) == PIX_RUN) ctl->err = 22;
+        return;
     }
-    uint32_t word = bits[lo];
-    for (uint32_t k = j - pre[lo]; k; --k) word &= word - 1u;
-    return (int32_t)(32u * lo + (uint32_t)__ffs(word) - 1u);
+    const unsigned long long bm = t.bmax[s / PIX_B];
+    const unsigned long long old = atomicAdd(&t.cnt[s], v);
+    if (rise) {
+        const unsigned long long sel = pix_sel_of(t, key, old + v);
+        const uint32_t blk = s / PIX_B;
+        if (sel > bm) {
+            atomicMax(&t.bmax[blk], sel);
+            atomicMax(&t.sbmax[blk / PIX_SB], sel);
+        }
+    } else {
+        const unsigned long long sel = pix_sel_of(t, key, old);
+        if (sel && sel >= bm) pix_mark(t, B, ctl, s);
+    }
 }
 
-// The summed delta rows of the last merge (a, b) -> c into this shard's global counts: a fall marks
-// the block when the entry was its max, a rise (only pairs with c rise) lifts the block and
-// superblock maxima; a pair new to this shard gets a slot (no list here).  The rows read are zeroed
-// for this iteration's own changes; the header's first word, the shards' replacements summed, must
-// equal W.
+// The summed exchange of the last merge (a, b) -> c into this shard's global counts.  The words
+// read are zeroed for this iteration's own changes; the header's first word, the shards'
+// replacements summed, must equal W.
 __global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, PixCtl *ctl,
                                                          unsigned long long *__restrict__ xchg) {
     __shared__ uint32_t s_go;
@@ -1772,57 +1847,51 @@ __global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, 
         }
     }
     unsigned long long *d = xchg + XCHG_HDR;
-    // (compact: the sets of the last merge are still those k_pix_lr made for it)
-    const bool lr = t.lr_bits != nullptr;
-    const uint32_t nw = ((uint32_t)c + 32u) / 32u;
-    const uint32_t n = lr ? PIX_XCHG_SPECIAL + 4u * max(ctl->lr_n[0], ctl->lr_n[1])
-                          : (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);   // other tokens <= c
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const unsigned long long v = d[i];
-        if (!v) continue;
-        d[i] = 0;
-        uint32_t key;
-        if (lr) {
+    if (t.lr_bits) {
+        // compact (the sets of the last merge are still those k_pix_lr made for it): a thread per
+        // special word, then per id of L and of R: its lane (cleared with an atomic AND, since
+        // other threads read the other lanes of the word), n = the sites with that neighbour:
+        // side L loses (o, a) and gains (o, c); side R loses (b, o) and gains (c, o)
+        const uint32_t nid = (uint32_t)c + 1u;
+        const uint32_t n = PIX_XCHG_SPECIAL + 2u * nid;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
             if (i < PIX_XCHG_SPECIAL) {
                 if (i >= 9) continue;   // (never written)
+                const unsigned long long v = d[i];
+                if (!v) continue;
+                d[i] = 0;
                 const int32_t abc[3] = {a, b, c};
-                key = pix_key(abc[i / 3], abc[i % 3]);
-            } else {
-                const uint32_t j = (i - PIX_XCHG_SPECIAL) >> 2, r = (i - PIX_XCHG_SPECIAL) & 3u;
-                if (r < 2) {
-                    const int32_t o = lr_select(t.lr_bits, t.lr_pre, nw, j);
-                    key = pix_key(o, r ? c : a);
-                } else {
-                    const int32_t o = lr_select(t.lr_bits + PIX_LR_WORDS, t.lr_pre + PIX_LR_WORDS + 1, nw, j);
-                    key = pix_key(r == 2 ? b : c, o);
-                }
+                pix_global_add(t, B, ctl, pix_key(abc[i / 3], abc[i % 3]), v);
+                continue;
             }
-        } else {
+            const uint32_t k = i - PIX_XCHG_SPECIAL;
+            const int side = k >= nid;
+            const int32_t o = (int32_t)(side ? k - nid : k);
+            uint32_t shift;
+            bool wide;
+            const uint32_t w = lr_lane(t, ctl, side, (uint32_t)o, shift, wide);
+            if (w == PIX_NONE) continue;
+            unsigned long long *p = d + PIX_XCHG_SPECIAL + w;
+            const unsigned long long v = *p;
+            const unsigned long long cnt = wide ? v : (v >> shift) & PIX_LANE_MAX;
+            if (!cnt) continue;
+            if (wide) *p = 0;
+            else atomicAnd(p, ~(PIX_LANE_MAX << shift));
+            pix_global_add(t, B, ctl, side ? pix_key(b, o) : pix_key(o, a), (unsigned long long)-(long long)cnt);
+            pix_global_add(t, B, ctl, side ? pix_key(c, o) : pix_key(o, c), cnt);
+        }
+    } else {
+        // dense rows: every token id <= c
+        const uint32_t n = (uint32_t)DELTA_ROWS * (uint32_t)(c + 1);
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const unsigned long long v = d[i];
+            if (!v) continue;
+            d[i] = 0;
             const uint32_t row = i % DELTA_ROWS;
             const int32_t o = (int32_t)(i / DELTA_ROWS);
             const int32_t m = row == 0 || row == 2 ? a : row == 1 || row == 3 ? b : c;
             const bool left = row == 0 || row == 1 || row == 4;   // (m, o), else (o, m)
-            key = pix_key(left ? m : o, left ? o : m);
-        }
-        const bool rise = (long long)v > 0;
-        const uint32_t s = pix_slot(t, ctl, key, rise, true);
-        if (s == PIX_NONE) {   // (a fall of a pair no shard holds: the tables disagree)
-            if (rise) pix_fail(ctl, 1);
-            else if (atomicCAS(&ctl->status, PIX_RUN, PIX_ERROR) == PIX_RUN) ctl->err = 22;
-            continue;
-        }
-        const unsigned long long bm = t.bmax[s / PIX_B];
-        const unsigned long long old = atomicAdd(&t.cnt[s], v);
-        if (rise) {
-            const unsigned long long sel = pix_sel_of(t, key, old + v);
-            const uint32_t blk = s / PIX_B;
-            if (sel > bm) {
-                atomicMax(&t.bmax[blk], sel);
-                atomicMax(&t.sbmax[blk / PIX_SB], sel);
-            }
-        } else {
-            const unsigned long long sel = pix_sel_of(t, key, old);
-            if (sel && sel >= bm) pix_mark(t, B, ctl, s);
+            pix_global_add(t, B, ctl, pix_key(left ? m : o, left ? o : m), v);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) xchg[0] = 0;

@@ -307,6 +307,8 @@ typedef struct {
     int64_t xchg_iters;       /* rank loop: iterations those bytes cover */
     int64_t pix_fallbacks;    /* multi-device context, incremental mode: times the shards' index kept
                                  handing over and the run went on in the streaming mode */
+    int64_t xchg_pauses;      /* rank loop, incremental mode: batches ended early because a merge's
+                                 compact exchange outgrew the batch's capacity (made in the next) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -297,10 +297,13 @@ def test_incremental_mode_over_shards(shards, corpus, n, max_length):
 
 
 def test_incremental_exchange_compact_vs_dense_rows(monkeypatch):
-    """The sharded incremental mode's exchange in its compact layout (round 5: per merge, L = the
-    ids x with a pair (x, a) and R = the ids y with a pair (b, y), numbered alike on every shard
-    from the global counts; 4 words per entry) against the dense delta rows (6 per token id,
-    BPE_XCHG_DENSE=1): the same merges and corpus as one context, and fewer bytes per merge."""
+    """The sharded incremental mode's exchange in its compact layout (round 5: per merge, one
+    count per member of L = the ids x with a pair (x, a) and of R = the ids y with a pair (b, y),
+    numbered alike on every shard from the global counts; 16-bit lanes for members whose pair
+    counts at most 0xFFFF) against the dense delta rows (6 u64 per token id, BPE_XCHG_DENSE=1),
+    and with a capacity that many merges outgrow (BPE_XCHG_TIGHT=1: those batches pause before
+    the merge and the next one makes it): the same merges and corpus as one context, and far fewer
+    bytes per merge."""
     data = pkg.synth_latin1(16 << 20, seed=4242, A=96, base=32)
     one = pkg.Engine(0)
     one.add_latin1(data, sample_bytes=1 << 20)
@@ -308,11 +311,13 @@ def test_incremental_exchange_compact_vs_dense_rows(monkeypatch):
     ids1, _ = one.read_corpus()
     one.close()
     per_merge = {}
-    for layout in ('dense', 'compact'):
+    for layout in ('dense', 'compact', 'tight'):
+        monkeypatch.delenv('BPE_XCHG_DENSE', raising=False)
+        monkeypatch.delenv('BPE_XCHG_TIGHT', raising=False)
         if layout == 'dense':
             monkeypatch.setenv('BPE_XCHG_DENSE', '1')
-        else:
-            monkeypatch.delenv('BPE_XCHG_DENSE', raising=False)
+        elif layout == 'tight':
+            monkeypatch.setenv('BPE_XCHG_TIGHT', '1')
         multi = pkg.Engine(devices=[0] * 4, reduce='host')
         multi.add_latin1(data, sample_bytes=1 << 20)
         multi.set_mode('incremental')
@@ -323,11 +328,14 @@ def test_incremental_exchange_compact_vs_dense_rows(monkeypatch):
         ids, _ = multi.read_corpus()
         assert np.array_equal(ids, ids1), layout
         assert st['pix_merges'] >= 4 * 1400 and st['xchg_iters'] >= 1400, st
+        assert st['pix_host'] == 0, (layout, st)
+        if layout == 'tight':
+            assert st['xchg_pauses'] > 10, st
         # (xchg_bytes is summed over the 4 shards)
         per_merge[layout] = st['xchg_bytes'] / 4 / st['xchg_iters']
         multi.close()
-    # (a small vocabulary: the dense rows are short too; the 32k-vocabulary test reports the gap)
-    assert per_merge['compact'] < per_merge['dense'], per_merge
+    print('exchange bytes per merge', per_merge)
+    assert per_merge['compact'] * 8 < per_merge['dense'], per_merge
 
 
 @pytest.mark.slow

@@ -25,7 +25,8 @@
 #   profmulti  rocprofv3 --kernel-trace --stats of the streaming leg of `multi`
 #   profmultipix  the same for the incremental leg
 #   sqenc      SQ counter passes and FETCH_SIZE of the device encoder (tools/encode_bench.py, zipf
-#              merges, 20 000 texts), summarised per k_encode launch (tools/sq_loop_summary.py)
+#              merges, 20 000 texts), summarised per k_encode launch (tools/sq_loop_summary.py),
+#              under TAG/enc (apart from the sq / pmc steps' directories)
 # Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), BPE_LIB (A/B builds)
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -132,28 +133,31 @@ for step in "$@"; do
       tail -2 "$OUT/multi8_$mode.jsonl"
     done ;;
   profmulti)
-    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/multi" -o run --output-format csv \
+    BPE_MULTI_ONE_THREAD=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/multi" -o run --output-format csv \
         -- python3 tools/multi_pix_probe.py 512 8 32512 4096 stream > "$OUT/pmulti.jsonl" 2> "$OUT/pmulti.err" \
         || fail profmulti "$OUT/pmulti.err"
     tail -2 "$OUT/pmulti.jsonl"; prof_stats "$OUT/multi" ;;
   profmultipix)
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/multipix" -o run --output-format csv \
+    # (one enqueue thread: rocprofv3's kernel trace crashed in hipEventRecord with the
+    # per-shard threads, gpurun_out/r05i; the kernels are the same)
+    BPE_MULTI_ONE_THREAD=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/multipix" -o run --output-format csv \
         -- python3 tools/multi_pix_probe.py 512 8 32512 4096 incremental > "$OUT/pmultipix.jsonl" 2> "$OUT/pmultipix.err" \
         || fail profmultipix "$OUT/pmultipix.err"
     tail -2 "$OUT/pmultipix.jsonl"; prof_stats "$OUT/multipix"
     python3 tools/trace_gaps.py "$OUT/multipix" "$OUT/gaps_multipix.json" > /dev/null || true ;;
   sqenc)
+    E="$OUT/enc"; mkdir -p "$E"
     ENC="tools/encode_bench.py --corpus zipf --texts 20000 --reps 1 --cpu-texts 20"
     timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
-        -d "$OUT/sq" -o run --output-format csv -- python3 $ENC > "$OUT/sq.log" 2>&1 || fail sqenc "$OUT/sq.log"
+        -d "$E/sq" -o run --output-format csv -- python3 $ENC > "$E/sq.log" 2>&1 || fail sqenc "$E/sq.log"
     timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
-        -d "$OUT/sq2" -o run --output-format csv -- python3 $ENC > "$OUT/sq2.log" 2>&1 || fail sqenc2 "$OUT/sq2.log"
-    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
-        -- python3 $ENC > "$OUT/fetch.log" 2>&1 || fail sqenc3 "$OUT/fetch.log"
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
-        -- python3 $ENC > "$OUT/trace.log" 2>&1 || fail sqenc4 "$OUT/trace.log"
-    python3 tools/sq_loop_summary.py "$OUT" > "$OUT/sq_summary.txt" && grep -A30 k_encode "$OUT/sq_summary.txt" | head -80
-    prof_stats "$OUT/trace" ;;
+        -d "$E/sq2" -o run --output-format csv -- python3 $ENC > "$E/sq2.log" 2>&1 || fail sqenc2 "$E/sq2.log"
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$E/fetch" -o run --output-format csv \
+        -- python3 $ENC > "$E/fetch.log" 2>&1 || fail sqenc3 "$E/fetch.log"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$E/trace" -o run --output-format csv \
+        -- python3 $ENC > "$E/trace.log" 2>&1 || fail sqenc4 "$E/trace.log"
+    python3 tools/sq_loop_summary.py "$E" > "$E/sq_summary.txt" && grep -A30 k_encode "$E/sq_summary.txt" | head -80
+    prof_stats "$E/trace" ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -24,6 +24,7 @@ def main():
     e.set_mode(mode)
     e.stats_enable(True)
     done = 0
+    prev = (0, 0)
     t_all = time.perf_counter()
     while done < total:
         k = min(chunk, total - done)
@@ -32,12 +33,16 @@ def main():
         dt = time.perf_counter() - t0
         done += len(got)
         st = e.stats()
-        print(json.dumps({'merges': done, 'chunk_s': round(dt, 3), 'ms_per_merge': dt * 1e3 / max(1, len(got)),
+        # (this chunk's exchange per iteration, each shard)
+        dx, di = st['xchg_bytes'] - prev[0], st['xchg_iters'] - prev[1]
+        prev = (st['xchg_bytes'], st['xchg_iters'])
+        print(json.dumps({'merges': done, 'chunk_xchg_bytes_per_iter': dx / shards / max(1, di), 'chunk_s': round(dt, 3), 'ms_per_merge': dt * 1e3 / max(1, len(got)),
                           'last_w': got[-1][2] if got else None, 'pix_merges': st['pix_merges'],
                           'pix_builds': st['pix_builds'], 'pix_host': st['pix_host'],
                           'loop_host': st['loop_host'],
                           # (the exchange each shard all-reduces per iteration, over the run so far)
-                          'xchg_bytes_per_iter': st['xchg_bytes'] / shards / max(1, st['xchg_iters'])}),
+                          'xchg_bytes_per_iter': st['xchg_bytes'] / shards / max(1, st['xchg_iters']),
+                          'xchg_pauses': st['xchg_pauses']}),
               flush=True)
         if len(got) < k:
             break
