@@ -187,7 +187,12 @@ struct bpe_ctx {
     uint64_t pix_min_cap = 0;    // (the next index build's least table size)
     // sharded incremental mode, compact exchange: entries of L and of R the next batch's exchange
     // holds (0: not known yet, every token id; sized from the largest need of the batches before)
-    int64_t pix_lr_cap = 0;
+    // the lane layout of the sharded incremental exchange: the last merge's count (0: unknown),
+    // the layout {bits, lanes per word, right side's first word} of this batch and of the batch
+    // whose last merge's lanes are pending
+    unsigned long long pix_w_last = 0;
+    uint32_t pix_lane[3] = {0, 0, 0}, pix_lane_prev[3] = {0, 0, 0};
+    bool pix_first_pending = false;
 };
 
 namespace {
@@ -2139,6 +2144,7 @@ int pix_set_global(bpe_ctx *c, const unsigned long long *table, const uint32_t *
     c->rl_global = true;
     c->rl_pix = true;
     c->rl_delta_pending = false;
+    c->pix_w_last = 0;   // (the first batch's lanes: full words)
     c->counts_valid = c->sketch_valid = c->best_ready = false;
     c->cold_exact = false;
     return BPE_OK;
@@ -2244,36 +2250,46 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
         // (the selection keys filter on max_length: every block max again)
         P->max_length = max_length;
         P->T.ml = max_length;
+        c->pix_w_last = 0;   // (pairs the filter held back may now count more than the last W)
         k_pix_bmax_all<<<4096, 256, 0, s>>>(P->T);
         k_pix_sbmax<<<1024, 256, 0, s>>>(P->T, P->B, P->d_ctl, 1);
     }
     P->T.delta = xchg;
-    // the exchange: the compact layout (a count per member of L and of R of each merge, k_pix_lr),
-    // sized for this batch, or (BPE_XCHG_DENSE=1, A/B and checks) six dense rows per token id
+    // the exchange: the lane layout (a count per token id and side, in lanes as wide as the last
+    // merge's count needs, bpe_pix.hip.h), or (BPE_XCHG_DENSE=1, A/B and checks) six dense rows per
+    // token id
     const bool dense = getenv("BPE_XCHG_DENSE") != nullptr;   // (read per batch: tests switch it)
     const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, base + LOOP_BATCH + 1);
-    int64_t nw, lr_cap = 0;
+    int64_t nw;
+    // (the last batch's pending merge keeps its own layout for its decode, and its words)
+    c->pix_first_pending = c->rl_delta_pending;
+    for (int i = 0; i < 3; ++i) c->pix_lane_prev[i] = c->pix_lane[i];
+    const int64_t prev_words = c->rl_delta_pending && c->pix_lane_prev[0] ? 2 * (int64_t)c->pix_lane_prev[2]
+                                                                          : 0;
     if (dense) {
-        P->T.lr_bits = P->T.lr_pre = nullptr;
+        P->T.lane_w = P->T.lane_q = P->T.lane_base = 0;
         nw = XCHG_HDR + DELTA_ROWS * ids;
     } else {
-        if (!P->T.lr_bits) {
-            if ((rc = pix_alloc(P, &P->T.lr_bits, 4 * PIX_LR_WORDS))) return rc;
-            if ((rc = pix_alloc(P, &P->T.lr_pre, 4 * (PIX_LR_WORDS + 1)))) return rc;
-            HIP_TRY(hipMemsetAsync(P->T.lr_bits, 0, 4 * PIX_LR_WORDS * sizeof(uint32_t), s));
-            c->rl_delta_pending = false;   // (a fresh index: no merge of the old layout pending)
-        }
-        // (words after the specials: at most one per member of L and of R, each at most ids)
-        lr_cap = c->pix_lr_cap > 0 ? std::min(c->pix_lr_cap, 2 * ids) : 2 * ids;
-        nw = XCHG_HDR + PIX_XCHG_SPECIAL + lr_cap;
+        uint32_t w = c->pix_w_last ? 64u - (uint32_t)__builtin_clzll(c->pix_w_last) : 64u;
+        // (BPE_XCHG_LANE_BITS=n, tests: lanes of at most n bits after a known count, so that
+        // counts outgrow them, pause the batch and the next one takes full words)
+        if (const char *lb = getenv("BPE_XCHG_LANE_BITS"))
+            if (c->pix_w_last) w = std::max(1u, std::min<uint32_t>(w, (uint32_t)atoi(lb)));
+        const uint32_t q = 64u / w;
+        P->T.lane_w = w;
+        P->T.lane_q = q;
+        P->T.lane_base = (uint32_t)((ids + q - 1) / q);
+        nw = XCHG_HDR + PIX_XCHG_SPECIAL + std::max<int64_t>(2 * (int64_t)P->T.lane_base, prev_words);
     }
+    c->pix_lane[0] = P->T.lane_w;
+    c->pix_lane[1] = P->T.lane_q;
+    c->pix_lane[2] = P->T.lane_base;
     // (delta pending: the last batch's last merge's rows are in xchg, for this batch's first
     // all-reduce; else all of it zero: the rows past this batch's words are read by later ones)
     if (!c->rl_delta_pending)
         HIP_TRY(hipMemsetAsync(xchg, 0, XCHG_WORDS * sizeof(unsigned long long), s));
     k_pix_rank_begin<<<1, 1, 0, s>>>(P->d_ctl, LOOP_BATCH, (int32_t)base,
-                                     min_weight == 0 ? 2 : min_weight,   // core.ts:256
-                                     (uint32_t)lr_cap);
+                                     min_weight == 0 ? 2 : min_weight);   // core.ts:256
     HIP_TRY(hipGetLastError());
     c->opt_max_length = max_length;
     c->rl_table = xchg;
@@ -2292,14 +2308,16 @@ int pix_rank_select(bpe_ctx *c) {
     PixState *P = c->pix;
     hipStream_t s = c->stream;
     hipEvent_t e = span_begin(c);
-    k_pix_apply_delta<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->rl_table);
+    // (the batch's first iteration decodes the last batch's pending merge in its layout)
+    PixTable T = P->T;
+    if (c->rl_enqueued == 0 && c->pix_first_pending) {
+        T.lane_w = c->pix_lane_prev[0];
+        T.lane_q = c->pix_lane_prev[1];
+        T.lane_base = c->pix_lane_prev[2];
+    }
+    k_pix_apply_delta<<<PIX_GRID, 256, 0, s>>>(T, P->B, P->d_ctl, c->rl_table);
     k_pix_dirty<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
     k_pix_select<<<1, 1024, 0, s>>>(P->T, P->B, P->d_ctl);
-    if (P->T.lr_bits) {
-        // (one thread per token id of the batch's vocabulary)
-        const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, c->rl_base + LOOP_BATCH + 1);
-        k_pix_lr<<<(unsigned)((ids + 255) / 256), 256, 0, s>>>(P->T, P->d_ctl);
-    }
     k_pix_sites<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl);
     k_pix_export<<<1, 64, 0, s>>>(P->d_ctl, c->rl_table, c->rl_tie, c->rl_rank);
     HIP_TRY(hipGetLastError());
@@ -2375,21 +2393,12 @@ int pix_rank_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *st
     }
     c->len16_lo = base + nd;   // (pix_commit wrote the new lengths on the device)
     const int st = h->status == PIX_DONE ? LOOP_DONE : h->status == PIX_HOST ? LOOP_HOST : LOOP_RUN;
-    if (P->T.lr_bits) {
-        // the next batch's capacity: 1.25 times the most words a merge of this one took (every
-        // shard alike: the sets come from the global counts), shrinking by at most a quarter per
-        // batch, and no more than every id in both sets with narrow lanes takes unless a merge
-        // needed more (wide members); a merge past it pauses the batch (k_pix_lr) and is made in
-        // the next one
-        const int64_t need = (int64_t)h->lr_need;
-        const int64_t prev = c->pix_lr_cap > 0 ? c->pix_lr_cap : 2 * need;
-        const int64_t ids = std::min<int64_t>(BPE_MAX_VOCAB, (int64_t)c->h_len16.size() + LOOP_BATCH + 1);
-        const int64_t narrow_all = 2 * ((ids + 3) / 4);
-        c->pix_lr_cap = std::max<int64_t>({64, need + need / 4 + 16, prev * 3 / 4});
-        if (need <= narrow_all) c->pix_lr_cap = std::min(c->pix_lr_cap, narrow_all);
-        // (BPE_XCHG_TIGHT=1, tests: exactly the largest need, so that merges pause often)
-        if (getenv("BPE_XCHG_TIGHT") != nullptr) c->pix_lr_cap = std::max<int64_t>(1, need);
-        if (c->stats_on) c->stats.xchg_pauses += h->lr_pauses;
+    // the next batch's lanes: the last merge's count bounds every later one's (and each of its
+    // per-neighbour counts); a count past the lanes (lane_over) takes full words once
+    if (nd > 0) c->pix_w_last = (unsigned long long)P->h_log[PIX_LOG * (nd - 1) + 2];
+    if (h->lane_over) {
+        c->pix_w_last = 0;
+        HIP_TRY(hipMemsetAsync(&P->d_ctl->lane_over, 0, sizeof(uint32_t), s));
     }
     if (st != LOOP_RUN) {
         static const bool dbg = getenv("BPE_DEBUG_PIX") != nullptr;

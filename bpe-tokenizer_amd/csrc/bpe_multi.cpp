@@ -1013,7 +1013,6 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.pix_build_ms = std::max(acc.pix_build_ms, x.pix_build_ms);
         acc.xchg_bytes += x.xchg_bytes;
         acc.xchg_iters = std::max(acc.xchg_iters, x.xchg_iters);
-        acc.xchg_pauses = std::max(acc.xchg_pauses, x.xchg_pauses);
     }
     acc.pix_fallbacks = m->pix_fallbacks;
     *out = acc;

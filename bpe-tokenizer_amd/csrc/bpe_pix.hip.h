@@ -56,13 +56,9 @@ struct PixTable {
     // from the summed delta rows (include/bpe.h BPE_XCHG_*); this shard's count changes go to its
     // delta rows (delta != nullptr) instead of cnt.  The lists stay this shard's own.
     unsigned long long *delta;
-    // ... in the compact layout (round 5, lr_bits != nullptr): the merge's left set L (every x
-    // with a pair (x, a)) and right set R (every y with a pair (b, y)), and their wide members
-    // (global count of the pair > 0xFFFF), as bitmaps over the token ids,
-    // [L | Lwide | R | Rwide] x PIX_LR_WORDS, and their exclusive word prefixes of set bits,
-    // [L | Lwide | R | Rwide] x (PIX_LR_WORDS + 1): every shard numbers the same sets alike
-    // (k_pix_lr)
-    uint32_t *lr_bits, *lr_pre;
+    // ... in the lane layout (round 5, lane_w != 0): lane_w-bit lanes, lane_q to a u64 word, the
+    // right side's lanes from word lane_base on (pix_delta)
+    uint32_t lane_w, lane_q, lane_base;
     int32_t *len16;          // UTF-16 lengths (max_length filter)
     long long ml;            // max_length of this index's selections
     uint32_t *keys;
@@ -101,11 +97,10 @@ struct PixCtl {
     // sharded (delta rows): the last merge's rows are still to be added (k_pix_apply_delta); this
     // shard's sites of the merge being made (the header word the shards' sum must equal W in)
     uint32_t merged, pad1;
-    // sharded, compact layout: the narrow and wide members of L and of R of the last merge made,
-    // the exchange words they take; the batch's capacity (words after the special ones); the
-    // largest lr_words of the batch (the host sizes the next batch from it); merges paused for
-    // capacity; k_pix_lr's last-block ticket
-    uint32_t lr_n[4], lr_words, lr_cap, lr_need, lr_pauses, lr_ticket, pad2;
+    // sharded, lane layout: a selected count past the batch's lanes paused the batch (the next
+    // one takes wider lanes)
+    uint32_t lane_over, pad2;
+
 };
 
 __device__ __forceinline__ uint32_t pix_key(int32_t u, int32_t v) {
@@ -191,52 +186,30 @@ __device__ __forceinline__ uint32_t pix_slot(const PixTable &t, PixCtl *ctl, uin
 // A shard of a sharded corpus: the change goes to this shard's delta row of the pair (every pair a
 // merge (a, b) -> c changes has a side in {a, b, c}: delta_slot), summed over the shards and added
 // to every shard's global counts by k_pix_apply_delta.
-// The compact layout of the exchange (round 5): HDR, then PIX_XCHG_SPECIAL words for the pairs of
-// two of {a, b, c}, then one count per member of L and of R.  Every pair a merge (a, b) -> c
-// changes is one of these: a site's left neighbour l loses (l, a) and gains
-// (l, c), and l is in L since (l, a) occurs; its right neighbour r loses (b, r) and gains (c, r)
-// (a == b: (a, r)); chains, runs and the new (c, c) pair only ids of {a, b, c}.  So one number
-// per member carries both changes: n_l, the sites with left neighbour l (the loss of (l, a), the
-// gain of (l, c)), and n_r likewise.  n_l <= the global count of (l, a) (each such site is one of
-// its occurrences), so a member whose pair counts at most 0xFFFF (narrow) takes a 16-bit lane, four
-// to a word, the u64 all-reduce(SUM) adding the lanes without carries (the counts are never
-// negative); a wide member takes a word.  Words after the specials: [L narrow | L wide |
-// R narrow | R wide], each part in increasing id order.  At the 32k vocabulary that is ~1/16 of
-// the four u64 words per member of the first compact layout.
-constexpr uint32_t PIX_LR_WORDS = (55296 + 31) / 32;   // (BPE_MAX_VOCAB ids)
+// The lane layout of the exchange (round 5): HDR, then PIX_XCHG_SPECIAL words for the pairs of two
+// of {a, b, c}, then one count per token id and side.  Every pair a merge (a, b) -> c changes is
+// one of these: a site's left neighbour l loses (l, a) and gains (l, c); its right
+// neighbour r loses (b, r) and gains (c, r) (a == b: (a, r)); chains, runs and the new (c, c) pair
+// only ids of {a, b, c}.  So one number per neighbour carries both changes: n_l, the sites with
+// left neighbour l (the loss of (l, a), the gain of (l, c)), and n_r likewise.  No count is
+// negative and n_l <= W, the merge's count, which never exceeds the last merge's (a pair counts at
+// most the selected max, and the pairs a merge makes at most its W): so a batch whose first merge
+// follows one of count W_0 packs lanes of bits(W_0) bits, floor(64 / bits) to a u64 word, and the
+// u64 all-reduce(SUM) adds the lanes without carries.  Lanes: left side at word j / q of the
+// lanes, right side from word lane_base on.
 constexpr uint32_t PIX_XCHG_SPECIAL = 16;
-constexpr unsigned long long PIX_LANE_MAX = 0xFFFFull;
 
-// first word (after the specials) of part q = 2 side + wide
-__device__ __forceinline__ uint32_t lr_part_base(const PixCtl *ctl, int q) {
-    const uint32_t wln = (ctl->lr_n[0] + 3u) / 4u, wrn = (ctl->lr_n[2] + 3u) / 4u;
-    const uint32_t base[4] = {0u, wln, wln + ctl->lr_n[1], wln + ctl->lr_n[1] + wrn};
-    return base[q];
-}
-
-// exchange word (after the specials) and lane shift of member o of side (0: L, 1: R), wide: a
-// word of its own; PIX_NONE when o is not a member
-__device__ __forceinline__ uint32_t lr_lane(const PixTable &t, const PixCtl *ctl, int side,
-                                            uint32_t o, uint32_t &shift, bool &wide) {
-    const uint32_t *bm = t.lr_bits + 2 * side * PIX_LR_WORDS, *bw = bm + PIX_LR_WORDS;
-    const uint32_t *pm = t.lr_pre + 2 * side * (PIX_LR_WORDS + 1), *pw = pm + PIX_LR_WORDS + 1;
-    const uint32_t w = o >> 5, bit = 1u << (o & 31u), below = bit - 1u;
-    const uint32_t m = bm[w], wd = bw[w];
-    if (!(m & bit)) return PIX_NONE;
-    wide = (wd & bit) != 0u;
-    if (wide) {
-        shift = 0;
-        return lr_part_base(ctl, 2 * side + 1) + pw[w] + (uint32_t)__popc(wd & below);
-    }
-    const uint32_t j = pm[w] - pw[w] + (uint32_t)__popc(m & ~wd & below);
-    shift = 16u * (j & 3u);
-    return lr_part_base(ctl, 2 * side) + j / 4u;
+// exchange word (after the specials) and lane shift of token o on side (0: left, 1: right)
+__device__ __forceinline__ uint32_t lane_word(const PixTable &t, int side, uint32_t o, uint32_t &shift) {
+    const uint32_t q = o / t.lane_q;
+    shift = (o - q * t.lane_q) * t.lane_w;
+    return (side ? t.lane_base : 0u) + q;
 }
 
 __device__ __forceinline__ void pix_delta(const PixTable &t, PixCtl *ctl, uint32_t key, long long d) {
     if (!d) return;
     const int32_t x = (int32_t)(key >> 16), y = (int32_t)(key & 0xFFFFu);
-    if (!t.lr_bits) {
+    if (!t.lane_w) {
         const uint32_t slot = delta_slot(x, y, ctl->a, ctl->b, ctl->c);
         if (slot == PIX_NONE) {
             pix_fail(ctl, 41);   // (cannot happen: every changed pair has its word)
@@ -275,12 +248,7 @@ __device__ __forceinline__ void pix_delta(const PixTable &t, PixCtl *ctl, uint32
     }
     if (gain) return;
     uint32_t shift;
-    bool wide;
-    const uint32_t w = lr_lane(t, ctl, side, o, shift, wide);
-    if (w == PIX_NONE) {
-        pix_fail(ctl, 41);
-        return;
-    }
+    const uint32_t w = lane_word(t, side, o, shift);
     atomicAdd(&t.delta[XCHG_HDR + PIX_XCHG_SPECIAL + w], (unsigned long long)(-d) << shift);
 }
 
@@ -1194,6 +1162,13 @@ __global__ void __launch_bounds__(1024) k_pix_select(PixTable t, PixBufs B, PixC
         }
         ctl->best = best;
         ctl->W = (unsigned long long)W;
+        if (t.lane_w && t.lane_w < 64 && ((unsigned long long)W >> t.lane_w) != 0ull) {
+            // (cannot happen while counts only fall: the lanes hold the last merge's W; a pause
+            // before any shard makes the merge, alike on every shard, rather than a carry)
+            ctl->status = PIX_PAUSE;
+            ctl->lane_over = 1;
+            return;
+        }
         // (sorted by key: the shards of a sharded corpus index their tie words alike)
         for (uint32_t i = 1; i < nc; ++i)
             for (uint32_t j = i; j > 0 && cs_key[j - 1] > cs_key[j]; --j) {
@@ -1692,113 +1667,13 @@ __global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restr
 //   rank_loop_count    k_pix_alloc, k_pix_apply (this shard's corpus and lists)
 constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
 
-// the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on; lr_cap
-// words after the specials in the compact exchange (0: the dense rows)
-__global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight,
-                                 uint32_t lr_cap) {
+// the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on
+__global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight) {
     if (ctl->status == PIX_PAUSE) ctl->status = PIX_RUN;
     ctl->n_done = 0;
     ctl->n_want = n;
     ctl->next_id = next_id;
     ctl->min_weight = min_weight;
-    ctl->lr_cap = lr_cap;
-    ctl->lr_need = 0;
-    ctl->lr_pauses = 0;
-}
-
-// The compact exchange's sets of the merge (a, b) -> c just decided (k_pix_select), from the
-// GLOBAL counts every shard holds alike: L = {x : (x, a) occurs}, R = {y : (b, y) occurs}, ids of
-// {a, b, c} aside, and their wide members (count > PIX_LANE_MAX), as bitmaps; the last block
-// writes their word prefixes and sizes.  When the words exceed the batch's capacity the batch
-// pauses before this merge (every shard alike, before any shard counts its sites): the next batch,
-// sized from lr_need, selects it again from the same counts.  Runs between k_pix_select and
-// k_pix_sites.
-__global__ void __launch_bounds__(256) k_pix_lr(PixTable t, PixCtl *ctl) {
-    __shared__ uint32_t s_go, s_last;
-    __shared__ uint32_t s_sum[4][4];
-    if (threadIdx.x == 0) s_go = ctl->status == PIX_RUN && ctl->tie == PIX_TIE_NONE;
-    __syncthreads();
-    if (!s_go) return;
-    const int32_t a = ctl->a, b = ctl->b, c = ctl->c;
-    const uint32_t nid = (uint32_t)c + 1u, nw = (nid + 31u) / 32u;
-    const int lane = threadIdx.x & 63;
-    // (one id per thread; a wave's ballots are two whole words: 64-aligned ids per wave)
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nw * 32u; x += gridDim.x * blockDim.x) {
-        unsigned long long nl = 0, nr = 0;
-        if (x < nid && (int32_t)x != a && (int32_t)x != b && (int32_t)x != c) {
-            const PixProbe pl = pix_probe(t, pix_key((int32_t)x, a));
-            const PixProbe pr = pix_probe(t, pix_key(b, (int32_t)x));
-            const uint32_t sl = pix_slot(t, ctl, pix_key((int32_t)x, a), false, false, pl);
-            const uint32_t sr = pix_slot(t, ctl, pix_key(b, (int32_t)x), false, false, pr);
-            nl = sl != PIX_NONE ? t.cnt[sl] : 0ull;
-            nr = sr != PIX_NONE ? t.cnt[sr] : 0ull;
-        }
-        const unsigned long long m[4] = {__ballot(nl != 0), __ballot(nl > PIX_LANE_MAX),
-                                         __ballot(nr != 0), __ballot(nr > PIX_LANE_MAX)};
-        if ((lane & 31) == 0 && (x >> 5) < nw)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) t.lr_bits[q * PIX_LR_WORDS + (x >> 5)] = (uint32_t)(m[q] >> lane);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        s_last = atomicAdd(&ctl->lr_ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    // exclusive prefixes of the words' set bits: each thread a contiguous range of words
-    const uint32_t per = (nw + blockDim.x - 1) / blockDim.x;
-    const uint32_t w0 = min(nw, threadIdx.x * per), w1 = min(nw, w0 + per);
-    auto bits = [&](int q, uint32_t w) {
-        return (uint32_t)__popc(__hip_atomic_load(&t.lr_bits[q * PIX_LR_WORDS + w], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT));
-    };
-    uint32_t cnt[4] = {0, 0, 0, 0};
-    for (uint32_t w = w0; w < w1; ++w)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cnt[q] += bits(q, w);
-    const int wv = threadIdx.x >> 6;
-    uint32_t incl[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        incl[q] = wave_incl_sum((int)cnt[q], lane);
-        if (lane == 63) s_sum[q][wv] = incl[q];
-    }
-    __syncthreads();
-    uint32_t tot[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t before = 0, all = 0;
-        for (int v = 0; v < 4; ++v) {
-            if (v < wv) before += s_sum[q][v];
-            all += s_sum[q][v];
-        }
-        tot[q] = all;
-        uint32_t e = before + incl[q] - cnt[q];   // (exclusive, this thread's first word)
-        for (uint32_t w = w0; w < w1; ++w) {
-            t.lr_pre[q * (PIX_LR_WORDS + 1) + w] = e;
-            e += bits(q, w);
-        }
-        if (threadIdx.x == 0) t.lr_pre[q * (PIX_LR_WORDS + 1) + nw] = all;
-    }
-    if (threadIdx.x == 0) {
-        // (narrow = members - wide)
-        const uint32_t n[4] = {tot[0] - tot[1], tot[1], tot[2] - tot[3], tot[3]};
-        const uint32_t words = (n[0] + 3u) / 4u + n[1] + (n[2] + 3u) / 4u + n[3];
-        ctl->lr_need = max(ctl->lr_need, words);
-        if (words > ctl->lr_cap) {
-            // (merge not made: k_pix_select's next run, in the next batch, selects it again; err
-            // stays clear, other checks read it)
-            ctl->status = PIX_PAUSE;
-            ctl->lr_pauses += 1;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ctl->lr_n[q] = n[q];
-            ctl->lr_words = words;
-        }
-        ctl->lr_ticket = 0;
-    }
 }
 
 // One summed count change into this shard's global counts: a fall marks the block when the entry
@@ -1847,13 +1722,14 @@ __global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, 
         }
     }
     unsigned long long *d = xchg + XCHG_HDR;
-    if (t.lr_bits) {
-        // compact (the sets of the last merge are still those k_pix_lr made for it): a thread per
-        // special word, then per id of L and of R: its lane (cleared with an atomic AND, since
-        // other threads read the other lanes of the word), n = the sites with that neighbour:
-        // side L loses (o, a) and gains (o, c); side R loses (b, o) and gains (c, o)
+    if (t.lane_w) {
+        // lanes: a thread per special word, then per token id <= c and side: its lane (cleared
+        // with an atomic AND, since other threads read the other lanes of the word), n = the sites
+        // with that neighbour: the left side loses (o, a) and gains (o, c), the right side loses
+        // (b, o) and gains (c, o)
         const uint32_t nid = (uint32_t)c + 1u;
         const uint32_t n = PIX_XCHG_SPECIAL + 2u * nid;
+        const unsigned long long mask = t.lane_w >= 64 ? ~0ull : (1ull << t.lane_w) - 1ull;
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
             if (i < PIX_XCHG_SPECIAL) {
                 if (i >= 9) continue;   // (never written)
@@ -1868,15 +1744,11 @@ __global__ void __launch_bounds__(256) k_pix_apply_delta(PixTable t, PixBufs B, 
             const int side = k >= nid;
             const int32_t o = (int32_t)(side ? k - nid : k);
             uint32_t shift;
-            bool wide;
-            const uint32_t w = lr_lane(t, ctl, side, (uint32_t)o, shift, wide);
-            if (w == PIX_NONE) continue;
-            unsigned long long *p = d + PIX_XCHG_SPECIAL + w;
-            const unsigned long long v = *p;
-            const unsigned long long cnt = wide ? v : (v >> shift) & PIX_LANE_MAX;
+            unsigned long long *p = d + PIX_XCHG_SPECIAL + lane_word(t, side, (uint32_t)o, shift);
+            const unsigned long long cnt = (*p >> shift) & mask;
             if (!cnt) continue;
-            if (wide) *p = 0;
-            else atomicAnd(p, ~(PIX_LANE_MAX << shift));
+            if (t.lane_q == 1) *p = 0;
+            else atomicAnd(p, ~(mask << shift));
             pix_global_add(t, B, ctl, side ? pix_key(b, o) : pix_key(o, a), (unsigned long long)-(long long)cnt);
             pix_global_add(t, B, ctl, side ? pix_key(c, o) : pix_key(o, c), cnt);
         }

@@ -199,8 +199,12 @@ int bpe_tie_positions(bpe_ctx *ctx, const int32_t *cand, int64_t n, uint64_t *la
  *     recount of every pair the merge (a, b) -> c touched, at HDR + 6 * other + row, rows
  *     (a, .) (b, .) (., a) (., b) (c, .) (., c) in this order of precedence.  In the
  *     incremental mode (bpe_set_mode) the global state lives in the shard's position index instead
- *     (every pair's global count beside this shard's own lists) and the same rows carry each
- *     merge's signed count CHANGES (two's complement u64; a sum of them is the global change).
+ *     (every pair's global count beside this shard's own lists) and the exchange carries each
+ *     merge's count CHANGES: 16 words for the pairs of two of {a, b, c} (signed, two's complement
+ *     u64), then per token id and side the sites with that neighbour (left: (x, a) -> (x, c);
+ *     right: (b, y) -> (c, y)) in unsigned lanes as wide as the last merge's count, packed in the
+ *     u64 words (their u64 sum adds the lanes without carries).  *xchg_words is
+ *     then 8 + 16 + 2 ceil(ids / lanes per word) for the batch's ids.
  *     A tie there takes one iteration of its own: the scan's positions cross in `tie`, and the
  *     next iteration commits the winner, so a batch may merge fewer times than it iterates.
  * tie: the tied candidates' last positions (rank << 40 | position, rule R3: rank r's occurrences
@@ -307,8 +311,6 @@ typedef struct {
     int64_t xchg_iters;       /* rank loop: iterations those bytes cover */
     int64_t pix_fallbacks;    /* multi-device context, incremental mode: times the shards' index kept
                                  handing over and the run went on in the streaming mode */
-    int64_t xchg_pauses;      /* rank loop, incremental mode: batches ended early because a merge's
-                                 compact exchange outgrew the batch's capacity (made in the next) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -41,8 +41,7 @@ def main():
                           'pix_builds': st['pix_builds'], 'pix_host': st['pix_host'],
                           'loop_host': st['loop_host'],
                           # (the exchange each shard all-reduces per iteration, over the run so far)
-                          'xchg_bytes_per_iter': st['xchg_bytes'] / shards / max(1, st['xchg_iters']),
-                          'xchg_pauses': st['xchg_pauses']}),
+                          'xchg_bytes_per_iter': st['xchg_bytes'] / shards / max(1, st['xchg_iters'])}),
               flush=True)
         if len(got) < k:
             break
