@@ -913,7 +913,17 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                     ++m->pix_fallbacks;
                     for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
                 }
-                MTRY(enter_maintained(m));
+                int erc = enter_maintained(m);
+                if (erc != BPE_OK && pix && m->pix_auto) {
+                    // (the automatic switch: the shards' indexes do not fit beside their corpora,
+                    // e.g. 2 GiB shards sharing one device; the stream goes on)
+                    m->pix_off = true;
+                    ++m->pix_fallbacks;
+                    for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
+                    for (auto s : m->sh) MTRY(bpe_leave_global(s));
+                    erc = enter_maintained(m);
+                }
+                MTRY(erc);
             }
             batch_maintained = m->maintained;
             int64_t nw = -1;
