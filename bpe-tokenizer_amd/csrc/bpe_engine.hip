@@ -2116,7 +2116,8 @@ int pix_set_global(bpe_ctx *c, const unsigned long long *table, const uint32_t *
     // every pair of the corpus at most half the table (n counts a pair once per shard holding it;
     // pix_reserve grows the table in place as merges add pairs)
     c->pix_min_cap = 2 * (uint64_t)(HOT_BINS + n);
-    rc = pix_build(c, c->opt_max_length);
+    // (BPE_PIX_FORCE_OOM=1, tests: the build fails as if out of device memory)
+    rc = getenv("BPE_PIX_FORCE_OOM") ? BPE_ERR_OOM : pix_build(c, c->opt_max_length);
     c->pix_min_cap = 0;
     if (rc == PIX_NOT_ELIGIBLE || rc == BPE_ERR_OOM) {
         if (c->pix) {

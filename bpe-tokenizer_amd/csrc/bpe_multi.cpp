@@ -893,7 +893,10 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
         // r05_kernel_stats_multi8_32k_stream.csv).  So the shards go on in the incremental mode,
         // whose merges and counts are the same.  BPE_STREAM_ONLY=1 keeps the stream.
         static const bool stream_only = getenv("BPE_STREAM_ONLY") != nullptr;
-        if (!m->pix && !stream_only && nt >= AUTO_PIX_VOCAB) {
+        // (BPE_AUTO_PIX_VOCAB=n, tests: switch at n token ids; read per batch)
+        const char *av = getenv("BPE_AUTO_PIX_VOCAB");
+        const int32_t auto_vocab = av ? (int32_t)atoi(av) : AUTO_PIX_VOCAB;
+        if (!m->pix && !stream_only && nt >= auto_vocab) {
             MTRY(multi_set_mode(m, BPE_MODE_INCREMENTAL));
             m->pix_auto = true;
         }

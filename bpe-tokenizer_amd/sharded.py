@@ -217,6 +217,10 @@ class ShardedTrainer:
         self.pix = False
         self._pix_off = False
         self._pix_entries = self._pix_merged = 0
+        # (the incremental mode came from the automatic switch; times its indexes did not fit and
+        # the stream went on)
+        self._pix_auto = False
+        self.pix_fallbacks = 0
         # RCCL backend: the rank loop's two all-reduces per iteration are issued from C++ on the
         # engine's stream (bpe_rank_loop_rccl, one call per batch); BPE_RANK_LOOP=python keeps them
         # as torch.distributed calls (A/B)
@@ -227,6 +231,7 @@ class ShardedTrainer:
         self.engine.set_mode(mode)
         self.pix = mode == 'incremental'
         self._pix_off = False
+        self._pix_auto = False
         self._pix_entries = self._pix_merged = 0
         self._maintained = False
 
@@ -352,8 +357,25 @@ class ShardedTrainer:
         all_c = torch.cat([g[:z] for g, z in zip(gc, sizes)] + [cp[:0]]).to(dev).contiguous()
         total = all_k.numel()
         torch.cuda.synchronize(dev)
-        eng.set_global_counts(table.data_ptr(), all_k.data_ptr() if total else None,
-                              all_c.data_ptr() if total else None, total)
+        pix = self.pix and not self._pix_off
+        try:
+            eng.set_global_counts(table.data_ptr(), all_k.data_ptr() if total else None,
+                                  all_c.data_ptr() if total else None, total)
+            ok = 1
+        except pkg.BpeError:
+            if not (pix and self._pix_auto):
+                raise
+            ok = 0      # (this rank's index does not fit beside its corpus)
+        if pix and self._pix_auto:
+            # every rank alike: after the automatic switch, an index that does not fit on some
+            # rank sends every rank back to the stream (as bpe_multi.cpp)
+            flag = torch.tensor([ok], dtype=torch.int32, device=cdev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                self._pix_off = True
+                self.pix_fallbacks += 1
+                eng.set_mode('stream')
+                return self.enter_maintained()
         self._maintained = True
         self._heavy_streak = 0
 
@@ -393,9 +415,10 @@ class ShardedTrainer:
             # (as bpe_multi.cpp: past AUTO_PIX_VOCAB token ids the streaming mode's maintained state
             # outgrows its LDS rows and its scans of the claimed cold pairs; the ranks go on in the
             # incremental mode, same merges.  BPE_STREAM_ONLY=1 keeps the stream)
-            if (not self.pix and self.n_tokens >= AUTO_PIX_VOCAB
+            if (not self.pix and self.n_tokens >= int(os.environ.get('BPE_AUTO_PIX_VOCAB', AUTO_PIX_VOCAB))
                     and not os.environ.get('BPE_STREAM_ONLY')):
                 self.set_mode('incremental')
+                self._pix_auto = True
             pix = self.pix and not self._pix_off
             if not self._maintained and (self._heavy_streak >= 2 or pix):
                 if pix:

@@ -10,10 +10,12 @@ pytestmark = pytest.mark.gpu
 
 
 def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40, base=60,
-           mib=3, corpus='uniform', backend='gloo', engine_mode='stream', rank_loop='native'):
+           mib=3, corpus='uniform', backend='gloo', engine_mode='stream', rank_loop='native',
+           env=None):
     import importlib
     import sys
     os.environ['BPE_RANK_LOOP'] = rank_loop
+    os.environ.update(env or {})
     import torch
     import torch.distributed as dist
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -46,7 +48,8 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
         ids, off = tr.engine.read_corpus()
         if mode != 'step':
             assert tr._native == native, (tr._native, native)   # (the path asked for ran)
-        q.put((rank, tr.merges, ids.tolist(), off.tolist(), tr.engine.stats()))
+        st = dict(tr.engine.stats(), trainer_pix_fallbacks=tr.pix_fallbacks)
+        q.put((rank, tr.merges, ids.tolist(), off.tolist(), st))
     finally:
         dist.destroy_process_group()
 
@@ -175,3 +178,16 @@ def test_rccl_incremental_rank_loop_one_rank():
     st = check(1, mode='loop', n=500, corpus='zipf', mib=8, seed=12345, backend='nccl',
                engine_mode='incremental')
     assert st[0]['pix_merges'] >= 400, st
+
+
+def test_incremental_rank_loop_automatic_switch_and_fallback():
+    """The streaming rank loop's switch to the incremental mode past a vocabulary size (18432
+    ids; BPE_AUTO_PIX_VOCAB=400 here), and, when an index build fails on some rank
+    (BPE_PIX_FORCE_OOM=1, as out of device memory), every rank's agreed fall-back to the stream:
+    the same merges and corpus as one context either way."""
+    st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=2,
+               env={'BPE_AUTO_PIX_VOCAB': '400'})
+    assert all(s['pix_merges'] >= 100 and s['trainer_pix_fallbacks'] == 0 for s in st), st
+    st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=2,
+               env={'BPE_AUTO_PIX_VOCAB': '400', 'BPE_PIX_FORCE_OOM': '1'})
+    assert all(s['pix_merges'] == 0 and s['trainer_pix_fallbacks'] >= 1 for s in st), st
