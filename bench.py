@@ -403,7 +403,7 @@ def main():
                 'select': st['select_ms'] / max(1e-9, timed_frac) / max(1, args.steps),
                 'tie_passes': st['tie_passes'],
                 'compactions': st['compactions'],
-                'exact_passes': st['exact_passes'],
+                'exact_passes': st['exact_passes'], 'cold_rebuilds': st['cold_rebuilds'],
             },
         }
         if cpu is not None:

@@ -73,6 +73,7 @@ class Stats(ctypes.Structure):
         ('pix_build_ms', ctypes.c_double), ('cold_used', ctypes.c_int64),
         ('sel_blocks', ctypes.c_int64), ('xchg_bytes', ctypes.c_int64),
         ('xchg_iters', ctypes.c_int64), ('pix_fallbacks', ctypes.c_int64),
+        ('cold_rebuilds', ctypes.c_int64),
     ]
 
     def as_dict(self):

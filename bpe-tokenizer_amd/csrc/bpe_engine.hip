@@ -336,7 +336,8 @@ int cold_clear(bpe_ctx *c) {
     return BPE_OK;
 }
 
-int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
+// the cold table's capacity for a pass that creates at most `extra` cold-token occurrences
+uint64_t cold_cap_for(const bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     uint64_t s = extra;
     for (size_t t = HOT; t < c->h_count.size(); ++t) s += (uint64_t)std::max<int64_t>(0, c->h_count[t]);
     uint64_t need = 2 * s + 16;
@@ -345,6 +346,12 @@ int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     need = std::min<uint64_t>(need, (uint64_t)c->n_live + 16);
     uint64_t cap = 1024;
     while (cap < 2 * need || cap < min_cap) cap <<= 1;
+    return cap;
+}
+
+// (reallocates empty when it grows: the contents are lost, cold_rebuild keeps them)
+int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
+    const uint64_t cap = cold_cap_for(c, extra, min_cap);
     if (cap <= c->cold_cap) return BPE_OK;
     if (cap > (1ull << 31)) return fail(BPE_ERR_OOM, "bpe native: cold pair table too large");
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -375,6 +382,74 @@ int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
     c->counts_valid = false;
     c->cold_exact = false;
     return cold_clear(c);
+}
+
+// The maintained cold table rebuilt from itself (round 5): its live claims (a count > 0: every
+// cold pair of the corpus, the table being exact) gathered out, then loaded into a cleared table
+// of at least min_cap slots and four times their number, so that the dead claims and the holes go
+// and the fill drops to a quarter.  The exact pass over the corpus it replaces took 8 ms on 1 GiB
+// of zipf words, plus the table-state iterations until the maintained state was entered again.
+bool cold_rebuild_on() {   // (BPE_COLD_REBUILD=0: the exact pass instead, A/B; read per call)
+    const char *e = getenv("BPE_COLD_REBUILD");
+    return !e || atoi(e) != 0;
+}
+
+int cold_rebuild(bpe_ctx *c, uint64_t min_cap) {
+    hipStream_t s = c->stream;
+    uint32_t flags[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+    const uint64_t n = std::min<uint64_t>(flags[0], c->cold_cap);
+    uint32_t *keys = nullptr, *d_m = nullptr;
+    unsigned long long *counts = nullptr;
+    int rc;
+    auto release = [&]() {
+        (void)hipStreamSynchronize(s);
+        dfree(keys);
+        dfree(counts);
+        dfree(d_m);
+    };
+    if ((rc = dev_alloc(&keys, std::max<uint64_t>(n, 1))) || (rc = dev_alloc(&counts, std::max<uint64_t>(n, 1))) ||
+        (rc = dev_alloc(&d_m, 1))) {
+        release();
+        return rc;
+    }
+    HIP_TRY(hipMemsetAsync(d_m, 0, sizeof(uint32_t), s));
+    k_cold_gather<<<COLD_GRID, 256, 0, s>>>(c->cold, keys, counts, d_m);
+    HIP_TRY(hipGetLastError());
+    uint32_t m = 0;
+    HIP_TRY(hipMemcpyAsync(&m, d_m, sizeof m, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // (a table that grows is reallocated empty, which drops the maintained state: restored once
+    // the live claims are back)
+    const bool counts_valid = c->counts_valid, cold_exact = c->cold_exact;
+    for (int attempt = 0;; ++attempt) {
+        if ((rc = ensure_cold(c, 0, std::max<uint64_t>(min_cap, 4 * (uint64_t)m + 4096)))) {
+            release();
+            return rc;
+        }
+        if ((rc = cold_clear(c))) {
+            release();
+            return rc;
+        }
+        if (m) k_load_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, keys, counts, m);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!flags[1]) break;
+        if (attempt == 2) {
+            release();
+            return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
+        }
+        min_cap = 2 * c->cold_cap;
+    }
+    release();
+    c->cold_used = flags[0];
+    c->counts_valid = counts_valid;
+    c->cold_exact = cold_exact;
+    if (c->stats_on) c->stats.cold_rebuilds += 1;
+    return BPE_OK;
 }
 
 float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -720,9 +795,15 @@ int select_from_table(bpe_ctx *c, const unsigned long long *table, int64_t max_l
         if ((flags & 0xFFFFFFFFu) * 4 > c->cold_cap * 3 ||
             2 * c->h_res->cold_dead > (flags & 0xFFFFFFFFu) + 65536) {
             // too full to probe well, or mostly claims whose pair is gone (every scan streams
-            // them): this selection still reads it, the next one rebuilds it
-            c->cold_exact = false;
-            c->exact_streak = 1;
+            // them): this selection has read it (its result is on the host); rebuilt from its
+            // own live claims, it stays the maintained table (BPE_COLD_REBUILD=0: the exact pass
+            // over the corpus at the next selection, as before round 5)
+            if (cold_rebuild_on()) {
+                if ((rc = cold_rebuild(c, 0))) return rc;
+            } else {
+                c->cold_exact = false;
+                c->exact_streak = 1;
+            }
         }
     } else if (local && table == c->d_hot && c->best_ready && c->best_ml == max_length) {
         // the reduce already left the best hot key in the Result: collect its pairs and the
@@ -891,16 +972,22 @@ int do_apply(bpe_ctx *c, int32_t a, int32_t b, int32_t cc, int64_t *replaced) {
     // exact pass at the next selection instead.
     bool fused = false;
     if (c->cold_exact) {
-        const uint64_t cap0 = c->cold_cap;
         const int64_t na = c->h_count[a], nb = c->h_count[b];
         const uint64_t bound = (uint64_t)std::max<int64_t>(0, a == b ? na / 2 : std::min(na, nb));
-        if ((rc = ensure_cold(c, bound))) return rc;
         // the refresh claims at most 2 * bound new slots (holes included): it must fit the
         // table's 3/4 fill limit, which counts every claim made since the last rebuild
         const uint64_t V = c->h_len16.size() + 1;
-        const bool room = c->cold_used + std::min<uint64_t>(2 * bound, V * V) + 64 <=
-                          c->cold_cap / 4 * 3;
-        fused = c->cold_exact && c->cold_cap == cap0 && room && !getenv("BPE_DEBUG_NO_FUSED");
+        const uint64_t claims = std::min<uint64_t>(2 * bound, V * V) + 64;
+        if (cold_rebuild_on() &&
+            (cold_cap_for(c, bound) > c->cold_cap || c->cold_used + claims > c->cold_cap / 4 * 3)) {
+            // a table that has to grow, or has no room for the refresh: rebuilt from its own
+            // live claims, with room for both
+            if ((rc = cold_rebuild(c, std::max(cold_cap_for(c, bound), 2 * claims)))) return rc;
+        }
+        const uint64_t cap1 = c->cold_cap;
+        if ((rc = ensure_cold(c, bound))) return rc;
+        const bool room = c->cold_used + claims <= c->cold_cap / 4 * 3 && c->cold_cap == cap1;
+        fused = c->cold_exact && room && !getenv("BPE_DEBUG_NO_FUSED");
         if (!fused) {
             c->cold_exact = false;
             c->exact_streak = 1;   // (the next exact pass rebuilds the whole table)
@@ -2326,8 +2413,7 @@ int pix_rank_select(bpe_ctx *c) {
 }
 
 int pix_rank_decide(bpe_ctx *c) {
-    k_pix_decide<<<1, 1, 0, c->stream>>>(c->pix->d_ctl, c->rl_tie);
-    HIP_TRY(hipGetLastError());
+    (void)c;   // (the decision is made by k_pix_alloc's block 0 in pix_rank_count)
     return BPE_OK;
 }
 
@@ -2335,7 +2421,7 @@ int pix_rank_count(bpe_ctx *c) {
     PixState *P = c->pix;
     hipStream_t s = c->stream;
     hipEvent_t e = span_begin(c);
-    k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl);
+    k_pix_alloc<<<PIX_GRID, 256, 0, s>>>(P->T, P->B, P->d_ctl, c->rl_tie);   // (+ k_pix_decide)
     k_pix_apply<<<PIX_GRID, 256, 0, s>>>(P->C, P->T, P->B, P->d_ctl, P->d_log);
     HIP_TRY(hipGetLastError());
     c->rl_enqueued += 1;

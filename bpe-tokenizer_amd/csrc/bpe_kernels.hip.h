@@ -2608,6 +2608,36 @@ __global__ void __launch_bounds__(256) k_apply_delta(unsigned long long *__restr
 
 // bpe_set_global_counts: (key, count) entries of every shard, duplicates summed, into the cleared
 // cold table (holes, key EMPTY or count 0, skipped).
+// The live claims of the cold table (a key, a count > 0) into dense arrays, in any order: the
+// maintained table rebuilt from itself (bpe_engine.hip cold_rebuild) instead of from the corpus.
+// (A wave-uniform loop: one atomic per wave for the output slots.)
+__global__ void __launch_bounds__(256) k_cold_gather(ColdTable ct, uint32_t *__restrict__ keys,
+                                                     unsigned long long *__restrict__ counts,
+                                                     uint32_t *__restrict__ n_out) {
+    const uint32_t n = cold_used(ct), lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+        const uint32_t i = i0 + lane;
+        uint32_t k = EMPTY;
+        unsigned long long v = 0;
+        if (i < n) {
+            k = ct.dkeys[i];
+            v = ct.dcounts[i];
+        }
+        const bool live = k != EMPTY && v != 0ull;
+        const unsigned long long m = __ballot(live);
+        if (!m) continue;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(n_out, (uint32_t)__popcll(m));
+        b = __shfl(b, 0);
+        if (live) {
+            const uint32_t j = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            keys[j] = k;
+            counts[j] = v;
+        }
+    }
+}
+
 __global__ void k_load_cold(ColdTable ct, const uint32_t *__restrict__ keys,
                             const unsigned long long *__restrict__ counts, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;

@@ -1025,6 +1025,7 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.pix_host = std::max(acc.pix_host, x.pix_host);
         acc.pix_build_ms = std::max(acc.pix_build_ms, x.pix_build_ms);
         acc.xchg_bytes += x.xchg_bytes;
+        acc.cold_rebuilds += x.cold_rebuilds;
         acc.xchg_iters = std::max(acc.xchg_iters, x.xchg_iters);
     }
     acc.pix_fallbacks = m->pix_fallbacks;

@@ -1007,8 +1007,8 @@ __global__ void k_pix_begin(PixCtl *ctl, long long n, int32_t next_id, long long
 // and k_pix_apply do nothing; the next k_pix_select commits the decided pair.  (A separate tie
 // launch cost 5.5 us per merge for the 372 ties among the 8000 C3 merges; one block scanning the
 // lists took ~240 us per tie.)
-// Sharded: the scan leaves this shard's last counted occurrences (PIX_TIE_WAIT); k_pix_decide takes
-// the earliest of the all-reduced (shard << 40 | position) after the exchange.
+// Sharded: the scan leaves this shard's last counted occurrences (PIX_TIE_WAIT); pix_decide (block 0
+// of k_pix_alloc) takes the earliest of the all-reduced (shard << 40 | position) after the exchange.
 enum PixTie { PIX_TIE_NONE = 0, PIX_TIE_SCAN = 1, PIX_TIE_DECIDED = 2, PIX_TIE_WAIT = 3 };
 
 // The merge of pair slot s (key `key`, list length len): vocabulary and table-room checks, then
@@ -1497,15 +1497,26 @@ __global__ void __launch_bounds__(256) k_pix_sites(PixCorpus C, PixTable t, PixB
     }
 }
 
+constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
+__device__ void pix_decide(PixCtl *ctl, const unsigned long long *__restrict__ tie);
+
 // Segments for this merge's new pairs, from their owner entries (one pool atomic per block), and
 // the new pairs' maxima: their counts are final now.
-__global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl) {
+// A shard of a sharded corpus (tie != nullptr): block 0 first makes k_pix_decide's decision from
+// the all-reduced tie words (one launch fewer per iteration, round 5).  Every block reads the
+// vote from the tie words itself (block 0 may not have written the status yet); a tie scan's
+// iteration (ctl->tie WAIT, then DECIDED) makes no merge either way.
+__global__ void __launch_bounds__(256) k_pix_alloc(PixTable t, PixBufs B, PixCtl *ctl,
+                                                   const unsigned long long *__restrict__ tie = nullptr) {
     __shared__ unsigned long long wsum[4], wown[4], base_s;
     __shared__ uint32_t s_ne;
-    if (threadIdx.x == 0)   // (read once and broadcast: the loop around the barriers is uniform)
-        s_ne = ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE
+    if (threadIdx.x == 0) {   // (read once and broadcast: the loop around the barriers is uniform)
+        if (tie && blockIdx.x == 0) pix_decide(ctl, tie);
+        const bool vote = tie && tie[PIX_VOTE];
+        s_ne = vote || ctl->status != PIX_RUN || ctl->tie != PIX_TIE_NONE
                    ? 0u
                    : min(ctl->a != ctl->b ? 2 * ctl->n_sites : ctl->n_ent, B.ent_cap);
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t ne = s_ne;
@@ -1662,10 +1673,11 @@ __global__ void __launch_bounds__(256) k_pix_live_scatter(const int32_t *__restr
 //                      k_pix_dirty, k_pix_select, k_pix_sites (this shard's sites and count changes
 //                      into its delta rows; or the tie scan), k_pix_export (tie words and vote)
 //   [all-reduce(MAX) of the tie words]
-//   rank_loop_decide   k_pix_decide (a vote hands the iteration to the host on every shard alike; a
-//                      tie goes to the earliest (shard << 40 | last counted occurrence))
-//   rank_loop_count    k_pix_alloc, k_pix_apply (this shard's corpus and lists)
-constexpr int PIX_VOTE = MAX_CAND;       // tie word of the hand-off vote (BPE_TIE_WORDS >= 17)
+//   rank_loop_decide   nothing (round 5: its decision is the first thing k_pix_alloc does)
+//   rank_loop_count    k_pix_alloc: pix_decide in block 0 (a vote hands the iteration to the host
+//                      on every shard alike; a tie goes to the earliest (shard << 40 | last
+//                      counted occurrence)), then the new pairs' segments; k_pix_apply (this
+//                      shard's corpus and lists)
 
 // the batch: n iterations (each a merge or a tie scan) from vocabulary id next_id on
 __global__ void k_pix_rank_begin(PixCtl *ctl, long long n, int32_t next_id, long long min_weight) {
@@ -1806,7 +1818,7 @@ __global__ void k_pix_export(PixCtl *ctl, unsigned long long *__restrict__ xchg,
 // the host (the corpus is still the last merge's: k_pix_apply has not run), a tie scan's winner is
 // the candidate whose last counted occurrence is earliest (R3, core.ts:294-305), committed by the
 // next k_pix_select.
-__global__ void k_pix_decide(PixCtl *ctl, const unsigned long long *__restrict__ tie) {
+__device__ void pix_decide(PixCtl *ctl, const unsigned long long *__restrict__ tie) {
     if (ctl->status == PIX_ERROR || ctl->status == PIX_DONE || ctl->status == PIX_PAUSE) return;
     if (tie[PIX_VOTE]) {
         if (ctl->status == PIX_RUN) {

@@ -311,6 +311,8 @@ typedef struct {
     int64_t xchg_iters;       /* rank loop: iterations those bytes cover */
     int64_t pix_fallbacks;    /* multi-device context, incremental mode: times the shards' index kept
                                  handing over and the run went on in the streaming mode */
+    int64_t cold_rebuilds;    /* maintained state: cold pair tables rebuilt from their own live
+                                 claims (instead of an exact pass over the corpus) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

@@ -529,6 +529,30 @@ def test_zipf_maintained_rows_past_16_bits():
     assert e.stats()['fused_passes'] > 0, e.stats()
 
 
+def test_cold_table_rebuilt_from_itself(monkeypatch):
+    """The maintained cold table, when too full or mostly dead claims, is rebuilt from its own live
+    claims (round 5, cold_rebuild) instead of by an exact pass over the corpus and table-state
+    passes until the maintained state is entered again (BPE_COLD_REBUILD=0, the earlier path):
+    the same merges and final corpus, fewer exact passes, more merges in the maintained state."""
+    data = pkg.synth_zipf(256 << 20, seed=31)
+    runs = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('BPE_COLD_REBUILD', flag)
+        e = pkg.Engine(0)
+        e.stats_enable(True)
+        e.add_latin1(data, sample_bytes=1 << 20)
+        got = e.merge_until(0, 2, 3000)
+        flat, off = e.read_corpus()
+        runs[flag] = (got, flat, off, e.stats())
+        e.close()
+    assert runs['1'][0] == runs['0'][0]
+    assert np.array_equal(runs['1'][1], runs['0'][1]) and np.array_equal(runs['1'][2], runs['0'][2])
+    st1, st0 = runs['1'][3], runs['0'][3]
+    assert st1['cold_rebuilds'] >= 1 and st0['cold_rebuilds'] == 0, (st1, st0)
+    assert st1['exact_passes'] < st0['exact_passes'], (st1, st0)
+    assert st1['fused_passes'] > st0['fused_passes'], (st1, st0)
+
+
 @pytest.mark.slow
 def test_cold_pair_count_beyond_2_32():
     """A cold pair whose count exceeds 2^32 (the reference's Map counts are JS numbers, exact to
