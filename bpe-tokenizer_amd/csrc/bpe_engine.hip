@@ -389,7 +389,10 @@ int ensure_cold(bpe_ctx *c, uint64_t extra, uint64_t min_cap = 0) {
 // of at least min_cap slots and four times their number, so that the dead claims and the holes go
 // and the fill drops to a quarter.  The exact pass over the corpus it replaces took 8 ms on 1 GiB
 // of zipf words, plus the table-state iterations until the maintained state was entered again.
-bool cold_rebuild_on() {   // (BPE_COLD_REBUILD=0: the exact pass instead, A/B; read per call)
+// BPE_COLD_REBUILD=0: the exact pass instead (A/B; read per call).  (Rebuilding also ahead of a
+// batch at half fill, so that the batch hands no iteration over for it, timed 0.2 % slower on
+// zipf C3: profiles/r05_ab_cold_rebuild.txt)
+bool cold_rebuild_on() {
     const char *e = getenv("BPE_COLD_REBUILD");
     return !e || atoi(e) != 0;
 }
