@@ -938,27 +938,32 @@ __device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, 
     }
 }
 
-// The LDS adds of a fast-path chunk; their returned words go to o, screened at the end of the
+// The words a fast-path count's LDS adds returned (0 when the chunk took another path), and their
+// byte addresses.  Each stage of a ring round keeps its own, and they are all screened together at
+// the round's end, so the waves wait on LDS returns once per RING chunks, not once per chunk.
+// (Screening each chunk's returns one stage later left the compiler a wait for every add still
+// in flight at each stage: 5 % of the pass.)  The addresses let the screen sweep just the words
+// its adds saw at >= 0x4000 (round 5; see screen_round).
+struct Defer {
+    uint32_t o[4];
+    uint32_t a[4];
+};
+
+// The LDS adds of a fast-path chunk; their returned words and
+// addresses go to df, screened at the end of the
 // ring round (Returns), so no wave waits on its LDS atomics' return before then.
 template <bool FUSED = false>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
-                                          const Sink &k, uint32_t (&o)[4]) {
+                                          const Sink &k, Defer &df) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t addr, inc;
         pair_slot<FUSED>(x[e], y[e], addr, inc);
-        o[e] = atomicAdd(lds_word(k, addr), inc);
+        df.o[e] = atomicAdd(lds_word(k, addr), inc);
+        df.a[e] = addr;
     }
 }
 
-// The words a fast-path count's LDS adds returned (0 when the chunk took another path).  Each
-// stage of a ring round keeps its own, and they are all screened together at the round's end, so
-// the waves wait on LDS returns once per RING chunks, not once per chunk.  (Screening each chunk's
-// returns one stage later left the compiler a wait for every add still in flight at each stage:
-// 5 % of the pass.)
-struct Defer {
-    uint32_t o[4];
-};
 
 // The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (MODE_FUSED's refresh
 // of the maintained cold table): per-token membership masks (compares into lane masks,
@@ -1051,7 +1056,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             // one form for every chunk: 12 VALU per pair, both classes (a separate 5-VALU form
             // for chunks of hot tokens only paid off only on a fresh corpus; telling the two
             // apart cost more over a whole run: dropping it timed the C3 run 3 % faster)
-            add_pairs<MODE == MODE_FUSED>(x, y, k, df.o);
+            add_pairs<MODE == MODE_FUSED>(x, y, k, df);
             if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
@@ -1092,6 +1097,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
                     // `lane` is a row 0 counter, so its return can only raise a false alarm)
                     df.o[e] = atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + ba),
                                         (uint32_t)inrow << (((uint32_t)idx & 1u) << 4));
+                    df.a[e] = ba;
                     hsh |= (unsigned long long)(act & !inrow) << e;
                 }
                 if (__ballot(hsh != 0ull) != 0ull) {
@@ -1398,18 +1404,37 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         Defer D[RING];
         static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
             D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
+            D[i].a[0] = D[i].a[1] = D[i].a[2] = D[i].a[3] = 0u;
         });
-        // The overflow screen of a round (MODE_TABLE / MODE_FUSED): every word the wave's adds
-        // returned since the last screen, then a sweep if some half stood at >= 0x4000 (lds_sweep)
+        // The overflow screen of a round (MODE_TABLE / MODE_FUSED / MODE_INCR): every word the
+        // wave's adds returned since the last screen; where a half stood at >= 0x4000, a sweep.
+        // The fast path's adds kept their addresses: each lane sweeps just the words its adds saw
+        // high (sweep_word: an atomic AND, so lanes and waves sweeping one word take its bits
+        // once).  The next add to a half that crossed 0x4000 sees it high, and its wave sweeps it
+        // at the end of that round: the bound of the whole-table sweep, 0x4000 + the adds of one
+        // round of every wave (the static_assert on RING).  The exact path's adds (s.seen) kept
+        // no address: the whole table then, as before round 5.  (Early on a skewed corpus a few
+        // pairs hold most of a workgroup's counts: every round swept all 40960 words, and a pass
+        // took 4 ms instead of 0.6.)
         auto screen_round = [&]() __attribute__((always_inline)) {
             if (MODE != MODE_TABLE && MODE != MODE_FUSED && MODE != MODE_INCR) return;
-            uint32_t acc = s.seen;
+            const bool whole = __ballot((s.seen & SWEEP_BITS) != 0u) != 0ull;
             s.seen = 0;
+            uint32_t acc = 0;
             static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
                 acc |= D[i].o[0] | D[i].o[1] | D[i].o[2] | D[i].o[3];
+            });
+            if (!whole && __ballot((acc & SWEEP_BITS) != 0u) != 0ull) {
+                unsigned long long *sp = MODE == MODE_INCR ? rspill : spill;
+                static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) sweep_word(hist, sp, (int)(D[i].a[e] >> 2), D[i].o[e]);
+                });
+            }
+            static_for<0, RING>([&](auto i) __attribute__((always_inline)) {
                 D[i].o[0] = D[i].o[1] = D[i].o[2] = D[i].o[3] = 0u;
             });
-            if (__ballot((acc & SWEEP_BITS) != 0u) != 0ull) {
+            if (whole) {
                 if (MODE == MODE_INCR) {
                     const int vl = incr_vlim(mc);
                     for (int rw = 0; rw < 4; ++rw)
