@@ -239,6 +239,26 @@ def encode_line(args, merges, n_texts=100000, lo=16, hi=1024, reps=5):
             'cpu_baseline': encode_cpu_baseline(ids, off, abc, out, oo)}
 
 
+def maintained_roofline(st, traffic):
+    """Roofline of the device loop's maintained-state passes alone (k_step_loop<MODE_INCR>, the
+    stats' incr_* fields: HIP events over every 8th iteration, live tokens over all of them), or
+    None when the run made none."""
+    if not st.get('incr_timed'):
+        return None
+    k_ms = st['incr_ms'] / st['incr_timed']
+    alg = ALG_BYTES_PER_PAIR_SCAN * st['incr_live'] / max(1, st['incr_launches'])
+    achieved = alg / (k_ms * 1e-3) / 1e9
+    out = {'bound': 'hbm', 'kernel': 'k_step_loop<MODE_INCR> (apply + recount of the pairs '
+                                     'touching the merge)',
+           'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+           'frac': achieved / HBM_PEAK_GBS, 'kernel_avg_ms': k_ms, 'launches': st['incr_launches'],
+           'alg_bytes_per_launch': alg, 'traffic': None}
+    if 'MODE_INCR' in str(traffic.get('kernel', '')) or traffic.get('kernel') == 'k_step_loop<4>':
+        out['traffic'] = traffic.get('traffic_bytes_per_launch')
+        out['traffic_source'] = traffic.get('source')
+    return out
+
+
 def fixture_check(args, merges):
     """The run's merge list against the threaded CPU restatement's run of the same workload
     (tests/golden/config3_cpu_mt_8000.json for C3, zipf_cpu_mt_2000.json for the skewed variant;
@@ -392,6 +412,9 @@ def main():
                 'traffic_write_bytes': traffic.get('write_bytes_per_launch'),
                 'traffic_source': traffic.get('source'),
             },
+            # (the maintained state's passes on their own: the skewed corpus's pass once its
+            # table state is left, the kernel the zipf counters in current_pmc_zipf.json are of)
+            'roofline_maintained_pass': maintained_roofline(st, traffic),
             # (identity of the run's merge list across builds and modes: sha256 of the (a, b, W)
             # triples as int64, warmup merges included)
             'merges_sha256': hashlib.sha256(

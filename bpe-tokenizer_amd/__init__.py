@@ -73,7 +73,9 @@ class Stats(ctypes.Structure):
         ('pix_build_ms', ctypes.c_double), ('cold_used', ctypes.c_int64),
         ('sel_blocks', ctypes.c_int64), ('xchg_bytes', ctypes.c_int64),
         ('xchg_iters', ctypes.c_int64), ('pix_fallbacks', ctypes.c_int64),
-        ('cold_rebuilds', ctypes.c_int64),
+        ('cold_rebuilds', ctypes.c_int64), ('incr_ms', ctypes.c_double),
+        ('incr_timed', ctypes.c_int64), ('incr_launches', ctypes.c_int64),
+        ('incr_live', ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -488,9 +488,13 @@ int flush_spans(bpe_ctx *c) {
     HIP_TRY(hipEventSynchronize(c->spans.back().b));
     for (auto &sp : c->spans) {
         const double ms = ev_ms(sp.a, sp.b);
-        if (sp.kind == 0) {
+        if (sp.kind == 0 || sp.kind == 2) {   // (2: a maintained-state pass, MODE_INCR)
             c->stats.step_ms += ms;
             c->stats.step_timed += 1;
+            if (sp.kind == 2) {
+                c->stats.incr_ms += ms;
+                c->stats.incr_timed += 1;
+            }
         }
         else c->stats.select_ms += ms;
         c->ev_pool.push_back(sp.a);
@@ -1088,18 +1092,22 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
         }
         // the decision, the R3 tie pass when tied, and its commit: one launch
         k_tie_fused<<<(c->R + 3) / 4, 256, 0, s>>>(A, c->d_len16, c->d_log, c->d_ticket);
+        // (the maintained tables' entries touching the merge, zeroed for the pass to recount:
+        // timed with the selection, so that the pass's span is the pass kernel alone)
+        if (maint && c->use_incr)
+            k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl,
+                                                        c->d_len16, max_length);
+        else if (maint)
+            k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, c->d_ctl);
         HIP_TRY(hipGetLastError());
         if ((rc = span_end(c, e_sel, 1))) return rc;
         hipEvent_t e_step = span_begin(c);
         if (maint && c->use_incr) {
-            k_incr_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, c->d_hot, -1, -1, c->d_ctl,
-                                                        c->d_len16, max_length);
             k_step_loop<MODE_INCR><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
                                                        c->d_carry, c->d_ctl, c->d_partials,
                                                        c->d_spill, c->cold, c->d_sums,
                                                        &c->d_res->replaced, c->d_hot);
         } else if (maint) {
-            k_cold_invalidate<<<COLD_GRID, 256, 0, s>>>(c->cold, -1, -1, c->d_ctl);
             k_step_loop<MODE_FUSED><<<c->G, WG, 0, s>>>(c->d_ids, c->n_chunks, c->cpr, c->R,
                                                         c->d_carry, c->d_ctl, c->d_partials,
                                                         c->d_spill, c->cold, c->d_sums,
@@ -1111,7 +1119,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
                                                      &c->d_res->replaced));
         }
         HIP_TRY(hipGetLastError());
-        if ((rc = span_end(c, e_step, 0))) return rc;
+        if ((rc = span_end(c, e_step, maint && c->use_incr ? 2 : 0))) return rc;
         hipEvent_t e_red = span_begin(c);
         if (maint && c->use_incr) {
             k_runs<MODE_INCR><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
@@ -1170,6 +1178,10 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
             c->stats.step_launches += 1;
             c->stats.step_slots += c->n_chunks * CHUNK;
             c->stats.step_live += c->n_live;
+            if (maint && c->use_incr) {
+                c->stats.incr_launches += 1;
+                c->stats.incr_live += c->n_live;
+            }
         }
         out_abw[3 * i] = a;
         out_abw[3 * i + 1] = b;

@@ -1026,6 +1026,10 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.pix_build_ms = std::max(acc.pix_build_ms, x.pix_build_ms);
         acc.xchg_bytes += x.xchg_bytes;
         acc.cold_rebuilds += x.cold_rebuilds;
+        acc.incr_ms = std::max(acc.incr_ms, x.incr_ms);
+        acc.incr_timed = std::max(acc.incr_timed, x.incr_timed);
+        acc.incr_launches += x.incr_launches;
+        acc.incr_live += x.incr_live;
         acc.xchg_iters = std::max(acc.xchg_iters, x.xchg_iters);
     }
     acc.pix_fallbacks = m->pix_fallbacks;

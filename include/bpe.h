@@ -313,6 +313,11 @@ typedef struct {
                                  handing over and the run went on in the streaming mode */
     int64_t cold_rebuilds;    /* maintained state: cold pair tables rebuilt from their own live
                                  claims (instead of an exact pass over the corpus) */
+    double incr_ms;           /* the device loop's maintained-state passes (k_step_loop<MODE_INCR>)
+                                 among the timed step spans: their durations, */
+    int64_t incr_timed;       /* ... their number, */
+    int64_t incr_launches;    /* ... all such passes, */
+    int64_t incr_live;        /* ... and the live corpus tokens summed over them (pair-scans) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);
