@@ -336,6 +336,32 @@ def test_incremental_exchange_lanes_vs_dense_rows(monkeypatch):
     assert per_merge['lanes'] * 8 < per_merge['dense'], per_merge
 
 
+def test_incremental_exchange_lanes_across_max_length_changes():
+    """The lane layout bounds each count by the last merge's W, which holds while the selection's
+    filter stays: a call with max_length set, then one without (pairs the filter held back, with
+    counts above the last W, become selectable: the layout must go back to full words), then one
+    with it again.  4 shards against one context, the same calls."""
+    data = pkg.synth_zipf(16 << 20, seed=404)
+    calls = [(4, 300), (0, 300), (6, 300)]
+    one = pkg.Engine(0)
+    one.add_latin1(data, sample_bytes=1 << 20)
+    want = [one.merge_until(ml, 2, k) for ml, k in calls]
+    ids1, _ = one.read_corpus()
+    one.close()
+    multi = pkg.Engine(devices=[0] * 4, reduce='host')
+    multi.add_latin1(data, sample_bytes=1 << 20)
+    multi.set_mode('incremental')
+    multi.stats_enable(True)
+    got = [multi.merge_until(ml, 2, k) for ml, k in calls]
+    st = multi.stats()
+    ids, _ = multi.read_corpus()
+    multi.close()
+    assert got == want
+    assert np.array_equal(ids, ids1)
+    # (a few iterations go to the host protocol here, as in one context: ties of many candidates)
+    assert st['pix_merges'] >= 4 * 800 and st['pix_host'] <= 6, st
+
+
 def test_automatic_switch_to_the_incremental_mode_and_its_fallback(monkeypatch):
     """The streaming mode's switch to the incremental mode past a vocabulary size (18432 ids;
     BPE_AUTO_PIX_VOCAB=600 here), and its fall-back to the stream when the shards' indexes do not
