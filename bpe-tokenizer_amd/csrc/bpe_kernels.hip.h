@@ -303,14 +303,17 @@ __device__ __forceinline__ uint32_t pair_key(int32_t x, int32_t y) {
     return ((uint32_t)x << 16) | (uint32_t)y;
 }
 
-// Sketch hash of a cold pair: h = x * SKETCH_K + y (one v_mad_u32_u24), sketch dword
-// h & 0x1FFF = (x * K + y) mod 8192 (K odd).  Consecutive ids land in consecutive dwords, so the
-// merged tokens (allocated in sequence) spread evenly.
+// Sketch hash of a cold pair: h = y * SKETCH_K + (x >> 1) (one v_mad_u32_u24), sketch dword
+// h & 0x1FFF = (y * K + x / 2) mod 8192 (K odd), its half x & 1.  Consecutive ids land in
+// consecutive bins, so the merged tokens (allocated in sequence) spread evenly.  (Round 5: y
+// multiplied, x halved, so that the fast path forms 4 h from the x << 1 its hot address uses and
+// the sketch address in one more bit operation, pair_slot.  Round 4's x * K + y; a bucket of the
+// ids' low bits alone, with no multiply, collided: profiles/r05_ab_sketch_low.txt.)
 constexpr uint32_t SKETCH_K = 0x19B1u;
 __device__ __forceinline__ uint32_t sketch_hash(int32_t x, int32_t y) {
     // (written out: left to itself the compiler may widen this to a 64-bit multiply-add)
     uint32_t h;
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(x), "s"(SKETCH_K), "v"(y));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(y), "s"(SKETCH_K), "v"((uint32_t)x >> 1));
     return h;
 }
 
@@ -348,6 +351,8 @@ struct Sink {
     // rows (summed over the ranks, then added to every rank's copy of the global tables by
     // k_apply_delta) instead of straight into the tables
     unsigned long long *delta;
+    // HOT_BYTES in a VGPR: the third operand of the fast path's sketch address (pair_slot)
+    uint32_t hot_bytes_v;
 };
 
 // Delta rows of the sharded maintained state (include/bpe.h BPE_XCHG_*): the pairs a merge
@@ -442,14 +447,6 @@ __device__ __forceinline__ uint32_t hot_inc(int32_t x) {
 // byte address of sketch dword HOT_BINS / 2 + (h & 0x1FFF)
 __device__ __forceinline__ uint32_t cold_addr(uint32_t h) { return HOT_BYTES | ((h & 0x1FFFu) << 2); }
 
-// The same from the pair, as two instructions (the compiler otherwise re-associates the mask and
-// the shift into three, for lack of a second literal operand)
-__device__ __forceinline__ uint32_t cold_addr_of(int32_t x, int32_t y) {
-    uint32_t b, a;
-    asm("v_bfe_u32 %0, %1, 0, 13" : "=v"(b) : "v"(sketch_hash(x, y)));
-    asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(a) : "v"(b), "s"(HOT_BYTES));
-    return a;
-}
 
 __device__ __forceinline__ uint32_t *lds_word(const Sink &k, uint32_t addr) {
     return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(k.hist) + addr);
@@ -925,15 +922,25 @@ struct Tally {
 // FUSED (the maintained cold table counts the cold pairs): a cold pair adds 0 to a hot dword (its
 // address masked into the hot table) instead of going to the sketch.
 template <bool FUSED = false>
-__device__ __forceinline__ void pair_slot(int32_t x, int32_t y, uint32_t &addr, uint32_t &inc) {
+__device__ __forceinline__ void pair_slot(const Sink &k, int32_t x, int32_t y, uint32_t &addr,
+                                          uint32_t &inc) {
     uint32_t u = ~((uint32_t)x | (uint32_t)y);
     asm("" : "+v"(u));
-    const uint32_t hot = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
     if (FUSED) {
+        const uint32_t hot = (((uint32_t)x << 1) & 0x1FCu) | ((uint32_t)y << 9);
         addr = hot & (HOT_BYTES - 4);
         inc = (uint32_t)(u >= 0xFFFFFF00u) << (((uint32_t)x << 4) & 31u);   // both ids < 256
     } else {
-        addr = sel(u >= 0xFFFFFF00u, hot, cold_addr_of(x, y));   // both ids < 256
+        // both addresses as (a & b) | c (v_bitop3 table 0xEA): the hot one from x << 1 and
+        // y << 9; the sketch one from 4 h = y * 4K + (x << 1) (the sketch hash times 4: its
+        // dword's byte offset in bits 2..14) and HOT_BYTES
+        const uint32_t x2 = (uint32_t)x << 1;
+        uint32_t hot, h4, cold;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea"
+            : "=v"(hot) : "v"(x2), "s"(0x1FCu), "v"((uint32_t)y << 9));
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h4) : "v"(y), "s"(4u * SKETCH_K), "v"(x2));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(cold) : "v"(h4), "s"(0x7FFCu), "v"(k.hot_bytes_v));
+        addr = sel(u >= 0xFFFFFF00u, hot, cold);   // both ids < 256
         inc = (u >> 31) << (((uint32_t)x << 4) & 31u);
     }
 }
@@ -958,7 +965,7 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t addr, inc;
-        pair_slot<FUSED>(x[e], y[e], addr, inc);
+        pair_slot<FUSED>(k, x[e], y[e], addr, inc);
         df.o[e] = atomicAdd(lds_word(k, addr), inc);
         df.a[e] = addr;
     }
@@ -1350,6 +1357,8 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
     k.hot = hot_g;
     k.rspill = rspill;
     k.delta = delta;
+    k.hot_bytes_v = HOT_BYTES;
+    asm volatile("" : "+v"(k.hot_bytes_v));   // (kept in a VGPR for the whole pass)
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6)));
     if (r < R) {

@@ -153,7 +153,7 @@ int bpe_merge_until(bpe_ctx *ctx, int64_t max_length, int64_t min_weight, int64_
  *
  * The pair-count table has BPE_TABLE_BINS u64 entries: [0, 65536) exact counts of the pairs with
  * both ids < 256 at b*256+a, [65536, 81920) a count sketch of every other pair (bucket =
- * ((a * 0x19B1 + b) mod 8192) * 2 + (a & 1)): an upper bound of each such pair's count. */
+ * ((b * 0x19B1 + a / 2) mod 8192) * 2 + (a & 1)): an upper bound of each such pair's count. */
 #define BPE_HOT_BINS 65536
 #define BPE_TABLE_BINS 81920
 

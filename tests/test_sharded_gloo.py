@@ -26,7 +26,7 @@ def index(a, b):
     """Table index of libbpe's pair table (include/bpe.h): hot bin, or cold sketch bucket."""
     if a < 256 and b < 256:
         return (b << 8) | a
-    h = ((a & 0xFFFFFF) * 0x19B1 + (b & 0xFFFFFF)) & 0xFFFFFFFF
+    h = ((b & 0xFFFFFF) * 0x19B1 + (a >> 1)) & 0xFFFFFFFF
     return 65536 + (((h & 0x1FFF) << 1) | (a & 1))
 
 
