@@ -911,14 +911,12 @@ struct Tally {
     uint32_t seen;       // (per lane) OR of the words the exact path's LDS adds returned
 };
 
-// LDS adds of one chunk's pairs (x[e], y[e]), then the overflow screen.  Per pair: the hot
-// address (three operations), the increment (two, shared by both classes: a sketch bucket's
-// half is also x & 1), and, when the chunk has cold pairs, the sketch address (four) and a
-// select.  Pairs that do not count add 0; their address stays inside the table.
-// Per pair: the hot address (three operations), the sketch address (three), u = ~(x | y) (one,
-// opaque to the compiler so both uses below read it as is), the class select (two), and the
-// increment (three): hot_inc(x) for a valid pair, 0 when a side is negative (SEP, dead), with the
-// validity bit (u's sign) as the value shifted.  Pairs with a cold side go to their sketch bucket.
+// LDS adds of one chunk's pairs (x[e], y[e]), then the overflow screen.  Per pair (11 VALU): the
+// hot address (three operations: x << 1, y << 9, one bit operation), the sketch address (two:
+// a multiply-add on x << 1, one bit operation), u = ~(x | y) (one, opaque to the compiler so both
+// uses below read it as is), the class select (two), and the increment (three): hot_inc(x) for a
+// valid pair, 0 when a side is negative (SEP, dead), with the validity bit (u's sign) as the value
+// shifted.  Pairs with a cold side go to their sketch bucket (its half is also x & 1).
 // FUSED (the maintained cold table counts the cold pairs): a cold pair adds 0 to a hot dword (its
 // address masked into the hot table) instead of going to the sketch.
 template <bool FUSED = false>
@@ -1060,7 +1058,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
         // every X X pair starts its run, so every valid pair counts
         const int32_t x[4] = {t0, t1, t2, x3}, y[4] = {t1, t2, t3, r3};
         if (MODE == MODE_TABLE || MODE == MODE_FUSED) {
-            // one form for every chunk: 12 VALU per pair, both classes (a separate 5-VALU form
+            // one form for every chunk: 11 VALU per pair, both classes (a separate 5-VALU form
             // for chunks of hot tokens only paid off only on a fresh corpus; telling the two
             // apart cost more over a whole run: dropping it timed the C3 run 3 % faster)
             add_pairs<MODE == MODE_FUSED>(x, y, k, df);
