@@ -1472,6 +1472,13 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             } else {
                 cur = prv;   // rare: hand the pending chunk on
             }
+            // (prv kept live past the hand-on's merge of two register sets, so the register
+            // allocator gives the merged chunk cur's registers and puts the copies on the rare
+            // path: 7 -> 2 register moves per stage, C3 pass -0.9 %; in the other modes it timed
+            // 2 % slower on the skewed corpus; profiles/r05_ab_handon_live.txt)
+            if (MODE == MODE_TABLE)
+                asm volatile("" ::"v"(prv.t[0]), "v"(prv.t[1]), "v"(prv.t[2]), "v"(prv.t[3]),
+                             "s"(prv.last), "s"(prv.first), "s"(prv.len));
         };
         if (nc > 0) {
             Chunk S[RING];   // (constant indices only: the ring stays in registers)
