@@ -12,7 +12,8 @@
 #   prof       rocprofv3 --kernel-trace --stats of the full C3 bench (kernel stats CSV)
 #   profzipf   the same for zipf C3
 #   profpix    the same for the incremental mode (tools/pix_bench.py, full C3)
-#   pmc        FETCH_SIZE and WRITE_SIZE passes (300 C3 merges), summarised by tools/pmc_summary.py
+#   pmc        FETCH_SIZE and WRITE_SIZE passes (PMC_STEPS C3 merges, default 300; the bench's own
+#              7995 give per-launch bytes comparable with its roofline), by tools/pmc_summary.py
 #   sq         two SQ counter passes (300 C3 merges), summarised by tools/sq_loop_summary.py
 #   probe      tools/probe/bin/stream_probe3 (loads in flight x VALU work per chunk)
 #   rccl       the RCCL legs at world 1: tools/sharded_overhead.py (per-iteration cost)
@@ -27,7 +28,7 @@
 #   sqenc      SQ counter passes and FETCH_SIZE of the device encoder (tools/encode_bench.py, zipf
 #              merges, 20 000 texts), summarised per k_encode launch (tools/sq_loop_summary.py),
 #              under TAG/enc (apart from the sq / pmc steps' directories)
-# Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), BPE_LIB (A/B builds)
+# Environment: BENCH_EXTRA (extra bench.py flags), PMC_CORPUS (uniform|zipf), PMC_STEPS, BPE_LIB (A/B builds)
 set -o pipefail
 TAG=${1:?tag}; shift
 OUT=gpurun_out/$TAG
@@ -37,7 +38,7 @@ fail() { echo "step $1 failed"; tail -40 "$2"; exit 1; }
 prof_stats() {  # $1 dir: print the top kernels of the stats CSV
   find "$1" -name '*kernel_stats.csv' -exec head -14 {} \;
 }
-PMC_BENCH="bench.py --steps 300 --warmup 5 --no-cpu-baseline ${PMC_CORPUS:+--corpus $PMC_CORPUS}"
+PMC_BENCH="bench.py --steps ${PMC_STEPS:-300} --warmup 5 --no-cpu-baseline ${PMC_CORPUS:+--corpus $PMC_CORPUS}"
 for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
