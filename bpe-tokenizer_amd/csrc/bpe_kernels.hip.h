@@ -1625,7 +1625,22 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
                        int32_t mb = -1, int32_t mc = -1, unsigned long long *hot = nullptr,
                        unsigned long long *delta = nullptr) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R || loop_off(ctl)) return;
+    if (r >= R) return;
+    // the region and its two neighbours, loaded together before anything else (the loop's state
+    // included): one memory latency for the common case, where both neighbours are non-empty and
+    // no run crosses a boundary.  (Walking to the neighbours first made a chain of four dependent
+    // loads, each a round trip to memory for sums another XCD's L2 wrote: 4.9 us per launch.)
+    RegionSum empty;
+    empty.n_live = 0;
+    empty.lead_len = 0;
+    empty.first_tok = NONE;
+    empty.last_tok = NONE;
+    empty.uniform = 0;
+    empty.trail_odd = 0;
+    const RegionSum me = s[r];
+    const RegionSum sl = r > 0 ? s[r - 1] : empty;
+    const RegionSum sr = r + 1 < R ? s[r + 1] : empty;
+    if (loop_off(ctl)) return;
     if ((MODE == MODE_FUSED || MODE == MODE_INCR) && ctl) {   // (device loop: the merge applied)
         ma = ctl->a;
         mb = ctl->b;
@@ -1642,36 +1657,47 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     k.hot = hot;
     k.rspill = nullptr;
     k.delta = delta;
-    const int p = prev_nonempty(s, r - 1);
-    const int nx = next_nonempty(s, r + 1, R);
+    // the nearest non-empty regions before and after (rarely past the immediate neighbours)
+    int p = r - 1;
+    RegionSum P = sl;
+    if (p >= 0 && P.n_live == 0) {
+        p = prev_nonempty(s, p - 1);
+        P = p >= 0 ? s[p] : empty;
+    }
+    int nx = r + 1;
+    RegionSum N = sr;
+    if (nx < R && N.n_live == 0) {
+        nx = next_nonempty(s, nx + 1, R);
+        N = nx < R ? s[nx] : empty;
+    }
     RegionCarry rc;
-    rc.prev_tok = p >= 0 ? s[p].last_tok : SEP;
-    rc.next_tok = nx < R ? s[nx].first_tok : SEP;
+    rc.prev_tok = p >= 0 ? P.last_tok : SEP;
+    rc.next_tok = nx < R ? N.first_tok : SEP;
     rc.carry_off = 0;
-    const RegionSum me = s[r];
     if (me.n_live == 0) {
         carry[r] = rc;
         return;
     }
     const int32_t x0 = me.first_tok;
-    const bool linked = p >= 0 && x0 >= 0 && s[p].last_tok == x0;
+    const bool linked = p >= 0 && x0 >= 0 && P.last_tok == x0;
     if (linked) {
         // parity of the number of x0 tokens of the run before this region
         int64_t par = 0;
         for (int q = p; q >= 0;) {
-            if (s[q].uniform) {
-                par ^= s[q].n_live & 1;
+            const RegionSum Q = q == p ? P : s[q];
+            if (Q.uniform) {
+                par ^= Q.n_live & 1;
                 const int q2 = prev_nonempty(s, q - 1);
                 if (q2 >= 0 && s[q2].last_tok == x0) q = q2;
                 else break;
             } else {
-                par ^= s[q].trail_odd;
+                par ^= Q.trail_odd;
                 break;
             }
         }
         rc.carry_off = par;
-    } else if (p >= 0 && x0 >= 0 && s[p].last_tok >= 0) {
-        add_pairs_global<MODE>(k, s[p].last_tok, x0, 1);            // the boundary pair
+    } else if (p >= 0 && x0 >= 0 && P.last_tok >= 0) {
+        add_pairs_global<MODE>(k, P.last_tok, x0, 1);            // the boundary pair
     }
     carry[r] = rc;
     // the run that starts in this region and reaches its end
@@ -1680,13 +1706,15 @@ __global__ void k_runs(const RegionSum *__restrict__ s, int R, RegionCarry *__re
     if (x < 0) return;
     int64_t odd = me.uniform ? (me.n_live & 1) : me.trail_odd;
     int segs = 1;
-    for (int q = nx; q < R && s[q].first_tok == x;) {
+    for (int q = nx; q < R;) {
+        const RegionSum Q = q == nx ? N : s[q];
+        if (Q.first_tok != x) break;
         ++segs;
-        if (s[q].uniform) {
-            odd += s[q].n_live & 1;
+        if (Q.uniform) {
+            odd += Q.n_live & 1;
             q = next_nonempty(s, q + 1, R);
         } else {
-            odd += s[q].lead_len & 1;
+            odd += Q.lead_len & 1;
             break;
         }
     }
