@@ -1163,6 +1163,10 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             s.lead_len = s.n_live + f;
             s.in_lead = 0;
         }
+        // (MODE_TABLE: kept a scalar; as a select the compiler made it a vector value, read back
+        // with a readfirstlane in every chunk's fast-path test: C3 pass 0.7249 -> 0.7207 ms.  The
+        // maintained state's pass timed 4 % slower with it; profiles/r05_ab_in_lead.txt)
+        if (MODE == MODE_TABLE) s.in_lead = __builtin_amdgcn_readfirstlane(s.in_lead);
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
