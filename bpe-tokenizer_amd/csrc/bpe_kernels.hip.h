@@ -859,14 +859,15 @@ __device__ __forceinline__ unsigned long long member3(int32_t t, int32_t ma, int
 }
 
 // Wave-uniform facts of a freshly loaded chunk, from slot 255 (a live token, or the tail tag).
-__device__ __forceinline__ void finish_load(Chunk &c) {
-    c.first = bcast(c.t[0], 0);
+__device__ __forceinline__ void finish_load(Chunk &c, int32_t first) {
+    c.first = first;
     const int32_t l3 = bcast(c.t[3], 63);
     const int32_t v = LEN_TAG - l3;
     const int live = l3 >= SEP;
     c.len = live ? CHUNK : (v & 255);
     c.last = live ? l3 : (v >> 8) - 3;
 }
+__device__ __forceinline__ void finish_load(Chunk &c) { finish_load(c, bcast(c.t[0], 0)); }
 
 // Exact run-offset parity of every live slot (SEPs are runs of their own), and the run starts.
 // prev = the live token before slot 0 (NONE: none), prev_par = the parity of its offset.
@@ -1456,11 +1457,18 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 }
             }
         };
+        // pf (MODE_TABLE): slot 0 of the chunk the next stage takes up, read (a lane read, one
+        // VALU) by the stage before it for its merge test's right-hand neighbour, and handed on
+        // rather than read again when that chunk's own stage begins: C3 pass -0.2 %; the other
+        // modes read it again (the maintained state's pass timed 2.6 % slower with the hand-on;
+        // profiles/r05_ab_first_handon.txt)
+        int32_t pf = 0;
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
                          Defer &df) __attribute__((always_inline)) {
             load(fre, c + LEAD);
+            const int32_t f_next = bcast(nxt_slot.t[0], 0);
             if (c < nc) {
-                finish_load(cur);
+                finish_load(cur, MODE == MODE_TABLE ? pf : bcast(cur.t[0], 0));
             } else {
                 // past the region: an empty chunk hands the pending one on (every field stored on
                 // both sides, so the stores merge as values, not as a select of addresses)
@@ -1469,8 +1477,9 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 cur.last = NONE;
             }
             if (MERGE && cur.len)
-                apply_chunk<MERGE>(cur, live_from(c + 1, bcast(nxt_slot.t[0], 0)), ma, mb, mc, rs, c,
-                                   lane, ap);
+                apply_chunk<MERGE>(cur,
+                                   live_from(c + 1, MODE == MODE_TABLE ? f_next : bcast(nxt_slot.t[0], 0)),
+                                   ma, mb, mc, rs, c, lane, ap);
             if (cur.len) {
                 if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, df);
             } else {
@@ -1483,14 +1492,16 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             if (MODE == MODE_TABLE)
                 asm volatile("" ::"v"(prv.t[0]), "v"(prv.t[1]), "v"(prv.t[2]), "v"(prv.t[3]),
                              "s"(prv.last), "s"(prv.first), "s"(prv.len));
+            pf = f_next;
         };
         if (nc > 0) {
             Chunk S[RING];   // (constant indices only: the ring stays in registers)
             static_for<0, LEAD>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
             S[RING - 1].len = 0;
+            pf = bcast(S[0].t[0], 0);
             if (MERGE) {
                 // does the token before the region match the region's first live token?
-                const int32_t f = live_from(0, bcast(S[0].t[0], 0));
+                const int32_t f = live_from(0, pf);
                 // (integer arithmetic: a short-circuit && here makes the flag a vector value)
                 ap.match = (((uint32_t)(ap.prev ^ ma) | (uint32_t)(f ^ mb)) == 0u) &
                            ((MERGE == MERGE_XY) | (ap.par == 0));
