@@ -7,7 +7,8 @@ Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted o
 synthetic latin1 corpus (xorshift32 seed 12345, 256-char alphabet, 1 MiB samples; SURVEY.md
 §8(d)) per GPU, mergeUntil({min_weight: 2}) for 8000 merges: by default W = 5 untimed warmup
 merges, then the remaining K = 7995 merges of the config are timed (every pass, tie pass and
-exact pass of the run is inside the timed region).
+exact pass of the run is inside the timed region).  Before the warmup merges, ~100 ms of plain count
+passes over the resident corpus (no merge; --device-warmup-ms) bring the GPU to steady clocks.
 With N > 1 GPUs each rank holds its own contiguous 1 GiB shard of one corpus stream (weak
 scaling); the per-iteration pair-count exchange is an RCCL all-reduce enqueued on the engine's
 stream between the selection and apply kernels (the rank loop, bpe-tokenizer_amd/sharded.py).
@@ -259,6 +260,31 @@ def maintained_roofline(st, traffic):
     return out
 
 
+def device_warmup(trainer, ms):
+    """Plain count passes over the resident corpus (bpe_recount: no merge, the corpus and the merge
+    sequence are unchanged) for about `ms` ms before the W warmup merges.  A fresh box's first
+    passes run slower (clocks and caches coming up: profiles/r06_warm_probe.jsonl, the first ~10
+    launches 780-840 us against 755 us after), and the driver's W = 5 warmup merges are ~4 ms of
+    GPU work; so the timed window starts at steady state, as the full run's does.  Outside the
+    timed region; reported in the line (`device_warmup`)."""
+    import torch
+    if ms <= 0:
+        return None
+    eng = trainer.engine
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for _ in range(8):
+            eng.recount()
+        n += 8
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= ms:
+            break
+    return {'count_passes': n, 'seconds': time.perf_counter() - t0,
+            'what': 'plain count passes (bpe_recount) over the resident corpus before the warmup '
+                    'merges; no merge, corpus unchanged'}
+
+
 def fixture_check(args, merges):
     """The run's merge list against the threaded CPU restatement's run of the same workload
     (tests/golden/config3_cpu_mt_8000.json for C3, zipf_cpu_mt_2000.json for the skewed variant;
@@ -289,6 +315,9 @@ def main():
     ap.add_argument('--cpu-sample-mib', type=int, default=256)
     ap.add_argument('--cpu-budget-s', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--device-warmup-ms', type=float, default=100.0,
+                    help='plain count passes over the resident corpus (no merge) before the warmup '
+                         'merges, so that the timed window starts at steady clocks (0: none)')
     ap.add_argument('--incremental', action='store_true',
                     help='also run the incremental mode on the same workload, printed as a second '
                          'JSON line after the bench line')
@@ -326,6 +355,7 @@ def main():
                                                seed=12345, alphabet=args.alphabet, base=base,
                                                dist=dist, corpus=args.corpus)
 
+    heat = device_warmup(trainer, args.device_warmup_ms)
     if len(trainer.run(args.warmup, max_length=0, min_weight=2)) != args.warmup:
         raise SystemExit('corpus exhausted during warmup')
     trainer.engine.reset_stats()
@@ -421,12 +451,16 @@ def main():
                 np.asarray(trainer.merges, dtype=np.int64).tobytes()).hexdigest(),
             # (the merges of the whole run, warmup included, against the CPU restatement's run)
             'fixture_check': fixture_check(args, trainer.merges) if world == 1 else None,
+            'device_warmup': heat,
             'breakdown_ms_per_step': {
                 'stream_pass': k1_ms * st['step_launches'] / max(1, args.steps),
                 'select': st['select_ms'] / max(1e-9, timed_frac) / max(1, args.steps),
                 'tie_passes': st['tie_passes'],
                 'compactions': st['compactions'],
                 'exact_passes': st['exact_passes'], 'cold_rebuilds': st['cold_rebuilds'],
+                # (passes whose LDS adds return nothing: no counter can reach 16 bits, LoopCtl::
+                # unscreened in csrc/bpe_kernels.hip.h)
+                'unscreened_passes': st.get('unscreened_passes'),
             },
         }
         if cpu is not None:

@@ -55,8 +55,16 @@ TIE_WORDS = 32      # BPE_TIE_WORDS
 ENCODE_LDS_TOKENS = 16384   # BPE_ENCODE_LDS_TOKENS: longer texts are replayed by apply passes
 
 
+ERR_ARG, ERR_HIP, ERR_OOM, ERR_STATE, ERR_VOCAB = -1, -2, -3, -4, -5
+ERR_NOFIT = -6      # BPE_ERR_NOFIT: the position index does not fit beside the shard's corpus
+
+
 class BpeError(RuntimeError):
-    pass
+    """A libbpe call failed; `code` is its status (BPE_ERR_*, include/bpe.h)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class Stats(ctypes.Structure):
@@ -75,7 +83,7 @@ class Stats(ctypes.Structure):
         ('xchg_iters', ctypes.c_int64), ('pix_fallbacks', ctypes.c_int64),
         ('cold_rebuilds', ctypes.c_int64), ('incr_ms', ctypes.c_double),
         ('incr_timed', ctypes.c_int64), ('incr_launches', ctypes.c_int64),
-        ('incr_live', ctypes.c_int64),
+        ('incr_live', ctypes.c_int64), ('unscreened_passes', ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -202,7 +210,7 @@ def last_error():
 
 def _check(rc, what):
     if rc < 0:
-        raise BpeError('%s failed (%d): %s' % (what, rc, last_error()))
+        raise BpeError('%s failed (%d): %s' % (what, rc, last_error()), rc)
     return rc
 
 

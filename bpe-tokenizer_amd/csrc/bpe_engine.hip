@@ -192,6 +192,7 @@ struct bpe_ctx {
     // whose last merge's lanes are pending
     unsigned long long pix_w_last = 0;
     uint32_t pix_lane[3] = {0, 0, 0}, pix_lane_prev[3] = {0, 0, 0};
+    int64_t pix_nw_last = 0;   // words the last rank-loop batch all-reduced (its pending merge's)
     bool pix_first_pending = false;
 };
 
@@ -404,50 +405,42 @@ int cold_rebuild(bpe_ctx *c, uint64_t min_cap) {
     HIP_TRY(hipStreamSynchronize(s));
     if (flags[1]) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
     const uint64_t n = std::min<uint64_t>(flags[0], c->cold_cap);
-    uint32_t *keys = nullptr, *d_m = nullptr;
-    unsigned long long *counts = nullptr;
+    // (the temporary lists are freed on every way out, HIP_TRY's early returns included)
+    struct Scratch {
+        hipStream_t s;
+        uint32_t *keys = nullptr, *d_m = nullptr;
+        unsigned long long *counts = nullptr;
+        ~Scratch() {
+            (void)hipStreamSynchronize(s);
+            dfree(keys);
+            dfree(counts);
+            dfree(d_m);
+        }
+    } t{s};
     int rc;
-    auto release = [&]() {
-        (void)hipStreamSynchronize(s);
-        dfree(keys);
-        dfree(counts);
-        dfree(d_m);
-    };
-    if ((rc = dev_alloc(&keys, std::max<uint64_t>(n, 1))) || (rc = dev_alloc(&counts, std::max<uint64_t>(n, 1))) ||
-        (rc = dev_alloc(&d_m, 1))) {
-        release();
+    if ((rc = dev_alloc(&t.keys, std::max<uint64_t>(n, 1))) ||
+        (rc = dev_alloc(&t.counts, std::max<uint64_t>(n, 1))) || (rc = dev_alloc(&t.d_m, 1)))
         return rc;
-    }
-    HIP_TRY(hipMemsetAsync(d_m, 0, sizeof(uint32_t), s));
-    k_cold_gather<<<COLD_GRID, 256, 0, s>>>(c->cold, keys, counts, d_m);
+    HIP_TRY(hipMemsetAsync(t.d_m, 0, sizeof(uint32_t), s));
+    k_cold_gather<<<COLD_GRID, 256, 0, s>>>(c->cold, t.keys, t.counts, t.d_m);
     HIP_TRY(hipGetLastError());
     uint32_t m = 0;
-    HIP_TRY(hipMemcpyAsync(&m, d_m, sizeof m, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&m, t.d_m, sizeof m, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // (a table that grows is reallocated empty, which drops the maintained state: restored once
     // the live claims are back)
     const bool counts_valid = c->counts_valid, cold_exact = c->cold_exact;
     for (int attempt = 0;; ++attempt) {
-        if ((rc = ensure_cold(c, 0, std::max<uint64_t>(min_cap, 4 * (uint64_t)m + 4096)))) {
-            release();
-            return rc;
-        }
-        if ((rc = cold_clear(c))) {
-            release();
-            return rc;
-        }
-        if (m) k_load_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, keys, counts, m);
+        if ((rc = ensure_cold(c, 0, std::max<uint64_t>(min_cap, 4 * (uint64_t)m + 4096)))) return rc;
+        if ((rc = cold_clear(c))) return rc;
+        if (m) k_load_cold<<<COLD_GRID, 256, 0, s>>>(c->cold, t.keys, t.counts, m);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(flags, c->d_cold_flags, sizeof flags, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (!flags[1]) break;
-        if (attempt == 2) {
-            release();
-            return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
-        }
+        if (attempt == 2) return fail(BPE_ERR_STATE, "bpe native: cold pair table overflow");
         min_cap = 2 * c->cold_cap;
     }
-    release();
     c->cold_used = flags[0];
     c->counts_valid = counts_valid;
     c->cold_exact = cold_exact;
@@ -1201,6 +1194,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
     }
     if (c->stats_on) {
         c->stats.tie_passes += h->n_tie;
+        c->stats.unscreened_passes += h->n_unscreened;
         c->stats.tie_tail += h->n_tail;
         c->stats.tie_lone += h->n_lone;
         c->stats.loop_host += h->n_host;
@@ -1515,6 +1509,7 @@ int rank_loop_end(bpe_ctx *c, int64_t *out, int64_t cap, int64_t *n_done, int *s
     c->len16_lo = base + nd;
     if (c->stats_on) {
         c->stats.tie_passes += h->n_tie;
+        c->stats.unscreened_passes += h->n_unscreened;
         c->stats.tie_tail += h->n_tail;
         c->stats.tie_lone += h->n_lone;
         c->stats.loop_host += h->n_host;
@@ -2226,7 +2221,7 @@ int pix_set_global(bpe_ctx *c, const unsigned long long *table, const uint32_t *
             (void)hipStreamSynchronize(c->stream);
             pix_free(c);
         }
-        return fail(BPE_ERR_STATE, "bpe native: the position index does not fit this shard "
+        return fail(BPE_ERR_NOFIT, "bpe native: the position index does not fit this shard "
                                    "(use the streaming mode)");
     }
     if (rc) return rc;
@@ -2367,11 +2362,12 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
     // (the last batch's pending merge keeps its own layout for its decode, and its words)
     c->pix_first_pending = c->rl_delta_pending;
     for (int i = 0; i < 3; ++i) c->pix_lane_prev[i] = c->pix_lane[i];
-    const int64_t prev_words = c->rl_delta_pending && c->pix_lane_prev[0] ? 2 * (int64_t)c->pix_lane_prev[2]
-                                                                          : 0;
+    // (a pending merge's rows span the words of its own batch's layout, lanes or dense rows: this
+    // batch all-reduces at least those, whatever layout it takes itself)
+    const int64_t prev_words = c->rl_delta_pending ? c->pix_nw_last : 0;
     if (dense) {
         P->T.lane_w = P->T.lane_q = P->T.lane_base = 0;
-        nw = XCHG_HDR + DELTA_ROWS * ids;
+        nw = std::max<int64_t>(XCHG_HDR + DELTA_ROWS * ids, prev_words);
     } else {
         uint32_t w = c->pix_w_last ? 64u - (uint32_t)__builtin_clzll(c->pix_w_last) : 64u;
         // (BPE_XCHG_LANE_BITS=n, tests: lanes of at most n bits after a known count, so that
@@ -2382,8 +2378,9 @@ int pix_rank_begin(bpe_ctx *c, int64_t max_length, int64_t min_weight, unsigned 
         P->T.lane_w = w;
         P->T.lane_q = q;
         P->T.lane_base = (uint32_t)((ids + q - 1) / q);
-        nw = XCHG_HDR + PIX_XCHG_SPECIAL + std::max<int64_t>(2 * (int64_t)P->T.lane_base, prev_words);
+        nw = std::max<int64_t>(XCHG_HDR + PIX_XCHG_SPECIAL + 2 * (int64_t)P->T.lane_base, prev_words);
     }
+    c->pix_nw_last = nw;
     c->pix_lane[0] = P->T.lane_w;
     c->pix_lane[1] = P->T.lane_q;
     c->pix_lane[2] = P->T.lane_base;

@@ -162,6 +162,9 @@ struct Result {
     unsigned long long replaced;         // apply: replacement count
     unsigned long long cold_flags;       // k_argmax_cold: (overflow << 32) | n_used of the cold table
     unsigned long long cold_dead;        // k_argmax_cold: claims whose pair is gone (count 0, key set)
+    // k_reduce_table: the largest bin of the table it wrote, plus one (0: unknown); consumed and
+    // cleared by the next decision (LoopCtl::unscreened)
+    unsigned long long bin_max;
 };
 
 // Device-resident mergeUntil loop (core.ts:367-384): the decision of each iteration stays in HBM and
@@ -201,6 +204,16 @@ struct LoopCtl {
     int32_t err;
     // (err 1: the count found and the W expected)
     unsigned long long err_got, err_want;
+    // The pass applying this merge cannot take any LDS counter of any workgroup to 16 bits, so it
+    // counts with adds that return nothing and no overflow screen (k_step_loop<MODE_TABLE>).  Set
+    // by the decision when (largest bin of the pre-merge table) + 2 W < 2^16: a pair's count never
+    // grows by a merge (a b -> c only removes occurrences of pairs next to a or b, and runs of X
+    // only shrink), the new pairs (x, c) and (c, y) number W each at most, and a workgroup's LDS
+    // count of a bin is at most the bin's count over the whole corpus (pairs across regions go
+    // to the spill; a run's segments count at most the run's floor(L / 2)).  0 (screened) for a
+    // sharded rank, the maintained state and the first pass of a batch.
+    int32_t unscreened;
+    int32_t n_unscreened;   // decisions that set it, in this batch
 };
 
 // Merge log entry of the device loop: (a, b, W, this corpus's replacement count).
@@ -595,7 +608,7 @@ __device__ __forceinline__ void incr_add(const Sink &k, int32_t x, int32_t y, ui
 // One counted occurrence of (x, y) (outside the streaming fast paths).
 // (MODE_TABLE / MODE_FUSED: the dword the add found is ORed into `seen`, the wave's overflow
 // screen; see lds_sweep)
-template <int MODE>
+template <int MODE, bool SCREEN = true>
 __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y, uint32_t &seen) {
     if (MODE == MODE_NONE) return;
     if (MODE == MODE_INCR) {
@@ -606,7 +619,9 @@ __device__ __forceinline__ void count_pair(const Sink &k, int32_t x, int32_t y, 
         const bool hot = ((uint32_t)x | (uint32_t)y) < (uint32_t)HOT;
         const uint32_t addr = hot ? hot_addr(x, y) : cold_addr(sketch_hash(x, y));
         // (MODE_FUSED keeps no sketch: its cold pairs go to the maintained table only)
-        if (MODE == MODE_TABLE || hot) {
+        if (MODE == MODE_TABLE && !SCREEN) {
+            atomicAdd(lds_word(k, addr), hot_inc(x));
+        } else if (MODE == MODE_TABLE || hot) {
             // (consumed at once: a `seen` still in flight would make every later join wait for
             // all of the wave's LDS adds, the fast path's deferred ones included)
             uint32_t old = atomicAdd(lds_word(k, addr), hot_inc(x));
@@ -958,15 +973,21 @@ struct Defer {
 // The LDS adds of a fast-path chunk; their returned words and
 // addresses go to df, screened at the end of the
 // ring round (Returns), so no wave waits on its LDS atomics' return before then.
-template <bool FUSED = false>
+// SCREEN false (MODE_TABLE, when no LDS counter can reach 16 bits in this pass: see LoopCtl::
+// unscreened): the adds return nothing, and no word is kept for a screen.
+template <bool FUSED = false, bool SCREEN = true>
 __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (&y)[4],
                                           const Sink &k, Defer &df) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t addr, inc;
         pair_slot<FUSED>(k, x[e], y[e], addr, inc);
-        df.o[e] = atomicAdd(lds_word(k, addr), inc);
-        df.a[e] = addr;
+        if (SCREEN) {
+            df.o[e] = atomicAdd(lds_word(k, addr), inc);
+            df.a[e] = addr;
+        } else {
+            atomicAdd(lds_word(k, addr), inc);   // (ds_add_u32: no return to wait for)
+        }
     }
 }
 
@@ -1010,7 +1031,7 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
 // in the next region, and the fast path does not work that parity out.
 // Fast-path counts of MODE_TABLE / MODE_FUSED leave the words their adds returned in `df`, and the
 // other paths OR theirs into s.seen: the overflow screen of the ring round (screen_round).
-template <int MODE, bool TAIL = false>
+template <int MODE, bool TAIL = false, bool SCREEN = true>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
                                             const Sink &k, Defer &df) {
     const int len = w.len;
@@ -1062,7 +1083,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             // one form for every chunk: 11 VALU per pair, both classes (a separate 5-VALU form
             // for chunks of hot tokens only paid off only on a fresh corpus; telling the two
             // apart cost more over a whole run: dropping it timed the C3 run 3 % faster)
-            add_pairs<MODE == MODE_FUSED>(x, y, k, df);
+            add_pairs<MODE == MODE_FUSED, SCREEN>(x, y, k, df);
             if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
@@ -1171,7 +1192,7 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-        if (cnt[e]) count_pair<MODE>(k, w.t[e], rr[e], s.seen);
+        if (cnt[e]) count_pair<MODE, SCREEN>(k, w.t[e], rr[e], s.seen);
     s.first_tok = s.n_live ? s.first_tok : w.first;
     s.prev = w.last;
     s.par = par_last;
@@ -1309,7 +1330,7 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
 
 // hist: the kernel's static LDS table (so, once inlined, LDS addresses are plain constants with no
 // symbol base to add per access)
-template <int MERGE, int MODE>
+template <int MERGE, int MODE, bool SCREEN = true>
 __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ ids,
                                           int64_t n_chunks, int64_t cpr, int R,
                                           const RegionCarry *__restrict__ carry, int32_t ma,
@@ -1430,6 +1451,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         // took 4 ms instead of 0.6.)
         auto screen_round = [&]() __attribute__((always_inline)) {
             if (MODE != MODE_TABLE && MODE != MODE_FUSED && MODE != MODE_INCR) return;
+            if (!SCREEN) return;
             const bool whole = __ballot((s.seen & SWEEP_BITS) != 0u) != 0ull;
             s.seen = 0;
             uint32_t acc = 0;
@@ -1481,7 +1503,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                                    live_from(c + 1, MODE == MODE_TABLE ? f_next : bcast(nxt_slot.t[0], 0)),
                                    ma, mb, mc, rs, c, lane, ap);
             if (cur.len) {
-                if (prv.len) count_chunk<MODE>(prv, cur.first, lane, s, k, df);
+                if (prv.len) count_chunk<MODE, false, SCREEN>(prv, cur.first, lane, s, k, df);
             } else {
                 cur = prv;   // rare: hand the pending chunk on
             }
@@ -1517,7 +1539,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 screen_round();
             }
             Defer dt;   // (the region's last chunk takes the exact path: s.seen)
-            if (S[RING - 1].len) count_chunk<MODE, true>(S[RING - 1], NONE, lane, s, k, dt);
+            if (S[RING - 1].len) count_chunk<MODE, true, SCREEN>(S[RING - 1], NONE, lane, s, k, dt);
             screen_round();
         }
         if (lane == 0) {
@@ -1611,6 +1633,9 @@ k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     if (ma == mb)
         step_body<MERGE_XX, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
                                   ct, nullptr, sums, replaced, hot_g, delta);
+    else if (MODE == MODE_TABLE && ctl->unscreened)
+        step_body<MERGE_XY, MODE, false>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
+                                         spill, ct, nullptr, sums, replaced, hot_g, delta);
     else
         step_body<MERGE_XY, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
                                   ct, nullptr, sums, replaced, hot_g, delta);
@@ -1811,12 +1836,22 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         k = pack_key(v, bin_a(bin), bin_b(bin));
     // one atomic per workgroup (a wave each would queue over a thousand on one address)
     k = wave_max_u64(k);
-    __shared__ unsigned long long s_best[4];
-    if ((t & 63) == 0) s_best[t >> 6] = k;
+    // (and the largest bin of all, hot and sketch alike: the next decision's bound, LoopCtl::
+    // unscreened)
+    unsigned long long vm = wave_max_u64(v);
+    __shared__ unsigned long long s_best[4], s_vmax[4];
+    if ((t & 63) == 0) {
+        s_best[t >> 6] = k;
+        s_vmax[t >> 6] = vm;
+    }
     __syncthreads();
     if (t == 0 && res) {
-        for (int w = 1; w < 4; ++w) k = s_best[w] > k ? s_best[w] : k;
+        for (int w = 1; w < 4; ++w) {
+            k = s_best[w] > k ? s_best[w] : k;
+            vm = s_vmax[w] > vm ? s_vmax[w] : vm;
+        }
         if (k) atomicMax(&res->best, k);
+        atomicMax(&res->bin_max, vm + 1);
     }
 }
 
@@ -2389,6 +2424,12 @@ __device__ void decide_commit(LoopCtl *ctl, Result *res, const LoopCtl &C, long 
     ctl->w = W;
     ctl->next_id = c + 1;
     ctl->n_done = i + 1;
+    const unsigned long long bm = res->bin_max;
+    const int32_t uns = !C.sharded && !C.maintained && bm &&
+                        (bm - 1) + 2 * (unsigned long long)W < 0x10000ull;
+    ctl->unscreened = uns;
+    ctl->n_unscreened = C.n_unscreened + uns;
+    res->bin_max = 0;
     res->best = 0;
     res->n_cand = 0;
     res->n_heavy = 0;

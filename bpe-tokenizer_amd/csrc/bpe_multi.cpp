@@ -81,6 +81,9 @@ struct bpe_multi {
     int64_t pix_entries = 0, pix_merged = 0, pix_fallbacks = 0;
     // the streaming mode went on in the incremental mode past AUTO_PIX_VOCAB token ids (round 5)
     bool pix_auto = false;
+    // the caller chose a mode (bpe_set_mode): the automatic switch to the incremental mode past
+    // AUTO_PIX_VOCAB ids then leaves it alone
+    bool mode_explicit = false;
     std::vector<ncclComm_t> comms;
     Rccl rccl;
     // shards sharing one device (the one-GPU test box, BPE_REDUCE_HOST): the exchange is a device
@@ -439,8 +442,9 @@ int multi_shard_count(bpe_multi *m, int *n) {
     return BPE_OK;
 }
 
-int multi_set_mode(bpe_multi *m, int mode) {
+int multi_set_mode(bpe_multi *m, int mode, bool explicit_choice) {
     for (auto s : m->sh) MTRY(bpe_set_mode(s, mode));
+    if (explicit_choice) m->mode_explicit = true;
     m->pix = mode == BPE_MODE_INCREMENTAL;
     m->pix_auto = false;
     m->pix_off = false;
@@ -891,13 +895,14 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
         // maxima fall back to full scans past 2^16 blocks), whose number grows with the vocabulary
         // (8 shards of 512 MiB: 1.0 ms/merge at 4k merges, 5.1 ms/merge at 32k; profiles/
         // r05_kernel_stats_multi8_32k_stream.csv).  So the shards go on in the incremental mode,
-        // whose merges and counts are the same.  BPE_STREAM_ONLY=1 keeps the stream.
+        // whose merges and counts are the same.  A mode the caller set
+        // (bpe_set_mode) is kept; BPE_STREAM_ONLY=1 keeps the stream for every context.
         static const bool stream_only = getenv("BPE_STREAM_ONLY") != nullptr;
         // (BPE_AUTO_PIX_VOCAB=n, tests: switch at n token ids; read per batch)
         const char *av = getenv("BPE_AUTO_PIX_VOCAB");
         const int32_t auto_vocab = av ? (int32_t)atoi(av) : AUTO_PIX_VOCAB;
-        if (!m->pix && !stream_only && nt >= auto_vocab) {
-            MTRY(multi_set_mode(m, BPE_MODE_INCREMENTAL));
+        if (!m->pix && !m->mode_explicit && !stream_only && nt >= auto_vocab) {
+            MTRY(multi_set_mode(m, BPE_MODE_INCREMENTAL, false));
             m->pix_auto = true;
         }
         int64_t want = std::min<int64_t>(batch, BPE_MAX_VOCAB - (int64_t)nt);
@@ -917,9 +922,10 @@ int multi_merge_until(bpe_multi *m, int64_t max_length, int64_t min_weight,
                     for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
                 }
                 int erc = enter_maintained(m);
-                if (erc != BPE_OK && pix && m->pix_auto) {
+                if (erc == BPE_ERR_NOFIT && pix && m->pix_auto) {
                     // (the automatic switch: the shards' indexes do not fit beside their corpora,
-                    // e.g. 2 GiB shards sharing one device; the stream goes on)
+                    // e.g. 2 GiB shards sharing one device; the stream goes on.  Only on that code:
+                    // any other error, a HIP fault or a table overflow, is the caller's)
                     m->pix_off = true;
                     ++m->pix_fallbacks;
                     for (auto s : m->sh) MTRY(bpe_set_mode(s, BPE_MODE_STREAM));
@@ -1030,6 +1036,7 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out) {
         acc.incr_timed = std::max(acc.incr_timed, x.incr_timed);
         acc.incr_launches += x.incr_launches;
         acc.incr_live += x.incr_live;
+        acc.unscreened_passes += x.unscreened_passes;
         acc.xchg_iters = std::max(acc.xchg_iters, x.xchg_iters);
     }
     acc.pix_fallbacks = m->pix_fallbacks;

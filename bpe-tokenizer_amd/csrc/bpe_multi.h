@@ -35,7 +35,8 @@ int multi_get_stats(bpe_multi *m, bpe_stats *out);
 int multi_reset_stats(bpe_multi *m);
 int multi_get_stream(bpe_multi *m, void **stream);
 int multi_shard_count(bpe_multi *m, int *n);
-int multi_set_mode(bpe_multi *m, int mode);
+// explicit_choice: the caller's bpe_set_mode (false: the automatic switch past AUTO_PIX_VOCAB ids)
+int multi_set_mode(bpe_multi *m, int mode, bool explicit_choice = true);
 
 // shards that share one device exchange through a device kernel (bpe_engine.hip)
 constexpr int BPE_MAX_SHARDS_ONE_DEVICE = 16;

@@ -86,11 +86,17 @@ function encodeIdsOnDevice(owner, list, tripleOf, ids) {
 }
 
 /**
- * encodeIdsOnDevice when the cost model sends the call to the device and the device can take it,
- * else null (the caller then runs the reference's replay).  A device failure is cached on the owner
- * (non-enumerable `_enc_failed`): `true` when the encoder itself cannot be made, the list when its
- * merges cannot be loaded.
+ * encodeIdsMaybeOnDevice when the cost model sends the call to the device and the device can take it,
+ * else null (the caller then runs the reference's replay).  Only what the device cannot do is
+ * remembered on the owner (non-enumerable `_enc_failed`): `true` when the encoder itself cannot be
+ * made (no addon, no HIP device), the list when one of its merges has a token id the encoder does not
+ * hold (the list keeps that merge: fromJSON replaces the list).  A text with such an id replays alone.
+ * Any other failure (a device fault, out of memory) is reported once as a process warning and not
+ * remembered: that call replays, and the next one tries the device again with its encoder rebuilt.
  */
+const CAPABILITY_LIST = /merge token id out of range|more merges than token ids/
+const CAPABILITY_TEXT = /token id out of range in text/
+let warned = false
 function encodeIdsMaybeOnDevice(owner, list, tripleOf, ids) {
   if (!encodeOnDevice(ids.length, list.length)) return null
   if (ENCODE_DEVICE !== '1' && (owner._enc_failed === true || owner._enc_failed === list))
@@ -101,7 +107,18 @@ function encodeIdsMaybeOnDevice(owner, list, tripleOf, ids) {
     if (ENCODE_DEVICE === '1') throw e
     if (!Object.prototype.hasOwnProperty.call(owner, '_enc_failed'))
       Object.defineProperty(owner, '_enc_failed', { value: null, writable: true, enumerable: false })
-    owner._enc_failed = owner._encoder ? list : true
+    let msg = String((e && e.message) || e)
+    if (!owner._encoder) {
+      owner._enc_failed = true
+    } else {
+      // (the encoder may hold part of the list: the next call loads it again from the start)
+      owner._enc_list = null
+      if (CAPABILITY_LIST.test(msg)) owner._enc_failed = list
+      else if (!CAPABILITY_TEXT.test(msg) && !warned) {
+        warned = true
+        process.emitWarning('bpe device encoder failed, this call replays the merges in JS: ' + msg)
+      }
+    }
     return null
   }
 }

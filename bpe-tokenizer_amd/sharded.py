@@ -221,13 +221,20 @@ class ShardedTrainer:
         # the stream went on)
         self._pix_auto = False
         self.pix_fallbacks = 0
+        # the caller chose a mode (set_mode): the automatic switch past AUTO_PIX_VOCAB ids leaves it
+        self._mode_explicit = False
         # RCCL backend: the rank loop's two all-reduces per iteration are issued from C++ on the
         # engine's stream (bpe_rank_loop_rccl, one call per batch); BPE_RANK_LOOP=python keeps them
         # as torch.distributed calls (A/B)
         self._native = None
 
     def set_mode(self, mode):
-        """'stream' or 'incremental' (bpe_set_mode) for this rank's engine; every rank alike."""
+        """'stream' or 'incremental' (bpe_set_mode) for this rank's engine; every rank alike.
+        The choice is kept: no automatic switch to the incremental mode follows."""
+        self._set_mode(mode)
+        self._mode_explicit = True
+
+    def _set_mode(self, mode):
         self.engine.set_mode(mode)
         self.pix = mode == 'incremental'
         self._pix_off = False
@@ -362,8 +369,10 @@ class ShardedTrainer:
             eng.set_global_counts(table.data_ptr(), all_k.data_ptr() if total else None,
                                   all_c.data_ptr() if total else None, total)
             ok = 1
-        except pkg.BpeError:
-            if not (pix and self._pix_auto):
+        except pkg.BpeError as e:
+            # (only "the index does not fit" (BPE_ERR_NOFIT) after the automatic switch: any
+            # other error, a HIP fault or a table overflow, is the caller's)
+            if not (pix and self._pix_auto and e.code == pkg.ERR_NOFIT):
                 raise
             ok = 0      # (this rank's index does not fit beside its corpus)
         if pix and self._pix_auto:
@@ -414,10 +423,12 @@ class ShardedTrainer:
             k = min(batch, n - len(ms))
             # (as bpe_multi.cpp: past AUTO_PIX_VOCAB token ids the streaming mode's maintained state
             # outgrows its LDS rows and its scans of the claimed cold pairs; the ranks go on in the
-            # incremental mode, same merges.  BPE_STREAM_ONLY=1 keeps the stream)
-            if (not self.pix and self.n_tokens >= int(os.environ.get('BPE_AUTO_PIX_VOCAB', AUTO_PIX_VOCAB))
+            # incremental mode, same merges.  A mode the caller set is kept; BPE_STREAM_ONLY=1
+            # keeps the stream)
+            if (not self.pix and not self._mode_explicit
+                    and self.n_tokens >= int(os.environ.get('BPE_AUTO_PIX_VOCAB', AUTO_PIX_VOCAB))
                     and not os.environ.get('BPE_STREAM_ONLY')):
-                self.set_mode('incremental')
+                self._set_mode('incremental')
                 self._pix_auto = True
             pix = self.pix and not self._pix_off
             if not self._maintained and (self._heavy_streak >= 2 or pix):

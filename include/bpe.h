@@ -36,6 +36,10 @@ extern "C" {
 #define BPE_ERR_OOM (-3)
 #define BPE_ERR_STATE (-4)
 #define BPE_ERR_VOCAB (-5)
+/* The incremental mode's position index does not fit beside this shard's corpus in device memory
+ * (bpe_set_global_counts on a shard in BPE_MODE_INCREMENTAL).  Nothing was changed: the streaming
+ * mode, which needs no index, can go on.  Drivers fall back to it on this code only. */
+#define BPE_ERR_NOFIT (-6)
 
 #define BPE_MAX_VOCAB 55296
 
@@ -318,6 +322,9 @@ typedef struct {
     int64_t incr_timed;       /* ... their number, */
     int64_t incr_launches;    /* ... all such passes, */
     int64_t incr_live;        /* ... and the live corpus tokens summed over them (pair-scans) */
+    int64_t unscreened_passes;/* device loop, table state: merge passes whose LDS adds return nothing
+                                 and skip the overflow screen (no counter can reach 16 bits: the
+                                 largest table bin + 2 W < 2^16) */
 } bpe_stats;
 
 int bpe_stats_enable(bpe_ctx *ctx, int on);

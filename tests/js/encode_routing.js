@@ -87,4 +87,36 @@ t2.fromJSON(j1)
 const s = text(40)
 assert.strictEqual(t2.encodeToCode(s), replay(j1, s))
 if (mode !== 'host') assert.notStrictEqual(t2._enc_failed, t2.merge_tokens)
-console.log('encode_routing ok', mode)
+// 3) a failure that is not a capability (here: an owner whose encoder handle is broken, so the
+// addon rejects it) replays that call, is reported once as a process warning and is NOT
+// remembered: the next call tries the device again with its encoder rebuilt from the start
+{
+  const native = require(path.join(__dirname, '..', '..', 'bpe-tokenizer_amd', 'js', 'native.js'))
+  let warnings = []
+  process.on('warning', w => warnings.push(w.message))
+  const owner = {}
+  Object.defineProperty(owner, '_encoder', { value: { not: 'a handle' }, writable: true, enumerable: false })
+  Object.defineProperty(owner, '_enc_list', { value: null, writable: true, enumerable: false })
+  // (2000 merges, 16 chars: the cost model sends the call to the device)
+  const list = Array.from({ length: 2000 }, (_, k) => [k % 10, (k + 1) % 10, 10 + k])
+  const ids = Array.from({ length: 16 }, (_, i) => i % 10)
+  let threw = false
+  try {
+    native.loadNative()
+  } catch (e) {
+    threw = true   // (no addon: nothing to test here)
+  }
+  if (!threw) {
+    const prev = process.env.BPE_ENCODE_DEVICE
+    assert.strictEqual(native.encodeIdsMaybeOnDevice(owner, list, t => t, ids), null, 'replayed')
+    assert.ok(owner._enc_failed !== list && owner._enc_failed !== true, 'not remembered')
+    assert.strictEqual(owner._enc_list, null, 'encoder reloaded on the next call')
+    assert.strictEqual(prev, process.env.BPE_ENCODE_DEVICE)
+    setImmediate(() => {
+      assert.strictEqual(warnings.length, 1, 'reported once: ' + JSON.stringify(warnings))
+      console.log('encode_routing ok', mode)
+    })
+  } else {
+    console.log('encode_routing ok', mode)
+  }
+}

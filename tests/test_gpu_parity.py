@@ -292,6 +292,34 @@ def test_lds_counters_past_16_bits(mode):
 
 
 @pytest.mark.parametrize('mode', MODES)
+def test_unscreened_passes_from_the_counts_bound(mode):
+    """The device loop's passes without the LDS overflow screen (LoopCtl::unscreened: adds that
+    return nothing), taken only while (largest table bin) + 2 W < 2^16.  'ab' x 2^19 makes a chain
+    of X X merges whose W halves from 2^19 (screened passes: a workgroup's counters pass 16 bits),
+    then a random text's merges (counts ~2 K: unscreened), so one batch switches mid-way; a long
+    run of one token (the exact path's adds) rides along.  100 base ids, so the merged tokens stay
+    hot (a cold X X chain would send the loop to the maintained state).  Merges and corpus equal
+    the oracle's."""
+    rng = np.random.default_rng(7)
+    samples = [np.tile(np.array([0, 1], np.int32), 1 << 19),
+               rng.integers(2, 42, size=3 << 20).astype(np.int32),
+               np.full(70000, 42, np.int32)]
+    ids, off = _flat(samples)
+    len16 = [1] * 100
+    st = OracleState(ids, off, len16, 100, extra=256)
+    want = st.merge_until(0, 2, 90)
+    e, got = run_engine(samples, len16, {'max_iterations': 90}, mode=mode, stats=True)
+    assert got == want
+    assert [m[2] for m in got[:3]] == [1 << 19, 1 << 18, 1 << 17]
+    assert e.samples() == st.samples()
+    if mode == 'loop':
+        s = e.stats()
+        # (the chain's first passes screened: W + 2 W passes 2^16 until W = 2^14)
+        assert 0 < s['unscreened_passes'] <= 90 - 4, s
+    e.close()
+
+
+@pytest.mark.parametrize('mode', MODES)
 def test_compaction_under_heavy_merging(mode):
     """'ab' * 1.5M: the first merge halves the corpus, which triggers the dead-slot compaction."""
     n = 3_000_000

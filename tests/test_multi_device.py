@@ -366,7 +366,8 @@ def test_automatic_switch_to_the_incremental_mode_and_its_fallback(monkeypatch):
     """The streaming mode's switch to the incremental mode past a vocabulary size (18432 ids;
     BPE_AUTO_PIX_VOCAB=600 here), and its fall-back to the stream when the shards' indexes do not
     fit (BPE_PIX_FORCE_OOM=1: every index build fails as out of device memory): the same merges
-    and corpus as one context either way."""
+    and corpus as one context either way.  A mode the caller set (set_mode('stream')) is kept:
+    no switch."""
     data = pkg.synth_latin1(16 << 20, seed=4243, A=96, base=32)
     one = pkg.Engine(0)
     one.add_latin1(data, sample_bytes=1 << 20)
@@ -374,19 +375,23 @@ def test_automatic_switch_to_the_incremental_mode_and_its_fallback(monkeypatch):
     ids1, _ = one.read_corpus()
     one.close()
     monkeypatch.setenv('BPE_AUTO_PIX_VOCAB', '600')
-    for oom in (False, True):
-        if oom:
+    for leg in ('auto', 'oom', 'explicit'):
+        if leg == 'oom':
             monkeypatch.setenv('BPE_PIX_FORCE_OOM', '1')
         multi = pkg.Engine(devices=[0] * 4, reduce='host')
         multi.add_latin1(data, sample_bytes=1 << 20)
+        if leg == 'explicit':
+            multi.set_mode('stream')
         multi.stats_enable(True)
         got = multi.merge_until(0, 2, 1200)
         st = multi.stats()
-        assert got == want, oom
+        assert got == want, leg
         ids, _ = multi.read_corpus()
-        assert np.array_equal(ids, ids1), oom
-        if oom:
+        assert np.array_equal(ids, ids1), leg
+        if leg == 'oom':
             assert st['pix_fallbacks'] >= 1 and st['pix_merges'] == 0, st
+        elif leg == 'explicit':
+            assert st['pix_fallbacks'] == 0 and st['pix_merges'] == 0, st
         else:
             assert st['pix_fallbacks'] == 0 and st['pix_merges'] >= 4 * 500, st
         multi.close()

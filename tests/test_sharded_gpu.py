@@ -36,8 +36,8 @@ def worker(rank, world, port, q, mode='step', n=60, max_length=0, seed=777, A=40
                                               corpus=corpus, rank_loop=True)
         assert tr.exchange and dist.get_backend() == backend
         native = rank_loop == 'native' and backend == 'nccl'
-        if engine_mode != 'stream':
-            tr.set_mode(engine_mode)
+        if engine_mode != 'stream':   # ('stream_explicit': the stream, chosen by the caller)
+            tr.set_mode('stream' if engine_mode == 'stream_explicit' else engine_mode)
         tr.engine.stats_enable(True)
         if mode == 'step':
             for _ in range(n):
@@ -184,10 +184,14 @@ def test_incremental_rank_loop_automatic_switch_and_fallback():
     """The streaming rank loop's switch to the incremental mode past a vocabulary size (18432
     ids; BPE_AUTO_PIX_VOCAB=400 here), and, when an index build fails on some rank
     (BPE_PIX_FORCE_OOM=1, as out of device memory), every rank's agreed fall-back to the stream:
-    the same merges and corpus as one context either way."""
+    the same merges and corpus as one context either way.  A mode the caller set
+    (set_mode('stream')) is kept: no switch."""
     st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=2,
                env={'BPE_AUTO_PIX_VOCAB': '400'})
     assert all(s['pix_merges'] >= 100 and s['trainer_pix_fallbacks'] == 0 for s in st), st
     st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=2,
                env={'BPE_AUTO_PIX_VOCAB': '400', 'BPE_PIX_FORCE_OOM': '1'})
     assert all(s['pix_merges'] == 0 and s['trainer_pix_fallbacks'] >= 1 for s in st), st
+    st = check(2, mode='loop', n=300, seed=12345, A=256, base=0, mib=2,
+               env={'BPE_AUTO_PIX_VOCAB': '400'}, engine_mode='stream_explicit')
+    assert all(s['pix_merges'] == 0 and s['trainer_pix_fallbacks'] == 0 for s in st), st
