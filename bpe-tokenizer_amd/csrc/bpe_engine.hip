@@ -593,7 +593,7 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         else
             k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(
                 c->d_sums, c->R, c->d_carry, c->d_spill, c->cold, c->d_heavy, nullptr);
-        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, REDUCE_THREADS, 0, s>>>(
             c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, c->opt_max_length, c->d_res,
             nullptr);
     }
@@ -1129,7 +1129,7 @@ int loop_batch(bpe_ctx *c, int64_t max_length, int64_t min_weight, int64_t n, in
                 k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
                                                                       c->d_spill, c->cold,
                                                                       c->d_heavy, c->d_ctl);
-            k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+            k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, REDUCE_THREADS, 0, s>>>(
                 c->d_partials, c->G, c->d_spill, c->d_hot, c->d_len16, max_length, c->d_res,
                 c->d_ctl);
         }
@@ -1420,7 +1420,7 @@ int rank_loop_count(bpe_ctx *c) {
         k_runs<MODE_TABLE><<<(c->R + 255) / 256, 256, 0, s>>>(c->d_sums, c->R, c->d_carry,
                                                               c->d_spill, c->cold, c->d_heavy,
                                                               c->d_ctl);
-        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, 256, 0, s>>>(
+        k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, REDUCE_THREADS, 0, s>>>(
             c->d_partials, c->G, c->d_spill, x + XCHG_HDR, c->d_len16, c->rl_max_length, nullptr,
             c->d_ctl, x, &c->d_res->replaced);
     }

@@ -992,6 +992,32 @@ __device__ __forceinline__ void add_pairs(const int32_t (&x)[4], const int32_t (
 }
 
 
+// MODE_TABLE merge passes: a chunk's pair-table slots (pair_slot) made at apply time, from the
+// chunk before the merge, and counted by the next stage's count of the same chunk whenever the
+// merge left it as it was (no rewrite: nearly every chunk).  The apply test then compares the
+// slots with the merge's own slot (4 VALU, where packing the pairs cost 8), and the count makes no
+// slot again.  A slot stands for two hot pairs (x, y) and (x ^ 1, y) (the counter's half is in
+// inc), and for a sketch dword's cold pairs: such a false hit only sends the chunk to the exact
+// apply test, which finds no match.
+struct Prep {
+    uint32_t addr[4], inc[4];
+    int32_t x3, r3;   // plane 3's pair: lane 63 of a partial chunk holds (last live slot, nx)
+    int32_t nx;       // the first live token after the chunk that r3 was made with
+    int32_t ok;       // the slots hold the chunk's current pairs (0: rewritten, or not made)
+};
+
+__device__ __forceinline__ void prep_pairs(const int32_t (&t)[4], int len, int32_t last,
+                                           int32_t nxt, const Sink &k, Prep &p) {
+    const unsigned long long P63 = (unsigned long long)((int64_t)len - CHUNK) & (1ull << 63);
+    p.x3 = sel(lane_in(P63), last, t[3]);
+    p.r3 = from_next(t[0], nxt);
+    const int32_t x[4] = {t[0], t[1], t[2], p.x3}, y[4] = {t[1], t[2], t[3], p.r3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pair_slot<false>(k, x[e], y[e], p.addr[e], p.inc[e]);
+    p.nx = nxt;
+    p.ok = 1;
+}
+
 // The fast-path pairs (x[e], y[e]) of a chunk with a side in {ma, mb, mc} (MODE_FUSED's refresh
 // of the maintained cold table): per-token membership masks (compares into lane masks,
 // combined on the scalar unit), one wave-wide test, and the LDS hash only in chunks that hold
@@ -1031,9 +1057,9 @@ __device__ __forceinline__ void refresh_pairs(const Sink &k, int32_t t0, int32_t
 // in the next region, and the fast path does not work that parity out.
 // Fast-path counts of MODE_TABLE / MODE_FUSED leave the words their adds returned in `df`, and the
 // other paths OR theirs into s.seen: the overflow screen of the ring round (screen_round).
-template <int MODE, bool TAIL = false, bool SCREEN = true>
+template <int MODE, bool TAIL = false, bool SCREEN = true, bool PREP = false>
 __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lane, Tally &s,
-                                            const Sink &k, Defer &df) {
+                                            const Sink &k, Defer &df, Prep &pp) {
     const int len = w.len;
     if (MODE == MODE_NONE && !TAIL) {
         // apply-only passes keep only the region sums: the chunk needs work only in the region's
@@ -1061,9 +1087,20 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
     // lane 63's bit when the chunk is partial (an integer mask, not a boolean: uniform booleans
     // cost a lane-mask round trip per use)
     const unsigned long long P63 = (unsigned long long)((int64_t)len - CHUNK) & (1ull << 63);
+    if (PREP && !TAIL) {
+        // the slots made at apply time (Prep): made now if the merge rewrote the chunk, plane 3
+        // made again if the first token after it changed (a merge at the next chunk's start)
+        if (!pp.ok) {
+            prep_pairs(w.t, len, w.last, nxt, k, pp);
+        } else if (pp.nx != nxt) {
+            pp.r3 = from_next(t0, nxt);
+            pair_slot<false>(k, pp.x3, pp.r3, pp.addr[3], pp.inc[3]);
+            pp.nx = nxt;
+        }
+    }
     // slot 3 of lane 63 holds the last live slot (a partial chunk's slot 255 is its tail tag)
-    const int32_t x3 = sel(lane_in(P63), w.last, t3);
-    const int32_t r3 = from_next(t0, nxt);
+    const int32_t x3 = PREP && !TAIL ? pp.x3 : sel(lane_in(P63), w.last, t3);
+    const int32_t r3 = PREP && !TAIL ? pp.r3 : from_next(t0, nxt);
     const int32_t l0 = from_prev(t3, s.prev);
     // E*: slot equals its right-hand neighbour (Em1: slot 0 equals the token before it).  No
     // dead slot equals its neighbour and slot 0 is live (an SEP next to an SEP only sends the chunk
@@ -1083,7 +1120,19 @@ __device__ __forceinline__ void count_chunk(const Chunk &w, int32_t nxt, int lan
             // one form for every chunk: 11 VALU per pair, both classes (a separate 5-VALU form
             // for chunks of hot tokens only paid off only on a fresh corpus; telling the two
             // apart cost more over a whole run: dropping it timed the C3 run 3 % faster)
-            add_pairs<MODE == MODE_FUSED, SCREEN>(x, y, k, df);
+            if (PREP) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (SCREEN) {
+                        df.o[e] = atomicAdd(lds_word(k, pp.addr[e]), pp.inc[e]);
+                        df.a[e] = pp.addr[e];
+                    } else {
+                        atomicAdd(lds_word(k, pp.addr[e]), pp.inc[e]);
+                    }
+                }
+            } else {
+                add_pairs<MODE == MODE_FUSED, SCREEN>(x, y, k, df);
+            }
             if (MODE == MODE_FUSED) refresh_pairs<MODE>(k, t0, t1, t2, x3, r3, x, y);
         } else if (MODE == MODE_EXACT) {
 #pragma unroll
@@ -1219,11 +1268,11 @@ __device__ __forceinline__ void tag_tail(int32_t (&y)[4], int total, int32_t las
 // Applies the merge (a, b) -> c to one pre-merge chunk (w.len > 0) at chunk index c of the region,
 // in place: nxt = the first pre-merge live token after it (the next region's first for the last
 // chunk).  A touched chunk is re-packed and written back.
-template <int MERGE>
+template <int MERGE, bool PREP = false>
 __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, int32_t mb,
                                             int32_t mc,
                                             const __amdgpu_buffer_rsrc_t rs, int c, int lane,
-                                            Apply &ap) {
+                                            Apply &ap, Prep &pp, uint32_t akey) {
 #ifdef BPE_PROBE_NOAPPLY
     if (lane >= 0) {   // (timing probe only: no merge detection or rewrite)
         ap.prev = w.last;
@@ -1238,13 +1287,19 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
     // (Testing for `a` alone, four compares instead of eight VALU, timed 2 % slower on C3 and zipf
     // C3: a chunk holding `a` without (a, b) then pays the full test; profiles/r05_ab_acheck.txt.)
     {
-        const int32_t r3 = from_next(w.t[0], nxt);
-        const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
-        const int32_t x3 = sel(lane_in(P63), w.last, w.t[3]);
-        const uint32_t key = pack_pair_s(ma, mb);
-        const unsigned long long H =
-            __ballot(pack_pair(w.t[0], w.t[1]) == key) | __ballot(pack_pair(w.t[1], w.t[2]) == key) |
-            __ballot(pack_pair(w.t[2], w.t[3]) == key) | __ballot(pack_pair(x3, r3) == key);
+        unsigned long long H;
+        if (PREP) {
+            // (the chunk's pair-table slots, made by prep_pairs: a slot equal to the merge's own)
+            H = __ballot(pp.addr[0] == akey) | __ballot(pp.addr[1] == akey) |
+                __ballot(pp.addr[2] == akey) | __ballot(pp.addr[3] == akey);
+        } else {
+            const int32_t r3 = from_next(w.t[0], nxt);
+            const unsigned long long P63 = (unsigned long long)((int64_t)w.len - CHUNK) & (1ull << 63);
+            const int32_t x3 = sel(lane_in(P63), w.last, w.t[3]);
+            const uint32_t key = pack_pair_s(ma, mb);
+            H = __ballot(pack_pair(w.t[0], w.t[1]) == key) | __ballot(pack_pair(w.t[1], w.t[2]) == key) |
+                __ballot(pack_pair(w.t[2], w.t[3]) == key) | __ballot(pack_pair(x3, r3) == key);
+        }
         unsigned long long T = H | (unsigned long long)(uint32_t)ap.match;
         // (X X merges also carry the run parity while the chunk ends in `a`)
         if (MERGE == MERGE_XX) T |= (unsigned long long)(uint32_t)(w.last == ma);
@@ -1319,6 +1374,7 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
         ap.n_match += (uint32_t)(__popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3));
         w.len = total;
         w.last = last;
+        pp.ok = 0;   // (the count makes the rewritten chunk's slots)
 #ifdef BPE_PROBE_COMMON
         }
 #endif
@@ -1485,8 +1541,17 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         // modes read it again (the maintained state's pass timed 2.6 % slower with the hand-on;
         // profiles/r05_ab_first_handon.txt)
         int32_t pf = 0;
+        // MODE_TABLE merge passes: each chunk's pair-table slots made at apply time (Prep), and the
+        // merge's own slot, to test against them
+        constexpr bool PREP = MODE == MODE_TABLE && MERGE != NO_MERGE;
+        uint32_t akey = 0;
+        if (PREP) {
+            uint32_t a0, i0;
+            pair_slot<false>(k, ma, mb, a0, i0);
+            akey = (uint32_t)__builtin_amdgcn_readfirstlane((int)a0);
+        }
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
-                         Defer &df) __attribute__((always_inline)) {
+                         Defer &df, Prep &pcur, Prep &pprv) __attribute__((always_inline)) {
             load(fre, c + LEAD);
             const int32_t f_next = bcast(nxt_slot.t[0], 0);
             if (c < nc) {
@@ -1498,14 +1563,16 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 cur.len = 0;
                 cur.last = NONE;
             }
-            if (MERGE && cur.len)
-                apply_chunk<MERGE>(cur,
-                                   live_from(c + 1, MODE == MODE_TABLE ? f_next : bcast(nxt_slot.t[0], 0)),
-                                   ma, mb, mc, rs, c, lane, ap);
+            if (MERGE && cur.len) {
+                const int32_t nx = live_from(c + 1, MODE == MODE_TABLE ? f_next : bcast(nxt_slot.t[0], 0));
+                if (PREP) prep_pairs(cur.t, cur.len, cur.last, nx, k, pcur);
+                apply_chunk<MERGE, PREP>(cur, nx, ma, mb, mc, rs, c, lane, ap, pcur, akey);
+            }
             if (cur.len) {
-                if (prv.len) count_chunk<MODE, false, SCREEN>(prv, cur.first, lane, s, k, df);
+                if (prv.len) count_chunk<MODE, false, SCREEN, PREP>(prv, cur.first, lane, s, k, df, pprv);
             } else {
                 cur = prv;   // rare: hand the pending chunk on
+                if (PREP) pcur = pprv;
             }
             // (prv kept live past the hand-on's merge of two register sets, so the register
             // allocator gives the merged chunk cur's registers and puts the copies on the rare
@@ -1518,6 +1585,8 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         };
         if (nc > 0) {
             Chunk S[RING];   // (constant indices only: the ring stays in registers)
+            Prep P[RING];
+            static_for<0, RING>([&](auto i) __attribute__((always_inline)) { P[i].ok = 0; });
             static_for<0, LEAD>([&](auto i) __attribute__((always_inline)) { load(S[i], i); });
             S[RING - 1].len = 0;
             pf = bcast(S[0].t[0], 0);
@@ -1534,12 +1603,13 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
                 static_for<0, RING>([&](auto I) __attribute__((always_inline)) {
                     constexpr int i = decltype(I)::value;
                     stage(S[i], S[(i + 1) % RING], S[(i + RING - 1) % RING],
-                          S[(i + LEAD) % RING], c + i, D[i]);
+                          S[(i + LEAD) % RING], c + i, D[i], P[i], P[(i + RING - 1) % RING]);
                 });
                 screen_round();
             }
             Defer dt;   // (the region's last chunk takes the exact path: s.seen)
-            if (S[RING - 1].len) count_chunk<MODE, true, SCREEN>(S[RING - 1], NONE, lane, s, k, dt);
+            if (S[RING - 1].len)
+                count_chunk<MODE, true, SCREEN>(S[RING - 1], NONE, lane, s, k, dt, P[RING - 1]);
             screen_round();
         }
         if (lane == 0) {
@@ -1773,22 +1843,31 @@ __device__ __forceinline__ bool pair_ok(int32_t a, int32_t b, const int32_t *len
                                         int64_t max_length);
 
 // A block owns 128 dwords (256 bins): 32 lanes x 4 dwords (512 contiguous bytes of a slab per
-// lane group), each of its 8 lane groups summing every 8th slab with eight 16-B loads in flight.
-// (Narrower column tiles, reading many slabs per wave-instruction, ran 2-3x slower.)
-__global__ void __launch_bounds__(256)
+// lane group), each of its REDUCE_GROUPS lane groups summing every REDUCE_GROUPS-th slab with up to
+// 16 16-B loads in flight.  (Narrower column tiles, reading many slabs per wave-instruction, ran
+// 2-3x slower.)  The slabs were just written (MALL-resident): the kernel is latency-bound, so the
+// lane groups are many (more waves per CU hiding the loads' latency) rather than few with deep
+// chains of loads.
+#ifndef BPE_REDUCE_GROUPS
+#define BPE_REDUCE_GROUPS 8
+#endif
+constexpr int REDUCE_GROUPS = BPE_REDUCE_GROUPS;
+constexpr int REDUCE_THREADS = 32 * REDUCE_GROUPS;
+static_assert(REDUCE_THREADS >= 256 && REDUCE_THREADS <= 1024, "reduce block");
+__global__ void __launch_bounds__(REDUCE_THREADS)
 k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long *__restrict__ spill,
                unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
                int64_t max_length, Result *res, const LoopCtl *ctl,
                unsigned long long *__restrict__ hdr = nullptr,
                const unsigned long long *__restrict__ rep = nullptr) {
-    __shared__ uint32_t s_sum[8][32][8];
+    __shared__ uint32_t s_sum[REDUCE_GROUPS][32][8];
     if (loop_off(ctl)) return;
     const int t = threadIdx.x;
     // (sharded: the exchange header carries this shard's replacement count, summed with the table)
     if (hdr && rep && blockIdx.x == 0 && t == 0) hdr[0] = *rep;
     const int wl = t & 31, grp = t >> 5;
     const int w0 = blockIdx.x * REDUCE_WORDS_PER_BLOCK + 4 * wl;   // first of my 4 words
-    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                 // < 2^23 each: G <= 256 x 2^15
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // < 2^24 each: G <= 256 slabs x halves < 2^16
     const uint4 *p4 = reinterpret_cast<const uint4 *>(partials + w0);
     auto add = [&](const uint4 p) {
         acc[0] += p.x & 0xFFFFu;
@@ -1800,47 +1879,48 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         acc[6] += p.w & 0xFFFFu;
         acc[7] += p.w >> 16;
     };
+    constexpr int RG = REDUCE_GROUPS;
     int g = grp;
-    // 16 slab loads in flight per thread (the slabs were just written: latency-bound, not
-    // bandwidth-bound)
-    for (; g + 120 < G; g += 128) {
+    for (; g + 15 * RG < G; g += 16 * RG) {
         uint4 p[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) p[q] = p4[(size_t)(g + 8 * q) * (HIST_WORDS / 4)];
+        for (int q = 0; q < 16; ++q) p[q] = p4[(size_t)(g + RG * q) * (HIST_WORDS / 4)];
 #pragma unroll
         for (int q = 0; q < 16; ++q) add(p[q]);
     }
-    for (; g + 56 < G; g += 64) {
+    for (; g + 7 * RG < G; g += 8 * RG) {
         uint4 p[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) p[q] = p4[(size_t)(g + 8 * q) * (HIST_WORDS / 4)];
+        for (int q = 0; q < 8; ++q) p[q] = p4[(size_t)(g + RG * q) * (HIST_WORDS / 4)];
 #pragma unroll
         for (int q = 0; q < 8; ++q) add(p[q]);
     }
-    for (; g < G; g += 8) add(p4[(size_t)g * (HIST_WORDS / 4)]);
+    for (; g < G; g += RG) add(p4[(size_t)g * (HIST_WORDS / 4)]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s_sum[grp][wl][i] = acc[i];
     __syncthreads();
-    // thread t finalises bin 2*w0' + i for one (word-lane, i) pair: 256 threads, 256 bins
-    const int bl = t >> 3, bi = t & 7;
-    uint32_t sum = 0;
+    // thread t < 256 finalises bin 2*w0' + i for one (word-lane, i) pair: 256 bins
+    unsigned long long k = 0, vm = 0;
+    if (t < 256) {
+        const int bl = t >> 3, bi = t & 7;
+        uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) sum += s_sum[q][bl][bi];
-    // dword w holds bins 2w and 2w + 1 (hot pairs and sketch buckets alike): contiguous writes
-    const int bin = blockIdx.x * (2 * REDUCE_WORDS_PER_BLOCK) + t;
-    const unsigned long long v = (unsigned long long)sum + spill[bin];
-    table[bin] = v;
-    spill[bin] = 0;
-    unsigned long long k = 0;
-    if (bin < HOT_BINS && v && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
-        k = pack_key(v, bin_a(bin), bin_b(bin));
-    // one atomic per workgroup (a wave each would queue over a thousand on one address)
+        for (int q = 0; q < RG; ++q) sum += s_sum[q][bl][bi];
+        // dword w holds bins 2w and 2w + 1 (hot pairs and sketch buckets alike): contiguous writes
+        const int bin = blockIdx.x * (2 * REDUCE_WORDS_PER_BLOCK) + t;
+        const unsigned long long v = (unsigned long long)sum + spill[bin];
+        table[bin] = v;
+        spill[bin] = 0;
+        if (bin < HOT_BINS && v && pair_ok(bin_a(bin), bin_b(bin), len16, max_length))
+            k = pack_key(v, bin_a(bin), bin_b(bin));
+        vm = v;
+    }
+    // one atomic per workgroup (a wave each would queue over a thousand on one address); and the
+    // largest bin of all, hot and sketch alike: the next decision's bound, LoopCtl::unscreened
     k = wave_max_u64(k);
-    // (and the largest bin of all, hot and sketch alike: the next decision's bound, LoopCtl::
-    // unscreened)
-    unsigned long long vm = wave_max_u64(v);
+    vm = wave_max_u64(vm);
     __shared__ unsigned long long s_best[4], s_vmax[4];
-    if ((t & 63) == 0) {
+    if ((t & 63) == 0 && t < 256) {
         s_best[t >> 6] = k;
         s_vmax[t >> 6] = vm;
     }

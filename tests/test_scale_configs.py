@@ -166,14 +166,17 @@ def test_config5_eight_shards_vs_one_context_and_cpu_restatement():
     assert got[:3] == want
 
 
-def test_config5_shard_to_the_32k_vocabulary():
-    """One GPU's C5 shard (2 GiB, the first 2 GiB of the C5 stream) to the 32k-token vocabulary
-    (32512 merges: most of them in the maintained state, MODE_INCR); the first merges against the
-    restatement, the final state's next merge against a recount from scratch of the corpus read
-    back from HBM, tokens conserved."""
+def test_config5_shard_to_the_32k_vocabulary_stream_and_incremental():
+    """One GPU's C5 shard (2 GiB, the first 2 GiB of the C5 stream; 2^31 + 2048 slots) to the
+    32k-token vocabulary (32512 merges).  The streaming mode (most merges in the maintained state,
+    MODE_INCR): the first merges against the restatement, the final state's next merge against a
+    recount from scratch of the corpus read back from HBM, tokens conserved.  Then the incremental
+    mode on a second copy (positions past 2^31): every merge on the position index, the same merges
+    and corpus as the streaming mode's (one streaming run serves both checks)."""
     n = 2 << 30
     data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
     e, cmap, nt = engine(data)
+    e2, _, _ = engine(data)
     cpu = CpuMT.from_latin1(data, SAMPLE, cmap, nt, threads=host_threads(), extra=64)
     del data
     want = cpu.merge_until(0, 2, 3)
@@ -186,30 +189,15 @@ def test_config5_shard_to_the_32k_vocabulary():
     assert e.corpus_size()[1] == n - sum(m[2] for m in got)
     ids, off = e.read_corpus()
     cpu = CpuMT(ids, off, [1] * 32768, 32768, threads=host_threads())
-    del ids
     nxt = cpu.find_next_merge(0, 2)
     cpu.close()
     assert e.find_next_merge(0, 2) == nxt
     e.close()
-
-
-def test_config5_shard_to_the_32k_vocabulary_incremental():
-    """The same 2 GiB C5 shard (2^31 + 2048 slots: positions past 2^31) to the 32k-token vocabulary
-    in the incremental mode: every merge on the position index, the same merges and corpus as the
-    streaming mode."""
-    n = 2 << 30
-    data = pkg.synth_latin1(n, seed=12345, A=256, base=0)
-    e, cmap, nt = engine(data)
-    e2, _, _ = engine(data)
-    del data
-    want = e.merge_until(0, 2, 32768 - nt)
-    ids1, off1 = e.read_corpus()
-    e.close()
     e2.set_mode('incremental')
-    got = e2.merge_until(0, 2, 32768 - nt)
-    st = e2.stats()
-    assert got == want
-    assert st['pix_merges'] >= len(want) - 64 * (st['pix_host'] + 1), st
-    ids, off = e2.read_corpus()
-    assert np.array_equal(ids, ids1) and np.array_equal(off, off1)
+    got2 = e2.merge_until(0, 2, 32768 - nt)
+    st2 = e2.stats()
+    assert got2 == got
+    assert st2['pix_merges'] >= len(got) - 64 * (st2['pix_host'] + 1), st2
+    ids2, off2 = e2.read_corpus()
+    assert np.array_equal(ids2, ids) and np.array_equal(off2, off)
     e2.close()

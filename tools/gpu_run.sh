@@ -48,7 +48,7 @@ for step in "$@"; do
     ( while sleep 50; do date +%T >> "$OUT/heartbeat"; done ) & HB=$!
     # (RCCL's warnings to a file: a communicator that fails to come up leaves its reason there)
     export NCCL_DEBUG=${NCCL_DEBUG:-WARN} NCCL_DEBUG_FILE=${NCCL_DEBUG_FILE:-$PWD/$OUT/nccl.%p.log}
-    timeout -k 10 1100 python3 -u -m pytest ${PYTEST_PATHS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -v \
+    timeout -k 10 1100 python3 -u -m pytest ${PYTEST_PATHS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -v --durations=40 \
         --maxfail=5 --timeout 400 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
     rc=$?; kill $HB 2>/dev/null
     [ $rc -eq 0 ] || fail tests "$OUT/pytest_gpu.log"
