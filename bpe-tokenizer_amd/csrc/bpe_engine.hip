@@ -1422,7 +1422,7 @@ int rank_loop_count(bpe_ctx *c) {
                                                               c->d_ctl);
         k_reduce_table<<<HIST_WORDS / REDUCE_WORDS_PER_BLOCK, REDUCE_THREADS, 0, s>>>(
             c->d_partials, c->G, c->d_spill, x + XCHG_HDR, c->d_len16, c->rl_max_length, nullptr,
-            c->d_ctl, x, &c->d_res->replaced);
+            c->d_ctl, x, &c->d_res->replaced, &c->d_res->bin_max);
     }
     HIP_TRY(hipGetLastError());
     c->rl_enqueued += 1;

@@ -65,6 +65,7 @@ static_assert(WAVES_PER_WG * RING * 256 < 49152,
 #endif
 constexpr int LEAD = BPE_LEAD;
 static_assert(LEAD >= 2 && LEAD <= RING - 2, "load lead");
+
 // Cache-policy bits of the streaming passes' corpus loads (buffer_load aux: 0 plain, 2 nt).  A
 // pass streams 4 GB, far past the caches, so the loads are non-temporal: 6.15 -> 7.0 TB/s for
 // this access pattern (tools/probe/stream_probe2.hip), k_step 2.6 % faster.
@@ -210,8 +211,9 @@ struct LoopCtl {
     // grows by a merge (a b -> c only removes occurrences of pairs next to a or b, and runs of X
     // only shrink), the new pairs (x, c) and (c, y) number W each at most, and a workgroup's LDS
     // count of a bin is at most the bin's count over the whole corpus (pairs across regions go
-    // to the spill; a run's segments count at most the run's floor(L / 2)).  0 (screened) for a
-    // sharded rank, the maintained state and the first pass of a batch.
+    // to the spill; a run's segments count at most the run's floor(L / 2)).  A sharded rank bounds
+    // its own shard's counts with its own largest bin and the global W (W >= the shard's count of
+    // the pair).  0 (screened) in the maintained state and for the first pass of a batch.
     int32_t unscreened;
     int32_t n_unscreened;   // decisions that set it, in this batch
 };
@@ -1550,6 +1552,9 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
             pair_slot<false>(k, ma, mb, a0, i0);
             akey = (uint32_t)__builtin_amdgcn_readfirstlane((int)a0);
         }
+        // (the stage waits for chunk c + 1's load at its start: chunk c's merge test needs its
+        // first token.  Loading slot 0 of every chunk on its own a stage earlier, so that a stage
+        // waits only for loads issued two stages back, timed the same: profiles/r06_ab_early.txt)
         auto stage = [&](Chunk &cur, const Chunk &nxt_slot, Chunk &prv, Chunk &fre, int c,
                          Defer &df, Prep &pcur, Prep &pprv) __attribute__((always_inline)) {
             load(fre, c + LEAD);
@@ -1859,7 +1864,8 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
                unsigned long long *__restrict__ table, const int32_t *__restrict__ len16,
                int64_t max_length, Result *res, const LoopCtl *ctl,
                unsigned long long *__restrict__ hdr = nullptr,
-               const unsigned long long *__restrict__ rep = nullptr) {
+               const unsigned long long *__restrict__ rep = nullptr,
+               unsigned long long *__restrict__ bin_max = nullptr) {
     __shared__ uint32_t s_sum[REDUCE_GROUPS][32][8];
     if (loop_off(ctl)) return;
     const int t = threadIdx.x;
@@ -1925,13 +1931,16 @@ k_reduce_table(const uint32_t *__restrict__ partials, int G, unsigned long long 
         s_vmax[t >> 6] = vm;
     }
     __syncthreads();
-    if (t == 0 && res) {
+    // (bin_max: where the largest bin goes, res->bin_max by default; a sharded rank's reduce has no
+    // Result to select from, but its own largest bin bounds its own next pass alike)
+    if (!bin_max && res) bin_max = &res->bin_max;
+    if (t == 0 && (res || bin_max)) {
         for (int w = 1; w < 4; ++w) {
             k = s_best[w] > k ? s_best[w] : k;
             vm = s_vmax[w] > vm ? s_vmax[w] : vm;
         }
-        if (k) atomicMax(&res->best, k);
-        atomicMax(&res->bin_max, vm + 1);
+        if (k && res) atomicMax(&res->best, k);
+        if (bin_max) atomicMax(bin_max, vm + 1);
     }
 }
 
@@ -2505,7 +2514,7 @@ __device__ void decide_commit(LoopCtl *ctl, Result *res, const LoopCtl &C, long 
     ctl->next_id = c + 1;
     ctl->n_done = i + 1;
     const unsigned long long bm = res->bin_max;
-    const int32_t uns = !C.sharded && !C.maintained && bm &&
+    const int32_t uns = !C.maintained && bm &&
                         (bm - 1) + 2 * (unsigned long long)W < 0x10000ull;
     ctl->unscreened = uns;
     ctl->n_unscreened = C.n_unscreened + uns;

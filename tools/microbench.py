@@ -58,6 +58,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(steps):
         m = e.find_next_merge(0, 2)
+        if m is None:   # (a timing-probe build that counts nothing)
+            break
         e.apply_merge(m[0], m[1], n_tokens)
         n_tokens += 1
     dt = time.perf_counter() - t0
@@ -68,10 +70,11 @@ def main():
         'recount_ms': rc['step_ms'] / max(1, rc['step_timed']),
         'recount_GBps_alg': 4 * live / (rc['step_ms'] / max(1, rc['step_timed']) * 1e-3) / 1e9,
         'merge_pass_ms': st['step_ms'] / max(1, st['step_timed']),
-        'merge_pass_GBps_alg': 4 * st['step_live'] / max(1, st['step_launches']) /
-                               (st['step_ms'] / max(1, st['step_timed']) * 1e-3) / 1e9,
-        'select_ms_per_iter': st['select_ms'] / steps,
-        'wall_ms_per_iter': dt * 1e3 / steps,
+        'merge_pass_GBps_alg': (4 * st['step_live'] / max(1, st['step_launches']) /
+                                (st['step_ms'] / max(1, st['step_timed']) * 1e-3) / 1e9
+                                if st['step_ms'] else None),
+        'select_ms_per_iter': st['select_ms'] / max(1, steps),
+        'wall_ms_per_iter': dt * 1e3 / max(1, steps),
         'tie_passes': st['tie_passes'], 'exact_passes': st['exact_passes'], 'compactions': st['compactions'],
     }
     print(json.dumps(out))
