@@ -21,6 +21,11 @@ hipError_t launch_step_loop_table(unsigned grid, hipStream_t s, int32_t *ids, in
                                   int64_t cpr, int R, const void *carry, const void *ctl,
                                   uint32_t *partials, unsigned long long *spill, const void *ct,
                                   void *sums, unsigned long long *replaced);
+hipError_t launch_step_table(int merge, unsigned grid, hipStream_t s, int32_t *ids, int64_t n_chunks,
+                             int64_t cpr, int R, const void *carry, int32_t ma, int32_t mb,
+                             int32_t mc, uint32_t *partials, unsigned long long *spill,
+                             const void *ct, const uint32_t *heavy, void *sums,
+                             unsigned long long *replaced);
 }
 
 #include <algorithm>
@@ -562,18 +567,12 @@ int run_pass(bpe_ctx *c, bool merge, int32_t a, int32_t b, int32_t cc, int64_t *
         k_step<MERGE_XY, MODE_FUSED><<<c->G, WG, 0, s>>>(
             c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
             c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
-    else if (merge && a == b)
-        k_step<MERGE_XX, MODE_TABLE><<<c->G, WG, 0, s>>>(
-            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
-            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
-    else if (merge)
-        k_step<MERGE_XY, MODE_TABLE><<<c->G, WG, 0, s>>>(
-            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, a, b, cc, c->d_partials, c->d_spill,
-            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
     else
-        k_step<NO_MERGE, MODE_TABLE><<<c->G, WG, 0, s>>>(
-            c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry, -1, -1, -1, c->d_partials, c->d_spill,
-            c->cold, c->d_heavy, c->d_sums, &c->d_res->replaced);
+        HIP_TRY(bpe_step::launch_step_table(!merge ? NO_MERGE : a == b ? MERGE_XX : MERGE_XY, c->G,
+                                            s, c->d_ids, c->n_chunks, c->cpr, c->R, c->d_carry,
+                                            merge ? a : -1, merge ? b : -1, merge ? cc : -1,
+                                            c->d_partials, c->d_spill, &c->cold, c->d_heavy,
+                                            c->d_sums, &c->d_res->replaced));
     HIP_TRY(hipGetLastError());
     if ((rc = span_end(c, e_step, 0))) return rc;
     hipEvent_t e_red = span_begin(c);

@@ -34,4 +34,29 @@ hipError_t launch_step_loop_table(unsigned grid, hipStream_t s, int32_t *ids, in
     return hipGetLastError();
 }
 
+// The host path's passes of the table state (findNextMerge / applyMerge one call each, the counts
+// after a compaction, core.ts:247-360): k_step<NO_MERGE | MERGE_XY | MERGE_XX, MODE_TABLE>, built
+// here with the same flags as the device loop's pass (in the engine's translation unit, with its
+// 6-slot ring and default flags, the merge pass timed 0.80-0.82 ms at C3 against 0.74 here).
+hipError_t launch_step_table(int merge, unsigned grid, hipStream_t s, int32_t *ids, int64_t n_chunks,
+                             int64_t cpr, int R, const void *carry, int32_t ma, int32_t mb,
+                             int32_t mc, uint32_t *partials, unsigned long long *spill,
+                             const void *ct, const uint32_t *heavy, void *sums,
+                             unsigned long long *replaced) {
+    using namespace bpe;
+    const RegionCarry *rc = static_cast<const RegionCarry *>(carry);
+    const ColdTable &t = *static_cast<const ColdTable *>(ct);
+    RegionSum *su = static_cast<RegionSum *>(sums);
+    if (merge == MERGE_XX)
+        k_step<MERGE_XX, MODE_TABLE><<<grid, WG, 0, s>>>(ids, n_chunks, cpr, R, rc, ma, mb, mc,
+                                                        partials, spill, t, heavy, su, replaced);
+    else if (merge == MERGE_XY)
+        k_step<MERGE_XY, MODE_TABLE><<<grid, WG, 0, s>>>(ids, n_chunks, cpr, R, rc, ma, mb, mc,
+                                                        partials, spill, t, heavy, su, replaced);
+    else
+        k_step<NO_MERGE, MODE_TABLE><<<grid, WG, 0, s>>>(ids, n_chunks, cpr, R, rc, ma, mb, mc,
+                                                        partials, spill, t, heavy, su, replaced);
+    return hipGetLastError();
+}
+
 }  // namespace bpe_step
