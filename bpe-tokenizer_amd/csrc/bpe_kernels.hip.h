@@ -1388,7 +1388,7 @@ __device__ __forceinline__ void apply_chunk(Chunk &w, int32_t nxt, int32_t ma, i
 
 // hist: the kernel's static LDS table (so, once inlined, LDS addresses are plain constants with no
 // symbol base to add per access)
-template <int MERGE, int MODE, bool SCREEN = true>
+template <int MERGE, int MODE, bool SCREEN = true, bool SLOTS = true>
 __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ ids,
                                           int64_t n_chunks, int64_t cpr, int R,
                                           const RegionCarry *__restrict__ carry, int32_t ma,
@@ -1545,7 +1545,7 @@ __device__ __forceinline__ void step_body(uint32_t *hist, int32_t *__restrict__ 
         int32_t pf = 0;
         // MODE_TABLE merge passes: each chunk's pair-table slots made at apply time (Prep), and the
         // merge's own slot, to test against them
-        constexpr bool PREP = MODE == MODE_TABLE && MERGE != NO_MERGE;
+        constexpr bool PREP = MODE == MODE_TABLE && MERGE != NO_MERGE && SLOTS;
         uint32_t akey = 0;
         if (PREP) {
             uint32_t a0, i0;
@@ -1711,6 +1711,12 @@ k_step_loop(int32_t *__restrict__ ids, int64_t n_chunks, int64_t cpr, int R,
     else if (MODE == MODE_TABLE && ctl->unscreened)
         step_body<MERGE_XY, MODE, false>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials,
                                          spill, ct, nullptr, sums, replaced, hot_g, delta);
+    else if (MODE == MODE_TABLE && (int64_t)ctl->w * 16 >= n_chunks)
+        // a heavy merge (a skewed corpus's first merges: W in the millions, always screened)
+        // rewrites too many chunks for the apply-time slots to pay: the packed-pair test
+        step_body<MERGE_XY, MODE, true, false>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc,
+                                               partials, spill, ct, nullptr, sums, replaced, hot_g,
+                                               delta);
     else
         step_body<MERGE_XY, MODE>(hist, ids, n_chunks, cpr, R, carry, ma, mb, mc, partials, spill,
                                   ct, nullptr, sums, replaced, hot_g, delta);
