@@ -21,8 +21,9 @@
 #              texts) and tools/encode_crossover.js (JS replay vs device per call)
 #   enclat     tools/encode_latency.py (one text per call: wall and kernel time per call)
 #   profenc    rocprofv3 --kernel-trace --stats of tools/encode_bench.py (zipf)
-#   multi      8 shards of the C5 stream (512 MiB) on one device to the 32k vocabulary, streaming
-#              rank loop then incremental mode (tools/multi_pix_probe.py)
+#   multi      8 shards of the C5 stream (512 MiB) on one device to the 32k vocabulary, the mode left
+#              to the engine (auto: the stream, switching past 18 432 ids) then the incremental mode
+#              (tools/multi_pix_probe.py; MULTI_MODES="stream ..." adds the stream kept by the caller)
 #   profmulti  rocprofv3 --kernel-trace --stats of the streaming leg of `multi`
 #   profmultipix  the same for the incremental leg
 #   sqenc      SQ counter passes and FETCH_SIZE of the device encoder (tools/encode_bench.py, zipf
@@ -128,14 +129,14 @@ for step in "$@"; do
         || fail profenc "$OUT/enc.err"
     cat "$OUT/enc.jsonl"; prof_stats "$OUT/enc" ;;
   multi)
-    for mode in stream incremental; do
+    for mode in ${MULTI_MODES:-auto incremental}; do
       timeout -k 10 500 python3 -u tools/multi_pix_probe.py 512 8 32512 4096 $mode > "$OUT/multi8_$mode.jsonl" \
           2> "$OUT/multi8_$mode.err" || fail multi "$OUT/multi8_$mode.err"
       tail -2 "$OUT/multi8_$mode.jsonl"
     done ;;
   profmulti)
     BPE_MULTI_ONE_THREAD=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/multi" -o run --output-format csv \
-        -- python3 tools/multi_pix_probe.py 512 8 32512 4096 stream > "$OUT/pmulti.jsonl" 2> "$OUT/pmulti.err" \
+        -- python3 tools/multi_pix_probe.py 512 8 32512 4096 auto > "$OUT/pmulti.jsonl" 2> "$OUT/pmulti.err" \
         || fail profmulti "$OUT/pmulti.err"
     tail -2 "$OUT/pmulti.jsonl"; prof_stats "$OUT/multi" ;;
   profmultipix)

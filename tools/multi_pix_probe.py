@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Progress of a sharded run on one device (shards exchanging through the device kernel): the C5
 stream over S shards merged in chunks, printing per chunk the time, the index entries (builds),
-hand-offs and merges on the index, for the streaming or the incremental mode.
-Usage: python tools/multi_pix_probe.py MiB shards merges chunk [stream|incremental]"""
+hand-offs and merges on the index, for the streaming or the incremental mode.  auto: the mode left
+to the engine (the stream, switching to the incremental mode past BPE_AUTO_PIX_VOCAB ids); stream:
+the stream set by the caller, which the engine keeps (no switch).
+Usage: python tools/multi_pix_probe.py MiB shards merges chunk [auto|stream|incremental]"""
 import importlib
 import json
 import os
@@ -21,7 +23,8 @@ def main():
     e = pkg.Engine(devices=[0] * shards, reduce='host')
     _, nt, _ = e.add_latin1(data, sample_bytes=1 << 20)
     del data
-    e.set_mode(mode)
+    if mode != 'auto':
+        e.set_mode(mode)
     e.stats_enable(True)
     done = 0
     prev = (0, 0)
